@@ -1,0 +1,212 @@
+"""Benchmark: PDHG iterations/s on the north-star grid (BASELINE.json) on 1..N MI355X.
+
+Workload (N = 1): configs[3] of BASELINE.json run on one GPU — egno 2, ndim 2, epsl 0.1,
+nx = ny = 4096, nt = 201 as ONE PDHG window of T = nt - 1 = 200 unknown time rows
+(time_step_per_PDHG = nt), rho_alp_iters = 1 (the fused-sweep headline),
+fp32 state resident in HBM, reference initial state (phi = g, rho = 70, alp = 0;
+utils_pdhg_solver.py:123-137).  One "step" = one outer PDHG iteration
+(utils_pdhg_solver.py:51-88): primal (residual + H1 preconditioner + update), extrapolation,
+dual (alpha/rho prox), err1/err2 and the device-side stop tests.
+
+N > 1 (launched by torch.distributed.run): one process per GPU.  The t-slab sharding of one
+window is not built yet, so every rank runs an independent replica of the same window
+("replicas", weak scaling); value = sum of the ranks' iterations / max-over-ranks time.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "pdhg-optimal-control_amd"))
+
+import numpy as np  # noqa: E402
+
+METRIC = "PDHG iterations/sec and achieved HBM GB/s on nt×nx[×ny] grid, 1/2/4/8 MI355X"
+HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+CONFIGS = {
+    # name: (egno, ndim, epsl, nx, ny, nt)
+    "c3": (2, 2, 0.1, 4096, 4096, 201),
+    "c2": (1, 2, 0.0, 2048, 2048, 101),
+    "c1": (1, 1, 0.0, 65536, 1, 401),
+    "c0": (1, 1, 0.0, 160, 1, 41),
+}
+
+
+def grid(ndim, nx, ny):
+    x1 = np.linspace(0.0, 2.0, num=nx, endpoint=False)
+    if ndim == 1:
+        return x1, None
+    return x1, np.linspace(0.0, 2.0, num=ny, endpoint=False)
+
+
+def cpu_baseline(cfg, T_sample, threads):
+    """The float64 oracle (restatement of the reference, labelled 'port') on a bounded sample:
+    the full nx x ny plane with T_sample unknown rows; extrapolated linearly to the full T."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    os.environ["ORACLE_FFT_WORKERS"] = str(threads)
+    import pdhg_oracle as O
+    egno, ndim, epsl, nx, ny, nt = cfg
+    T = nt - 1
+    x_arr = O.make_grid(ndim, nx, ny, egno)
+    bc = O.default_bc(egno, ndim)
+    fns = O.set_up_example_fns(egno, ndim, 0)
+    g = O.set_up_J(egno, ndim, (2.0, 2.0))(x_arr)
+    dt = 1.0 / (nt - 1)
+    dsp = (2.0 / nx,) if ndim == 1 else (2.0 / nx, 2.0 / ny)
+    nsp = (nx,) if ndim == 1 else (nx, ny)
+    fv = O.compute_Dxx_fft_fv(ndim, nsp, dsp, bc)
+    primal, dual = O.make_update_fns(ndim, bc, rho_alp_iters=1)
+    phi = np.repeat(g, T_sample + 1, axis=0)
+    rho = np.full((T_sample,) + nsp, 70.0)
+    nctrl = ndim
+    alp = tuple(np.zeros((T_sample,) + nsp + (nctrl,)) for _ in range(2 if ndim == 1 else 4))
+
+    def one():
+        nonlocal phi, rho, alp
+        phi_n = primal(phi, rho, 70.0, alp, 0.1 / 1.5, dt, dsp, fns, fv, epsl, x_arr, None)
+        rho_n, alp_n = dual(2 * phi_n - phi, rho, 70.0, alp, 0.15, dt, dsp, epsl, fns, x_arr, None, ndim, 1e-6)
+        O.outer_errors(phi, phi_n, rho, rho_n, alp, alp_n)
+        phi, rho, alp = phi_n, rho_n, alp_n
+
+    one()                      # warm-up
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        one()
+        reps += 1
+        el = time.perf_counter() - t0
+        if el > 8.0 or reps >= 5:
+            break
+    per_it = el / reps
+    pts_per_s = T_sample * np.prod(nsp) / per_it
+    full_pts = T * np.prod(nsp)
+    return {"value": float(pts_per_s / full_pts), "unit": "it/s", "cores": threads, "kind": "port",
+            "sample": "float64 NumPy/SciPy oracle (restatement of the JAX reference, which cannot run here), "
+                      "{} x {} plane with T'={} of T={} rows, {} iterations in {:.1f}s, it/s extrapolated "
+                      "linearly in T; scipy.fft workers={}, NumPy elementwise single-threaded".format(
+                          nx, ny, T_sample, T, reps, el, threads)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--rho-alp-iters", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-T", type=int, default=2)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl")
+        dist = tdist
+
+    from pdhg_amd.context import PDHGContext
+
+    egno, ndim, epsl, nx, ny, nt = CONFIGS[args.config]
+    T = nt - 1
+    k = args.rho_alp_iters
+    xs, ys = grid(ndim, nx, ny)
+    dt = 1.0 / (nt - 1)
+    ctx = PDHGContext(egno, ndim, nx, ny, T, 2.0 / nx, 2.0 / ny if ndim == 2 else 0.0, dt, xs, ys, epsl=epsl,
+                      precision="fp32", rho_alp_iters=k, device=local_rank if world > 1 else 0)
+    if ndim == 1:
+        g = np.sin(np.pi * xs)
+    else:
+        g = np.sin(np.pi * xs)[:, None] + np.sin(np.pi * ys)[None, :]
+    ctx.init_state(g)
+    # epsl = 0.1 on a 4096^2 grid is outside the reference algorithm's stability range (explicit
+    # sigma*epsl*Lap in the dual; its fp64 restatement diverges already at 256^2): keep executing
+    # exactly the requested iterations after the state goes non-finite, and report it.
+    ctx.set_stop_rules(converge=True, nan=False)
+    tau, sigma = 0.1 / 1.5, 0.1 * 1.5
+    eps = 1e-6
+
+    if args.warmup > 0:
+        ctx.iterate(args.warmup, tau, sigma, eps, k)
+    ctx.synchronize()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    ctx.profile_enable(True)
+    barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    st = ctx.iterate(args.steps, tau, sigma, eps, k)
+    ctx.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    iters = st["iters_run"]
+    if dist is not None:
+        import torch
+        t = torch.tensor([el, float(iters)], dtype=torch.float64, device="cuda")
+        tmax = t.clone()
+        dist.all_reduce(tmax[0:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:2], op=dist.ReduceOp.SUM)
+        el_max, iters_total = float(tmax[0]), int(t[1])
+    else:
+        el_max, iters_total = el, iters
+
+    # per-kernel live timing (HIP events on the context's stream)
+    kern = {}
+    for cls in ("residual", "precond", "update", "dual"):
+        ms, n = ctx.profile_query(cls)
+        if n:
+            kern[cls] = {"avg_ms": ms / n, "launches": n, "bytes_per_launch": ctx.algorithmic_bytes(k, cls)}
+    ctx.profile_enable(False)
+    dom = max(kern, key=lambda c: kern[c]["avg_ms"] * kern[c]["launches"])
+    d = kern[dom]
+    achieved = d["bytes_per_launch"] / (d["avg_ms"] * 1e-3) / 1e9
+    it_bytes = ctx.algorithmic_bytes(k, "iteration")
+    ms_per_step = el_max / max(iters, 1) * 1e3
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    out = {
+        "metric": METRIC,
+        "value": iters_total / el_max,
+        "unit": "it/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (reference initial state phi=g, rho=70, alp=0)",
+        "config": {"workload": "egno{} ndim{} epsl{} nx={} ny={} nt={}: one PDHG window of T={} rows, "
+                               "rho_alp_iters={}".format(egno, ndim, epsl, nx, ny, nt, T, k),
+                   "parallelism": "replicas" if world > 1 else "single GPU",
+                   "iters_executed": iters, "stop_status": st["status"], "state_nonfinite": bool(st["nan_seen"])},
+        "hbm_gbps_iteration": it_bytes / (ms_per_step * 1e-3) / 1e9,
+        "iteration_bytes": it_bytes,
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None},
+        "kernels": kern,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        threads = min(16, os.cpu_count() or 1)
+        sample_cfg = CONFIGS[args.config]
+        out["cpu_baseline"] = cpu_baseline(sample_cfg, args.cpu_sample_T if ndim == 2 else 8, threads)
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

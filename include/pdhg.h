@@ -1,0 +1,156 @@
+/*
+ * pdhg.h — C ABI of the MI355X-native PDHG iteration for Hamilton–Jacobi
+ * optimal-control PDEs (drop-in for the hot path of
+ * TingweiMeng/PDHG-optimal-control, jaxsrc/).
+ *
+ * Plain C types only: host pointers + sizes, an opaque context that owns all
+ * device (HBM) memory.  Bound from Python with ctypes by
+ * pdhg-optimal-control_amd/pdhg_amd/_native.py; any other FFI (cffi, a C++
+ * caller) can bind the same symbols.  See INTEGRATION.md.
+ *
+ * Reference interfaces replaced (file:line in jaxsrc/):
+ *   pdhg_create              problem setup done by solve_HJ            run_example.py:157-191
+ *                            + set_up_example_fns / compute_Dxx_fft_fv set_fns.py:52-166, utils/utils_precond.py:42-71
+ *   pdhg_set_state/get_state the (phi, rho, alp) arrays passed between the jitted updates
+ *                                                                       utils/utils_pdhg_solver.py:48-50, 96-98 (returns)
+ *   pdhg_update_primal       update_primal_1d / update_primal_2d      update_fns_in_pdhg.py:135-147
+ *                            (+ phi_bar = 2 phi' - phi and err1 sums,  utils/utils_pdhg_solver.py:55, 58)
+ *   pdhg_update_dual         update_dual_alternative (<= rho_alp_iters update_fns_in_pdhg.py:167-180
+ *                            calls of update_dual_oneiter :150-165)
+ *   pdhg_iterate             the body of PDHG_solver_oneiter's loop    utils/utils_pdhg_solver.py:51-88
+ *                            (primal, extrapolation, dual, err1/err2, convergence and NaN stop tests)
+ *
+ * Return convention: every function returns PDHG_OK (0) or a negative
+ * pdhg_status; pdhg_last_error() gives the message (thread-local).
+ * Threading: a context is single-caller.  It drives one GPU on its own HIP
+ * stream; multi-GPU runs use one process per GPU.
+ */
+#ifndef PDHG_MI355X_H
+#define PDHG_MI355X_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PDHG_ABI_VERSION 1
+
+typedef enum pdhg_status {
+  PDHG_OK = 0,
+  PDHG_ERR_ARG = -1,          /* bad argument (null pointer, size, value)            */
+  PDHG_ERR_UNSUPPORTED = -2,  /* (egno, ndim, bc) or size combination not supported  */
+  PDHG_ERR_HIP = -3,          /* HIP runtime error (message has the HIP error string) */
+  PDHG_ERR_STATE = -4,        /* call order / state error (e.g. dual before primal)   */
+  PDHG_ERR_NOMEM = -5         /* device allocation failed                             */
+} pdhg_status;
+
+/* Problem description: one PDHG time window of T unknown time rows
+ * (T = time_step_per_PDHG - 1, utils/utils_pdhg_solver.py:121-137).
+ * Mirrors the static arguments of the reference's jitted updates. */
+typedef struct pdhg_problem {
+  int egno;          /* example 1, 2 or 3                          set_fns.py:52            */
+  int ndim;          /* 1 or 2                                                              */
+  int bc_x, bc_y;    /* 0 periodic, 1 Neumann (egno 3: bc_x = 1)   run_example.py:229-240   */
+  int nx, ny;        /* grid; ny = 1 when ndim == 1                                         */
+  int T;             /* unknown time rows: phi is [T+1, nx(,ny)], rho / alp are [T, ...]    */
+  int precision;     /* 4 = fp32 (default, bench), 8 = fp64 (tight parity)                  */
+  int rho_alp_iters; /* max dual sub-iterations per outer iteration (reference: 10)         */
+  int reserved0;
+  double dx, dy, dt;
+  double epsl;       /* viscosity epsilon                                                   */
+  double c_on_rho;   /* c in R_T += c/dt                           update_fns_in_pdhg.py:80 */
+  double C, pow_, Ct;/* preconditioner; pow_ and Ct are honoured in 1-D only, as the
+                        reference (update_fns_in_pdhg.py:146)                              */
+  const double* xs;  /* [nx] grid x coordinates (x_arr[0,:,0(,0)])                         */
+  const double* ys;  /* [ny] grid y coordinates (x_arr[0,0,:,1]); NULL when ndim == 1      */
+} pdhg_problem;
+
+typedef struct pdhg_stats {
+  int iters_run;     /* outer iterations executed by this call (incl. the stopping one)     */
+  int status;        /* 0 = ran all n_iters, 1 = converged (err1<eps && err2<eps), 2 = NaN  */
+  int inner_last;    /* dual sub-iterations of the last executed outer iteration            */
+  int inner_total;   /* dual sub-iterations summed over this call                            */
+  double err1;       /* primal error ||phi'-phi||/||phi|| of the last executed iteration     */
+  double err2;       /* dual error (utils/utils_pdhg_solver.py:60-68)                         */
+  double err_inner;  /* last dual sub-iteration error (update_fns_in_pdhg.py:162-164)        */
+  double rho_min, rho_max; /* not computed (NaN) unless requested; reserved                 */
+  int nan_seen;      /* a NaN appeared in phi' or rho' during this call                        */
+  int reserved1;
+} pdhg_stats;
+
+typedef struct pdhg_ctx pdhg_ctx;
+
+const char* pdhg_last_error(void);
+int pdhg_abi_version(void);
+
+/* Number of HIP devices visible (0 when no GPU / no driver). */
+int pdhg_device_count(int* count);
+
+/* Allocates all device buffers for the window.  device = HIP ordinal. */
+int pdhg_create(const pdhg_problem* prob, int device, pdhg_ctx** out);
+int pdhg_destroy(pdhg_ctx* ctx);
+
+/* State in the reference layout, float64 host arrays (C order):
+ *   phi [T+1][nx][ny], rho [T][nx][ny],
+ *   alp: n_alp arrays (2 in 1-D, 4 in 2-D) each [T][nx][ny][n_ctrl]
+ *        (n_ctrl = 1 in 1-D and for egno 3, 2 otherwise), passed as one
+ *        contiguous [n_alp][T][nx][ny][n_ctrl] block.
+ * Only the live control components are stored on the device:
+ * set_state fails with PDHG_ERR_UNSUPPORTED if a dead component is non-zero;
+ * get_state writes zeros there. */
+int pdhg_set_state(pdhg_ctx* ctx, const double* phi, const double* rho, const double* alp);
+int pdhg_get_state(pdhg_ctx* ctx, double* phi, double* rho, double* alp);
+int pdhg_get_phi_bar(pdhg_ctx* ctx, double* phi_bar);   /* [T+1][nx][ny] */
+/* phi_bar input of the drop-in dual update (update_dual_oneiter's first argument). */
+int pdhg_set_phi_bar(pdhg_ctx* ctx, const double* phi_bar);
+
+/* The reference's PDHG_multi_step initial state for a window
+ * (utils/utils_pdhg_solver.py:123-137): every phi row = g, rho = c_on_rho,
+ * alp = 0.  g: [nx][ny] host float64.  Built on the device (HBM-resident). */
+int pdhg_init_state(pdhg_ctx* ctx, const double* g);
+
+/* One primal update: phi <- phi + tau * H1^{-1}(cont_residual(rho, alp));
+ * also forms phi_bar = 2 phi' - phi and the err1 sums. */
+int pdhg_update_primal(pdhg_ctx* ctx, double tau);
+
+/* update_dual_alternative: up to rho_alp_iters sub-iterations with early exit
+ * at err < eps; *inner_used receives the sub-iterations executed. */
+int pdhg_update_dual(pdhg_ctx* ctx, double sigma, double eps, int rho_alp_iters, int* inner_used);
+
+/* Errors of the last primal+dual pair (err1, err2) as utils_pdhg_solver.py:58-68. */
+int pdhg_errors(pdhg_ctx* ctx, double* err1, double* err2);
+
+/* Error of the last dual sub-iteration (update_fns_in_pdhg.py:162-164), the value
+ * update_dual_oneiter returns as its third output. */
+int pdhg_inner_error(pdhg_ctx* ctx, double* err);
+
+/* Up to n_iters outer iterations on the device with the reference's stop
+ * rules (converged, then NaN).  tau = stepsz/1.5, sigma = stepsz*1.5
+ * (utils_pdhg_solver.py:44-46).  No host synchronisation per iteration. */
+int pdhg_iterate(pdhg_ctx* ctx, int n_iters, double tau, double sigma, double eps, int rho_alp_iters,
+                 pdhg_stats* out);
+
+/* Stop rules of pdhg_iterate (default: both on, as the reference).  Benchmarks may turn the NaN
+ * stop off so a diverging configuration still executes exactly n_iters iterations. */
+int pdhg_set_stop_rules(pdhg_ctx* ctx, int stop_on_converge, int stop_on_nan);
+
+/* Blocks until the context's stream is idle. */
+int pdhg_synchronize(pdhg_ctx* ctx);
+
+/* Device bytes held by the context. */
+int pdhg_device_bytes(pdhg_ctx* ctx, unsigned long long* bytes);
+
+/* Per-launch kernel timing for the benchmark: HIP events recorded on the
+ * context's stream around every launch of the named kernel class
+ * ("dual", "precond_fwd", "precond_bwd", "residual", "update") while
+ * enabled.  Returns the accumulated milliseconds and launch count. */
+int pdhg_profile_enable(pdhg_ctx* ctx, int enable);
+int pdhg_profile_query(pdhg_ctx* ctx, const char* kernel_class, double* total_ms, int* launches);
+
+/* Algorithmic HBM bytes of one outer iteration for k dual
+ * sub-iterations, and of one launch of the named kernel class. */
+int pdhg_algorithmic_bytes(pdhg_ctx* ctx, int k, const char* kernel_class, double* bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PDHG_MI355X_H */

@@ -1,0 +1,292 @@
+// LDS-resident multi-line Stockham FFT for gfx950 + real Hartley unpack.
+//
+// The H1 preconditioner of the reference (utils/utils_precond.py:105-178) is an
+// FFT in space, a tridiagonal solve in t per Fourier mode, and an inverse FFT.
+// Because the spatial operator is a real symmetric circulant, the separable
+// discrete Hartley transform (DHT) diagonalises it with the same symbol, so the
+// whole preconditioner runs in REAL arithmetic with no half-spectrum padding:
+// two real lines a, b are packed as z = a + i b, one complex FFT of z is
+// taken, and   H_a(k) = (Re Z_k + Re Z_-k - Im Z_k + Im Z_-k) / 2,
+//              H_b(k) = (Im Z_k + Im Z_-k - Re Z_-k + Re Z_k) / 2.
+// The DHT is its own inverse up to 1/n, so the inverse pass is the same code.
+#pragma once
+#include "common.hpp"
+
+namespace pdhg {
+
+struct FFTPlan {
+  int n;
+  int npass;
+  int pow2;             // n is a power of two (fast index math)
+  int radix[kMaxPass];
+};
+
+// cos / sin of 2*pi*k/16
+__device__ constexpr double kC16[16] = {1.0, 0.92387953251128674, 0.70710678118654752, 0.38268343236508977,
+                                        0.0, -0.38268343236508977, -0.70710678118654752, -0.92387953251128674,
+                                        -1.0, -0.92387953251128674, -0.70710678118654752, -0.38268343236508977,
+                                        0.0, 0.38268343236508977, 0.70710678118654752, 0.92387953251128674};
+__device__ constexpr double kS16[16] = {0.0, 0.38268343236508977, 0.70710678118654752, 0.92387953251128674,
+                                        1.0, 0.92387953251128674, 0.70710678118654752, 0.38268343236508977,
+                                        0.0, -0.38268343236508977, -0.70710678118654752, -0.92387953251128674,
+                                        -1.0, -0.92387953251128674, -0.70710678118654752, -0.38268343236508977};
+
+template <typename C>
+__device__ __forceinline__ void dft2(C& a, C& b) {
+  const C t = a;
+  a = cadd(t, b);
+  b = csub(t, b);
+}
+template <typename C>
+__device__ __forceinline__ void dft4(C& v0, C& v1, C& v2, C& v3) {
+  const C s02 = cadd(v0, v2), d02 = csub(v0, v2);
+  const C s13 = cadd(v1, v3), d13 = cmul_mi(csub(v1, v3));
+  v0 = cadd(s02, s13);
+  v2 = csub(s02, s13);
+  v1 = cadd(d02, d13);
+  v3 = csub(d02, d13);
+}
+// multiply by W_16^m = exp(-2 pi i m / 16), m compile-time
+template <typename C, int M>
+__device__ __forceinline__ C tw16(C a) {
+  using T = decltype(C::x);
+  constexpr int m = M & 15;
+  if constexpr (m == 0) return a;
+  else if constexpr (m == 4) return cmul_mi(a);
+  else if constexpr (m == 8) return cmk<C>(-a.x, -a.y);
+  else if constexpr (m == 12) return cmk<C>(-a.y, a.x);
+  else return cmul(a, cmk<C>((T)kC16[m], (T)(-kS16[m])));
+}
+
+// In-register forward DFT of size R in {2,3,4,8,16}, natural order in/out.
+// R = R1*R2 split: n = n1 + R1 n2, k = R2 k1 + k2 (DFT_R2 over n2, twiddle W_R^{n1 k2}, DFT_R1 over n1).
+template <typename C, int R>
+__device__ __forceinline__ void dft_any(C* v) {
+  if constexpr (R == 2) {
+    dft2(v[0], v[1]);
+  } else if constexpr (R == 3) {
+    using T = decltype(C::x);
+    const T h = (T)0.86602540378443865;  // sqrt(3)/2
+    const C t1 = cadd(v[1], v[2]);
+    const C t2 = cmk<C>(v[0].x - (T)0.5 * t1.x, v[0].y - (T)0.5 * t1.y);
+    const C d = csub(v[1], v[2]);
+    const C s = cmk<C>(h * d.y, -h * d.x);     // (b - c) * (-i sqrt(3)/2)
+    v[0] = cadd(v[0], t1);
+    v[1] = cadd(t2, s);
+    v[2] = csub(t2, s);
+  } else if constexpr (R == 4) {
+    dft4(v[0], v[1], v[2], v[3]);
+  } else if constexpr (R == 8) {
+    // R1 = 2, R2 = 4
+    dft4(v[0], v[2], v[4], v[6]);
+    dft4(v[1], v[3], v[5], v[7]);
+    v[3] = tw16<C, 2>(v[3]);
+    v[5] = tw16<C, 4>(v[5]);
+    v[7] = tw16<C, 6>(v[7]);
+    // Y[n1][k2] sits at v[n1 + 2 k2]; X[4 k1 + k2] = DFT2 over n1
+    C x[8];
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2) {
+      C a = v[2 * k2], b = v[2 * k2 + 1];
+      dft2(a, b);
+      x[k2] = a;
+      x[4 + k2] = b;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = x[i];
+  } else if constexpr (R == 16) {
+    // R1 = 4, R2 = 4: DFT4 over n2 of v[n1 + 4 n2] -> Y[n1][k2] stored back at v[n1 + 4 k2]
+    dft4(v[0], v[4], v[8], v[12]);
+    dft4(v[1], v[5], v[9], v[13]);
+    dft4(v[2], v[6], v[10], v[14]);
+    dft4(v[3], v[7], v[11], v[15]);
+    v[5] = tw16<C, 1>(v[5]);
+    v[9] = tw16<C, 2>(v[9]);
+    v[13] = tw16<C, 3>(v[13]);
+    v[6] = tw16<C, 2>(v[6]);
+    v[10] = tw16<C, 4>(v[10]);
+    v[14] = tw16<C, 6>(v[14]);
+    v[7] = tw16<C, 3>(v[7]);
+    v[11] = tw16<C, 6>(v[11]);
+    v[15] = tw16<C, 9>(v[15]);
+    // DFT4 over n1 for each k2: inputs v[4 k2 + n1], outputs X[4 k1 + k2]
+    dft4(v[0], v[1], v[2], v[3]);
+    dft4(v[4], v[5], v[6], v[7]);
+    dft4(v[8], v[9], v[10], v[11]);
+    dft4(v[12], v[13], v[14], v[15]);
+    // now v[4 k2 + k1] = X[4 k1 + k2]: transpose the 4x4 index
+    C x[16];
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2)
+#pragma unroll
+      for (int k1 = 0; k1 < 4; ++k1) x[4 * k1 + k2] = v[4 * k2 + k1];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = x[i];
+  }
+}
+
+// One Stockham DIT pass of compile-time radix R on nl interleaved lines
+// (element e of line l at index e*nl + l; nl a power of two).
+template <typename C, int R>
+__device__ __forceinline__ void stockham_pass(const C* __restrict__ src, C* __restrict__ dst, int n, int nl,
+                                              int lnl, int Ls, int pow2, const C* __restrict__ tw) {
+  const int nR = n / R;
+  const int tws = n / (Ls * R);
+  const int total = nR * nl;
+#pragma unroll 1
+  for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
+    const int l = idx & (nl - 1);
+    const int j = idx >> lnl;
+    const int k = pow2 ? (j & (Ls - 1)) : (j % Ls);
+    C v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = src[(size_t)(j + r * nR) * nl + l];
+    if (k != 0) {
+#pragma unroll
+      for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw[r * k * tws]);
+    }
+    dft_any<C, R>(v);
+    const int base = (j - k) * R + k;
+#pragma unroll
+    for (int r = 0; r < R; ++r) dst[(size_t)(base + r * Ls) * nl + l] = v[r];
+  }
+}
+
+// Generic (any radix) pass: one output element per work item, O(R) reads.
+template <typename C>
+__device__ void stockham_pass_generic(const C* __restrict__ src, C* __restrict__ dst, int n, int nl, int lnl,
+                                      int Ls, int R, const C* __restrict__ tw) {
+  using T = decltype(C::x);
+  const int nR = n / R;
+  const int tws = n / (Ls * R);
+  const int total = n * nl;
+  for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
+    const int l = idx & (nl - 1);
+    const int q = idx >> lnl;
+    const int k = q % Ls;
+    const int s = (q / Ls) % R;
+    const int j = (q / (Ls * R)) * Ls + k;
+    T ax = 0, ay = 0;
+    for (int qq = 0; qq < R; ++qq) {
+      C v = src[(size_t)(j + qq * nR) * nl + l];
+      if (k != 0 && qq != 0) v = cmul(v, tw[qq * k * tws]);
+      const C w = tw[((qq * s) % R) * nR];
+      ax += v.x * w.x - v.y * w.y;
+      ay += v.x * w.y + v.y * w.x;
+    }
+    dst[(size_t)q * nl + l] = cmk<C>(ax, ay);
+  }
+}
+
+// Full forward FFT of nl interleaved lines of length plan.n held in LDS buffer
+// a; b is scratch of the same size.  All threads of the block take part; the
+// call starts and ends with a barrier-complete state.  Returns the buffer that
+// holds the result (natural order).
+template <typename C>
+__device__ C* lds_fft(C* a, C* b, int nl, const FFTPlan& pl, const C* __restrict__ tw) {
+  int lnl = 0;
+  while ((1 << lnl) < nl) ++lnl;
+  int Ls = 1;
+  C* src = a;
+  C* dst = b;
+  for (int p = 0; p < pl.npass; ++p) {
+    const int R = pl.radix[p];
+    switch (R) {
+      case 16: stockham_pass<C, 16>(src, dst, pl.n, nl, lnl, Ls, pl.pow2, tw); break;
+      case 8: stockham_pass<C, 8>(src, dst, pl.n, nl, lnl, Ls, pl.pow2, tw); break;
+      case 4: stockham_pass<C, 4>(src, dst, pl.n, nl, lnl, Ls, pl.pow2, tw); break;
+      case 2: stockham_pass<C, 2>(src, dst, pl.n, nl, lnl, Ls, pl.pow2, tw); break;
+      case 3: stockham_pass<C, 3>(src, dst, pl.n, nl, lnl, Ls, pl.pow2, tw); break;
+      default: stockham_pass_generic<C>(src, dst, pl.n, nl, lnl, Ls, R, tw); break;
+    }
+    __syncthreads();
+    C* t = src;
+    src = dst;
+    dst = t;
+    Ls *= R;
+  }
+  return src;
+}
+
+// ---------------- compile-time-size FFT (hot sizes) ----------------
+// N (power of two) and NL (lines) are template constants, so every LDS stride is an
+// immediate offset and the radix schedule (16,16,..., then 8/4/2) unrolls statically.
+template <int N>
+struct Pow2Sched {
+  static constexpr int lead = (N >= 16) ? 16 : N;
+};
+
+template <typename C, int N, int NL, int LS, int R>
+__device__ __forceinline__ void fixed_pass(const C* __restrict__ src, C* __restrict__ dst, const C* __restrict__ tw) {
+  constexpr int nR = N / R;
+  constexpr int tws = N / (LS * R);
+  constexpr int total = nR * NL;
+  constexpr int lnl = (NL == 1) ? 0 : (NL == 2) ? 1 : (NL == 4) ? 2 : (NL == 8) ? 3 : 4;
+#pragma unroll 1
+  for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
+    const int l = idx & (NL - 1);
+    const int j = idx >> lnl;
+    const int k = j & (LS - 1);
+    C v[R];
+    const C* s = src + (size_t)j * NL + l;
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = s[r * nR * NL];
+    if (LS > 1 && k != 0) {
+#pragma unroll
+      for (int r = 1; r < R; ++r) v[r] = cmul(v[r], tw[r * k * tws]);
+    }
+    dft_any<C, R>(v);
+    C* d = dst + (size_t)((j - k) * R + k) * NL + l;
+#pragma unroll
+    for (int r = 0; r < R; ++r) d[r * LS * NL] = v[r];
+  }
+}
+
+template <typename C, int N, int NL, int LS>
+__device__ __forceinline__ C* fixed_passes(C* src, C* dst, const C* __restrict__ tw) {
+  if constexpr (LS >= N) {
+    return src;
+  } else {
+    constexpr int rem = N / LS;
+    constexpr int R = (rem >= 16) ? 16 : rem;
+    fixed_pass<C, N, NL, LS, R>(src, dst, tw);
+    __syncthreads();
+    return fixed_passes<C, N, NL, LS * R>(dst, src, tw);
+  }
+}
+
+template <typename C, int N, int NL>
+__device__ __forceinline__ C* lds_fft_fixed(C* a, C* b, const C* __restrict__ tw) {
+  return fixed_passes<C, N, NL, 1>(a, b, tw);
+}
+
+// FFT policies used as kernel template arguments.
+struct FFTRt {              // any n (mixed radix, runtime plan), nl interleaved lines
+  FFTPlan pl;
+  int nl;
+  template <typename C>
+  __device__ __forceinline__ C* run(C* a, C* b, const C* __restrict__ tw) const { return lds_fft<C>(a, b, nl, pl, tw); }
+  __device__ __forceinline__ int n() const { return pl.n; }
+  __device__ __forceinline__ int lines() const { return nl; }
+};
+template <int N, int NL>
+struct FFTFx {              // compile-time power-of-two n, NL lines
+  template <typename C>
+  __device__ __forceinline__ C* run(C* a, C* b, const C* __restrict__ tw) const {
+    return lds_fft_fixed<C, N, NL>(a, b, tw);
+  }
+  __device__ __forceinline__ int n() const { return N; }
+  __device__ __forceinline__ int lines() const { return NL; }
+};
+
+// Hartley unpack of line l at frequency k from the FFT Z of z = a + i b.
+template <typename C, typename T>
+__device__ __forceinline__ void hartley_pair(const C* Z, int n, int nl, int k, int l, T& ha, T& hb) {
+  const int km = (k == 0) ? 0 : n - k;
+  const C z = Z[(size_t)k * nl + l];
+  const C w = Z[(size_t)km * nl + l];
+  ha = (T)0.5 * ((z.x + w.x) - (z.y - w.y));
+  hb = (T)0.5 * ((z.y + w.y) - (w.x - z.x));
+}
+
+}  // namespace pdhg

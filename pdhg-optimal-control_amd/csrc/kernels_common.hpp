@@ -1,0 +1,140 @@
+// Reductions-to-scalars and device-side loop control (utils_pdhg_solver.py:58-80,
+// update_fns_in_pdhg.py:162-176) plus state initialisation kernels.
+#pragma once
+#include "params.hpp"
+
+namespace pdhg {
+
+// Fixed-order reduction of nrows partial rows (ns sums each) into out[0..ns).
+__device__ void reduce_partials(const double* __restrict__ partials, int nrows, int ns, double* out) {
+  __shared__ double red[256];
+  for (int s = 0; s < ns; ++s) {
+    double acc = 0.0;
+    for (int r = threadIdx.x; r < nrows; r += blockDim.x) acc += partials[(size_t)r * kNumSums + s];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = blockDim.x >> 1; w > 0; w >>= 1) {
+      if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) out[s] = red[0];
+    __syncthreads();
+  }
+}
+
+// After the primal update: err1 sums (utils_pdhg_solver.py:58).  row0_sq = sum phi_0^2
+// (row 0 never changes: utils_precond.py:139/177).
+__global__ void __launch_bounds__(256) k_finalize_primal(const double* partials, int nrows, double row0_sq, Ctrl* ctrl) {
+  if (ctrl->done) return;
+  __shared__ double out[3];
+  reduce_partials(partials, nrows, 3, out);
+  if (threadIdx.x == 0) {
+    ctrl->s_dphi = out[0];
+    ctrl->s_phi_old = out[1] + row0_sq;
+    ctrl->s_phi_new = out[2] + row0_sq;
+    ctrl->primal_valid = 1;
+  }
+}
+
+// After dual sub-iteration `sub`: err = sum (drho)^2/sum rho'^2 + sum_a sum (dalp)^2/sum alp'^2
+// (update_fns_in_pdhg.py:162-164); early exit flag when err < eps (:176).  n_dead reference
+// arrays that are not stored (egno 3's y controls, identically zero) contribute 0/0 = NaN.
+__global__ void __launch_bounds__(256) k_finalize_dual(const double* partials, int nrows, int na, int n_dead,
+                                                       double eps, int sub, Ctrl* ctrl) {
+  if (ctrl->done || ctrl->inner_done) return;
+  __shared__ double out[kNumSums];
+  const int ns = 3 + 3 * na;
+  reduce_partials(partials, nrows, ns, out);
+  if (threadIdx.x == 0) {
+    double err = out[0] / out[1];
+    for (int a = 0; a < na; ++a) err += out[3 + 3 * a] / out[4 + 3 * a];
+    for (int a = 0; a < n_dead; ++a) {
+      volatile double z = 0.0;
+      err += z / z;
+    }
+    for (int s = 0; s < ns; ++s) ctrl->dual_sums[s] = out[s];
+    if (sub == 0) {
+      for (int s = 0; s < ns; ++s) ctrl->outer_sums[s] = out[s];
+    }
+    ctrl->err_inner = err;
+    ctrl->inner_count = sub + 1;
+    if (err < eps) ctrl->inner_done = 1;
+  }
+}
+
+// k > 1: sums between the outer iteration's initial (cur) and final (1-cur) dual state.
+// partial rows: [0] sum (rho_f - rho_i)^2 [1] unused [2] sum rho_i^2, [3+3a] sum (da)^2, [5+3a] sum a_i^2
+template <typename R>
+__global__ void __launch_bounds__(256) k_outer_sums(KP<R> p, size_t n) {
+  if (p.ctrl->done) return;
+  const int cur = p.ctrl->cur;
+  double s[kNumSums];
+  for (int i = 0; i < kNumSums; ++i) s[i] = 0.0;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const double ri = p.rho[cur][i], rf = p.rho[1 - cur][i];
+    s[0] += (rf - ri) * (rf - ri);
+    s[2] += ri * ri;
+    for (int a = 0; a < p.na; ++a) {
+      const double ai = p.alp[cur][a][i], af = p.alp[1 - cur][a][i];
+      s[3 + 3 * a] += (af - ai) * (af - ai);
+      s[5 + 3 * a] += ai * ai;
+    }
+  }
+  block_reduce_store<kNumSums>(s, p.partials, blockIdx.x);
+}
+
+// End of an outer iteration: err1, err2 (utils_pdhg_solver.py:58-68), stop tests (:74-80).
+// outer_rows > 0: reduce k_outer_sums partials first (k > 1); else use the sub-iteration-0 sums.
+__global__ void __launch_bounds__(256) k_finalize_outer(const double* partials, int outer_rows, int na, double eps,
+                                                        int flip, int stop_conv, int stop_nan, Ctrl* ctrl) {
+  if (ctrl->done) return;
+  __shared__ double out[kNumSums];
+  if (outer_rows > 0) reduce_partials(partials, outer_rows, kNumSums, out);
+  if (threadIdx.x == 0) {
+    const double* os = (outer_rows > 0) ? out : ctrl->outer_sums;
+    const double err1 = sqrt(ctrl->s_dphi) / sqrt(ctrl->s_phi_old);
+    double err2 = sqrt(os[0]) / sqrt(os[2]);
+    for (int a = 0; a < na; ++a) {
+      const double norm_alp = sqrt(os[5 + 3 * a]);
+      const double norm_err = sqrt(os[3 + 3 * a]);
+      if (norm_alp < 1e-6 && norm_err > 1e-6) err2 += norm_err;
+      else if (norm_alp >= 1e-6) err2 += norm_err / norm_alp;
+    }
+    ctrl->err1 = err1;
+    ctrl->err2 = err2;
+    ctrl->iters += 1;
+    ctrl->inner_total += ctrl->inner_count;
+    const double rho_new_sq = ctrl->dual_sums[1];
+    if (err1 < eps && err2 < eps) {
+      if (stop_conv) ctrl->done = 1;
+    } else if (ctrl->s_phi_new != ctrl->s_phi_new || rho_new_sq != rho_new_sq) {
+      if (stop_nan) ctrl->done = 2;
+      ctrl->nan_seen = 1;
+    }
+    if (flip) ctrl->cur = 1 - ctrl->cur;
+    ctrl->inner_done = 0;
+    ctrl->primal_valid = 0;
+  }
+}
+
+// ---- state initialisation / conversion ----
+template <typename R>
+__global__ void k_fill(R* __restrict__ p, size_t n, R v) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
+}
+
+// every row of dst [rows][plane] = src [plane]
+template <typename R>
+__global__ void k_bcast_rows(R* __restrict__ dst, const R* __restrict__ src, size_t plane, int rows) {
+  const size_t n = plane * (size_t)rows;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = src[i % plane];
+}
+
+template <typename R>
+__global__ void k_copy(R* __restrict__ dst, const R* __restrict__ src, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+
+}  // namespace pdhg

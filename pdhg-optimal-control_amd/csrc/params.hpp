@@ -1,0 +1,93 @@
+// Kernel parameter block (passed by value) and problem-plugin device functions.
+#pragma once
+#include "common.hpp"
+#include "fft_lds.hpp"
+
+namespace pdhg {
+
+template <typename R>
+struct KP {
+  int egno, ndim, bcx, bcy;
+  int nx, ny, T;
+  int B, lB, nb;           // spectral block width (power of two), log2(B), number of column blocks
+  int rows_per_wg;         // rows handled by one residual / inverse-y workgroup (even)
+  int na;                  // live control arrays stored (2 or 4)
+  int inplace;             // dual updates rho/alp in place (rho_alp_iters == 1)
+  int sub;                 // dual sub-iteration index of this launch
+  R inv_dx, inv_dy, inv_dt, inv_dx2, inv_dy2;
+  R epsl, c_over_dt;
+  R ae;                    // Ct/dt^2 (1-D) or 1/dt^2 (2-D): off-diagonal magnitude of the t-Laplacian
+  R tau, sigma;
+  R inv_n;                 // 1/(nx*ny): DHT normalisation
+  const R* ax;             // f coefficient a(x) = (x-1)^2+0.1 (egno 1/2) or x coordinate (egno 3)  [nx]
+  const R* ay;             // a(y) [ny]
+  const R* lamx;           // symbol of the x Laplacian per mode (<= 0) [nx]
+  const R* lamy;           // symbol of the y Laplacian per mode [nb*B], zero padded
+  const R* d0_1d;          // 1-D: (C - lam)^pow per mode [nx]
+  R C;
+  R* phi;                  // [T+1][nx][ny]
+  R* phibar;               // [T+1][nx][ny]
+  R* work;                 // spectral work buffer
+  R* rho[2];               // [T][nx][ny]
+  R* alp[2][4];            // live control components, each [T][nx][ny]
+  double* partials;        // [blocks][kNumSums]
+  Ctrl* ctrl;
+};
+
+// neighbour index along an axis of length n with boundary condition bc
+// (utils_diff_op.py:5-7): returns -1 when the value is a Dirichlet zero.
+__device__ __forceinline__ int nb_index(int i, int n, int bc) {
+  if (i >= 0 && i < n) return i;
+  if (bc == 0) return (i < 0) ? i + n : i - n;       // periodic (jnp.roll)
+  if (bc == 1) return (i < 0) ? 0 : n - 1;           // Neumann: one-sided difference 0 / mirrored Dxx
+  return -1;                                         // Dirichlet: zero outside
+}
+
+template <typename R>
+__device__ __forceinline__ R load_or_zero(const R* __restrict__ p, int idx) {
+  return idx >= 0 ? p[idx] : (R)0;
+}
+
+// f1 = f(alp1)^+ , f2 = f(alp2)^- for the x (d=0) / y (d=1) controls,
+// update_fns_in_pdhg.py:13-47 with f_fn of set_fns.py:96-160.
+// egno 1/2: f = -a * alp ; egno 3: f_x = alp, f_y = x coordinate.
+template <typename R>
+__device__ __forceinline__ R fpos(R f) { return f * (R)(f >= (R)0 ? 1 : 0); }
+template <typename R>
+__device__ __forceinline__ R fneg(R f) { return f * (R)(f < (R)0 ? 1 : 0); }
+
+// alpha prox (set_fns.py:63-95 base functions + masks :108-110, :132-138, :157-159).
+// D = one-sided derivative of phi_bar, a = coefficient, p = (rho+1e-4)/sigma.
+// right = true -> alp1 (mask f >= 0), false -> alp2 (mask f < 0).
+template <typename R, int EGNO>
+__device__ __forceinline__ R alp_prox(R alp, R D, R a, R p, bool right) {
+  R n;
+  R f;
+  if constexpr (EGNO == 1) {
+    n = (D * a + p * alp) / ((R)1 + p);
+    f = -(a * n);
+  } else if constexpr (EGNO == 2) {
+    n = D * a / p + alp;
+    n = nmin<R>((R)1, nmax<R>((R)-1, n));
+    f = -(a * n);
+  } else {  // egno 3 x-controls: f = alp, coefficient -1 on D
+    n = (-D + p * alp) / ((R)1 + p);
+    f = n;
+  }
+  const bool keep = right ? (f >= (R)0) : (f < (R)0);
+  return n * (R)(keep ? 1 : 0);
+}
+
+template <typename R, int EGNO>
+__device__ __forceinline__ R fval(R alp, R a) {
+  if constexpr (EGNO == 3) return alp;
+  else return -(a * alp);
+}
+
+template <typename R, int EGNO>
+__device__ __forceinline__ R lag(R a2) {   // numerical L per component (set_fns.py:26-49)
+  if constexpr (EGNO == 2) return (R)0 * a2;
+  else return a2 / (R)2;
+}
+
+}  // namespace pdhg

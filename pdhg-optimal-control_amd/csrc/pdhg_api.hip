@@ -1,0 +1,914 @@
+// Host side of libpdhg: context, FFT plans, launch sequencing, C ABI (include/pdhg.h).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/pdhg.h"
+#include "kernels_1d.hpp"
+#include "kernels_2d.hpp"
+#include "kernels_common.hpp"
+
+using namespace pdhg;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                           \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess) return fail(PDHG_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+constexpr size_t kLdsBytes = 160 * 1024;
+
+FFTPlan make_plan(int n, bool& ok) {
+  FFTPlan pl{};
+  pl.n = n;
+  pl.pow2 = (n > 0) && ((n & (n - 1)) == 0);
+  int m = n, np = 0;
+  ok = true;
+  auto push = [&](int r) {
+    if (np >= kMaxPass) { ok = false; return; }
+    pl.radix[np++] = r;
+  };
+  for (int r : {16, 8, 4, 2})
+    while (m % r == 0 && m > 1) { push(r); m /= r; }
+  while (m % 3 == 0) { push(3); m /= 3; }
+  for (int f = 5; m > 1; f += 2)
+    while (m % f == 0) { push(f); m /= f; }
+  pl.npass = np;
+  return pl;
+}
+
+template <typename R>
+std::vector<cplx<R>> twiddles(int n) {
+  std::vector<cplx<R>> t(n);
+  for (int k = 0; k < n; ++k) {
+    const double a = -2.0 * M_PI * (double)k / (double)n;
+    t[k].x = (R)std::cos(a);
+    t[k].y = (R)std::sin(a);
+  }
+  return t;
+}
+
+struct ProfEntry {
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  size_t used = 0;
+};
+
+struct ImplBase {
+  virtual ~ImplBase() {}
+};
+
+template <typename R>
+struct Impl : ImplBase {
+  using C = cplx<R>;
+  pdhg_problem pb{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  KP<R> kp{};
+  FFTPlan plx{}, ply{};
+  C* twx = nullptr;
+  C* twy = nullptr;
+  std::vector<void*> allocs;
+  size_t dev_bytes = 0;
+  int na = 0, n_dead = 0;
+  bool two_sets = false;
+  double row0_sq = 0.0;
+  // launch geometry
+  int NT2 = 512;
+  int gx1 = 0, gx4 = 0, g4 = 1, gx5 = 0, g5 = 1, g_outer = 1;
+  size_t lds_res = 0, lds_xt = 0;
+  size_t partial_rows = 0;
+  bool primal_done = false;
+  int stop_conv = 1, stop_nan = 1;   // reference stop rules (utils_pdhg_solver.py:74-80)
+  // profiling
+  bool prof = false;
+  std::map<std::string, ProfEntry> prof_ev;
+  int* h_done = nullptr;   // pinned
+
+  ~Impl() override {
+    if (stream) hipStreamSynchronize(stream);
+    for (void* p : allocs) hipFree(p);
+    for (auto& kv : prof_ev)
+      for (auto& e : kv.second.ev) {
+        hipEventDestroy(e.first);
+        hipEventDestroy(e.second);
+      }
+    if (h_done) hipHostFree(h_done);
+    if (stream) hipStreamDestroy(stream);
+  }
+
+  template <typename T>
+  int alloc(T** p, size_t n) {
+    void* q = nullptr;
+    const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+    hipError_t e = hipMalloc(&q, bytes);
+    if (e != hipSuccess) return fail(PDHG_ERR_NOMEM, "hipMalloc(%zu bytes) failed: %s", bytes, hipGetErrorString(e));
+    allocs.push_back(q);
+    dev_bytes += bytes;
+    *p = static_cast<T*>(q);
+    return PDHG_OK;
+  }
+
+  size_t plane() const { return (size_t)pb.nx * (size_t)pb.ny; }
+
+  int setup() {
+    const int nx = pb.nx, ny = pb.ny, T = pb.T;
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    HIP_TRY(hipHostMalloc((void**)&h_done, sizeof(int), hipHostMallocDefault));
+    const bool is2d = pb.ndim == 2;
+    na = (pb.ndim == 1 || pb.egno == 3) ? 2 : 4;
+    n_dead = (pb.ndim == 2 && pb.egno == 3) ? 2 : 0;
+    two_sets = pb.rho_alp_iters > 1;
+    bool ok1 = true, ok2 = true;
+    plx = make_plan(nx, ok1);
+    if (is2d) ply = make_plan(ny, ok2);
+    if (!ok1 || !ok2) return fail(PDHG_ERR_UNSUPPORTED, "FFT plan too deep for nx=%d ny=%d", nx, ny);
+
+    KP<R>& p = kp;
+    p.egno = pb.egno;
+    p.ndim = pb.ndim;
+    p.bcx = pb.bc_x;
+    p.bcy = pb.bc_y;
+    p.nx = nx;
+    p.ny = ny;
+    p.T = T;
+    p.na = na;
+    p.inv_dx = (R)(1.0 / pb.dx);
+    p.inv_dy = (R)(is2d ? 1.0 / pb.dy : 0.0);
+    p.inv_dt = (R)(1.0 / pb.dt);
+    p.inv_dx2 = (R)(1.0 / (pb.dx * pb.dx));
+    p.inv_dy2 = (R)(is2d ? 1.0 / (pb.dy * pb.dy) : 0.0);
+    p.epsl = (R)pb.epsl;
+    p.c_over_dt = (R)(pb.c_on_rho / pb.dt);
+    p.C = (R)pb.C;
+    p.inv_n = (R)(1.0 / ((double)nx * (double)ny));
+    // t-Laplacian off-diagonal: Ct/dt^2 in 1-D (utils_precond.py:128-131); 2-D ignores Ct (:164-168)
+    p.ae = (R)((is2d ? 1.0 : pb.Ct) / (pb.dt * pb.dt));
+
+    const size_t csz = sizeof(C);
+    if (is2d) {
+      // spectral block width B: contiguous [nx][B] slabs; the x-transform workgroup holds
+      // M = nx*B modes with 5*M*sizeof(R) bytes of LDS (FFT ping-pong + Thomas carries)
+      const size_t cap = (sizeof(R) == 4) ? 8192 : 4096;
+      int B = 16;
+      while (B > 2 && (size_t)nx * B > cap) B >>= 1;
+      int nyp = 2;
+      while (nyp < ny) nyp <<= 1;
+      if (B > nyp) B = nyp;
+      if ((size_t)nx * B > cap)
+        return fail(PDHG_ERR_UNSUPPORTED, "nx=%d too large for the x-transform slab (max %zu in this precision)", nx,
+                    cap / 2);
+      p.B = B;
+      p.lB = 0;
+      while ((1 << p.lB) < B) ++p.lB;
+      p.nb = (ny + B - 1) / B;
+      p.rows_per_wg = 2;
+      lds_res = 2 * (size_t)ny * csz;
+      const int nmodes = nx * B;
+      lds_xt = (size_t)5 * nmodes * sizeof(R);
+      if (lds_res > kLdsBytes) return fail(PDHG_ERR_UNSUPPORTED, "ny=%d exceeds the LDS row transform", ny);
+      NT2 = std::min(512, ((nmodes + 63) / 64) * 64);
+      gx1 = ((nx + 1) / 2) * T;                      // row-pair tasks (flat grid)
+      gx4 = (int)std::min<long long>((long long)gx1, 4096);
+      g4 = 1;
+      gx5 = (ny + 255) / 256;
+      g5 = std::max(1, std::min(T * nx, 8192 / std::max(1, gx5)));
+    } else {
+      p.B = 1;
+      p.lB = 0;
+      p.nb = 1;
+      p.rows_per_wg = 2;
+      lds_res = 2 * (size_t)nx * csz;
+      if (lds_res > kLdsBytes) return fail(PDHG_ERR_UNSUPPORTED, "nx=%d exceeds the LDS line transform (1-D)", nx);
+      gx1 = (T + 1) / 2;
+      gx4 = std::min(gx1, 2048);
+      g4 = 1;
+      gx5 = (nx + 255) / 256;
+      g5 = std::max(1, std::min(T, 8192 / std::max(1, gx5)));
+    }
+    g_outer = 2048;
+    partial_rows = std::max<size_t>({(size_t)gx4 * g4, (size_t)gx5 * g5, (size_t)g_outer, 1});
+
+    // ---- device buffers ----
+    const size_t npl = plane();
+    int rc;
+    if ((rc = alloc(&p.phi, (size_t)(T + 1) * npl))) return rc;
+    if ((rc = alloc(&p.phibar, (size_t)(T + 1) * npl))) return rc;
+    const size_t nwork = is2d ? (size_t)T * p.nb * nx * p.B : (size_t)T * nx;
+    if ((rc = alloc(&p.work, nwork))) return rc;
+    for (int s = 0; s < (two_sets ? 2 : 1); ++s) {
+      if ((rc = alloc(&p.rho[s], (size_t)T * npl))) return rc;
+      for (int a = 0; a < na; ++a)
+        if ((rc = alloc(&p.alp[s][a], (size_t)T * npl))) return rc;
+    }
+    if (!two_sets) {
+      p.rho[1] = p.rho[0];
+      for (int a = 0; a < 4; ++a) p.alp[1][a] = p.alp[0][a];
+    }
+    for (int a = na; a < 4; ++a) p.alp[0][a] = p.alp[1][a] = nullptr;
+    if ((rc = alloc(&p.partials, partial_rows * kNumSums))) return rc;
+    if ((rc = alloc(&p.ctrl, 1))) return rc;
+    HIP_TRY(hipMemsetAsync(p.ctrl, 0, sizeof(Ctrl), stream));
+
+    // ---- coefficient / symbol tables (host fp64 -> R) ----
+    std::vector<R> ax(nx), ay(std::max(ny, 1)), lamx(nx), d0(nx);
+    for (int i = 0; i < nx; ++i) {
+      const double x = pb.xs[i];
+      ax[i] = (R)(pb.egno == 3 ? x : (x - 1.0) * (x - 1.0) + 0.1);   // set_fns.py:145 / :117-118 / :98
+    }
+    if (is2d)
+      for (int i = 0; i < ny; ++i) {
+        const double y = pb.ys[i];
+        ay[i] = (R)((y - 1.0) * (y - 1.0) + 0.1);
+      }
+    // Laplacian symbol = FFT of the periodic stencil (utils_precond.py:42-71), real part
+    for (int k = 0; k < nx; ++k) {
+      const double l = -2.0 * (1.0 - std::cos(2.0 * M_PI * k / nx)) / (pb.dx * pb.dx);
+      lamx[k] = (R)l;
+      d0[k] = (R)std::pow(pb.C - l, pb.pow_);   // 1-D thomas_b = (C - fv)^pow, :125-126
+    }
+    R *d_ax, *d_ay, *d_lamx, *d_lamy, *d_d0;
+    if ((rc = alloc(&d_ax, nx))) return rc;
+    if ((rc = alloc(&d_ay, std::max(ny, 1)))) return rc;
+    if ((rc = alloc(&d_lamx, nx))) return rc;
+    if ((rc = alloc(&d_d0, nx))) return rc;
+    HIP_TRY(hipMemcpy(d_ax, ax.data(), nx * sizeof(R), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d_ay, ay.data(), ay.size() * sizeof(R), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d_lamx, lamx.data(), nx * sizeof(R), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d_d0, d0.data(), nx * sizeof(R), hipMemcpyHostToDevice));
+    const int nyp = is2d ? p.nb * p.B : 1;
+    std::vector<R> lamy(nyp, (R)0);
+    if (is2d)
+      for (int k = 0; k < ny; ++k) lamy[k] = (R)(-2.0 * (1.0 - std::cos(2.0 * M_PI * k / ny)) / (pb.dy * pb.dy));
+    if ((rc = alloc(&d_lamy, nyp))) return rc;
+    HIP_TRY(hipMemcpy(d_lamy, lamy.data(), nyp * sizeof(R), hipMemcpyHostToDevice));
+    p.ax = d_ax;
+    p.ay = d_ay;
+    p.lamx = d_lamx;
+    p.lamy = d_lamy;
+    p.d0_1d = d_d0;
+    {
+      auto t = twiddles<R>(nx);
+      if ((rc = alloc(&twx, nx))) return rc;
+      HIP_TRY(hipMemcpy(twx, t.data(), nx * sizeof(C), hipMemcpyHostToDevice));
+    }
+    if (is2d) {
+      auto t = twiddles<R>(ny);
+      if ((rc = alloc(&twy, ny))) return rc;
+      HIP_TRY(hipMemcpy(twy, t.data(), ny * sizeof(C), hipMemcpyHostToDevice));
+    }
+    return set_lds_attrs();
+  }
+
+  std::vector<const void*> lds_done;
+  template <typename K>
+  int ensure_lds(K kern, size_t bytes) {
+    const void* f = reinterpret_cast<const void*>(kern);
+    for (const void* q : lds_done)
+      if (q == f) return PDHG_OK;
+    HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    lds_done.push_back(f);
+    return PDHG_OK;
+  }
+  int set_lds_attrs() { return PDHG_OK; }
+
+  // FFT policy dispatch: compile-time sizes for the hot power-of-two lengths (fp32),
+  // runtime mixed-radix plan otherwise.
+  template <typename Fn>
+  int with_line_fft(const FFTPlan& pl, Fn&& fn) {
+    if constexpr (sizeof(R) == 4) {
+      if (pl.pow2) {
+        switch (pl.n) {
+          case 256: return fn(FFTFx<256, 1>{});
+          case 512: return fn(FFTFx<512, 1>{});
+          case 1024: return fn(FFTFx<1024, 1>{});
+          case 2048: return fn(FFTFx<2048, 1>{});
+          case 4096: return fn(FFTFx<4096, 1>{});
+          case 8192: return fn(FFTFx<8192, 1>{});
+          default: break;
+        }
+      }
+    }
+    return fn(FFTRt{pl, 1});
+  }
+  template <typename Fn>
+  int with_xt_fft(Fn&& fn) {
+    const int nl = kp.B / 2;
+    if constexpr (sizeof(R) == 4) {
+      if (plx.pow2) {
+        const int n = plx.n;
+        if (n == 4096 && nl == 1) return fn(FFTFx<4096, 1>{});
+        if (n == 2048 && nl == 2) return fn(FFTFx<2048, 2>{});
+        if (n == 1024 && nl == 4) return fn(FFTFx<1024, 4>{});
+        if (n == 512 && nl == 8) return fn(FFTFx<512, 8>{});
+        if (n == 256 && nl == 8) return fn(FFTFx<256, 8>{});
+      }
+    }
+    return fn(FFTRt{plx, nl});
+  }
+
+  // ---------------- profiling ----------------
+  struct ProfScope {
+    Impl* im;
+    ProfEntry* e = nullptr;
+    ProfScope(Impl* i, const char* cls) : im(i) {
+      if (!im->prof) return;
+      e = &im->prof_ev[cls];
+      if (e->used == e->ev.size()) {
+        hipEvent_t a, b;
+        hipEventCreate(&a);
+        hipEventCreate(&b);
+        e->ev.push_back({a, b});
+      }
+      hipEventRecord(e->ev[e->used].first, im->stream);
+    }
+    ~ProfScope() {
+      if (!e) return;
+      hipEventRecord(e->ev[e->used].second, im->stream);
+      e->used++;
+    }
+  };
+
+  // ---------------- launches ----------------
+  int launch_primal(R tau) {
+    KP<R> p = kp;
+    p.tau = tau;
+    const int T = pb.T;
+    if (pb.ndim == 2) {
+      int rc;
+      {
+        ProfScope ps(this, "residual");
+        dim3 g(gx1);
+        rc = with_line_fft(ply, [&](auto f) {
+          using F = decltype(f);
+          int r2;
+          switch (pb.egno) {
+            case 1:
+              if ((r2 = ensure_lds(k_res_fwdy_2d<R, 1, F>, lds_res))) return r2;
+              hipLaunchKernelGGL((k_res_fwdy_2d<R, 1, F>), g, dim3(256), lds_res, stream, p, f, twy);
+              break;
+            case 2:
+              if ((r2 = ensure_lds(k_res_fwdy_2d<R, 2, F>, lds_res))) return r2;
+              hipLaunchKernelGGL((k_res_fwdy_2d<R, 2, F>), g, dim3(256), lds_res, stream, p, f, twy);
+              break;
+            default:
+              if ((r2 = ensure_lds(k_res_fwdy_2d<R, 3, F>, lds_res))) return r2;
+              hipLaunchKernelGGL((k_res_fwdy_2d<R, 3, F>), g, dim3(256), lds_res, stream, p, f, twy);
+              break;
+          }
+          return (int)PDHG_OK;
+        });
+        if (rc) return rc;
+      }
+      {
+        ProfScope ps(this, "precond");
+        dim3 g(p.nb);
+        rc = with_xt_fft([&](auto f) {
+          using F = decltype(f);
+          int r2;
+          if ((r2 = ensure_lds(k_precond_xt_2d<R, F>, lds_xt))) return r2;
+          hipLaunchKernelGGL((k_precond_xt_2d<R, F>), g, dim3(NT2), lds_xt, stream, p, f, twx);
+          return (int)PDHG_OK;
+        });
+        if (rc) return rc;
+      }
+      {
+        ProfScope ps(this, "update");
+        rc = with_line_fft(ply, [&](auto f) {
+          using F = decltype(f);
+          int r2;
+          if ((r2 = ensure_lds(k_invy_update_2d<R, F>, lds_res))) return r2;
+          hipLaunchKernelGGL((k_invy_update_2d<R, F>), dim3(gx4), dim3(256), lds_res, stream, p, f, twy);
+          return (int)PDHG_OK;
+        });
+        if (rc) return rc;
+      }
+      hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(256), 0, stream, p.partials, gx4 * g4, row0_sq, p.ctrl);
+    } else {
+      int rc;
+      {
+        ProfScope ps(this, "residual");
+        rc = with_line_fft(plx, [&](auto f) {
+          using F = decltype(f);
+          int r2;
+          if (pb.egno == 1) {
+            if ((r2 = ensure_lds(k_res_fwdx_1d<R, 1, F>, lds_res))) return r2;
+            hipLaunchKernelGGL((k_res_fwdx_1d<R, 1, F>), dim3(gx1), dim3(256), lds_res, stream, p, f, twx);
+          } else {
+            if ((r2 = ensure_lds(k_res_fwdx_1d<R, 2, F>, lds_res))) return r2;
+            hipLaunchKernelGGL((k_res_fwdx_1d<R, 2, F>), dim3(gx1), dim3(256), lds_res, stream, p, f, twx);
+          }
+          return (int)PDHG_OK;
+        });
+        if (rc) return rc;
+      }
+      {
+        ProfScope ps(this, "precond");
+        hipLaunchKernelGGL((k_thomas_1d<R>), dim3((pb.nx + 255) / 256), dim3(256), 0, stream, p);
+      }
+      {
+        ProfScope ps(this, "update");
+        rc = with_line_fft(plx, [&](auto f) {
+          using F = decltype(f);
+          int r2;
+          if ((r2 = ensure_lds(k_invx_update_1d<R, F>, lds_res))) return r2;
+          hipLaunchKernelGGL((k_invx_update_1d<R, F>), dim3(gx4), dim3(256), lds_res, stream, p, f, twx);
+          return (int)PDHG_OK;
+        });
+        if (rc) return rc;
+      }
+      hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(256), 0, stream, p.partials, gx4, row0_sq, p.ctrl);
+    }
+    HIP_TRY(hipGetLastError());
+    return PDHG_OK;
+  }
+
+  int launch_dual(R sigma, double eps, int k) {
+    KP<R> p = kp;
+    p.sigma = sigma;
+    p.inplace = (k <= 1) ? 1 : 0;
+    if (!p.inplace && !two_sets)
+      return fail(PDHG_ERR_STATE, "rho_alp_iters=%d needs a context created with rho_alp_iters > 1", k);
+    for (int s = 0; s < k; ++s) {
+      p.sub = s;
+      {
+        ProfScope ps(this, "dual");
+        dim3 g(gx5, g5);
+        if (pb.ndim == 2) {
+          switch (pb.egno) {
+            case 1: hipLaunchKernelGGL((k_dual_2d<R, 1>), g, dim3(256), 0, stream, p); break;
+            case 2: hipLaunchKernelGGL((k_dual_2d<R, 2>), g, dim3(256), 0, stream, p); break;
+            default: hipLaunchKernelGGL((k_dual_2d<R, 3>), g, dim3(256), 0, stream, p); break;
+          }
+        } else {
+          if (pb.egno == 1)
+            hipLaunchKernelGGL((k_dual_1d<R, 1>), g, dim3(256), 0, stream, p);
+          else
+            hipLaunchKernelGGL((k_dual_1d<R, 2>), g, dim3(256), 0, stream, p);
+        }
+      }
+      hipLaunchKernelGGL(k_finalize_dual, dim3(1), dim3(256), 0, stream, p.partials, gx5 * g5, na, n_dead, eps, s,
+                         p.ctrl);
+    }
+    HIP_TRY(hipGetLastError());
+    return PDHG_OK;
+  }
+
+  int launch_outer(double eps, int k) {
+    KP<R> p = kp;
+    int rows = 0;
+    if (k > 1) {
+      hipLaunchKernelGGL((k_outer_sums<R>), dim3(g_outer), dim3(256), 0, stream, p, (size_t)pb.T * plane());
+      rows = g_outer;
+    }
+    hipLaunchKernelGGL(k_finalize_outer, dim3(1), dim3(256), 0, stream, p.partials, rows, na, eps, k > 1 ? 1 : 0,
+                       stop_conv, stop_nan, p.ctrl);
+    HIP_TRY(hipGetLastError());
+    return PDHG_OK;
+  }
+
+  int reset_ctrl() {
+    // zero everything except `cur` (which buffer set holds the state)
+    Ctrl h{};
+    int cur = 0;
+    HIP_TRY(hipMemcpyAsync(&cur, &kp.ctrl->cur, sizeof(int), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    h.cur = cur;
+    HIP_TRY(hipMemcpyAsync(kp.ctrl, &h, sizeof(Ctrl), hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    return PDHG_OK;
+  }
+
+  int read_ctrl(Ctrl& h) {
+    HIP_TRY(hipMemcpyAsync(&h, kp.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    return PDHG_OK;
+  }
+
+  int iterate(int n, double tau, double sigma, double eps, int k, pdhg_stats* st) {
+    int rc;
+    if ((rc = reset_ctrl())) return rc;
+    const int window = 8;   // host runs at most 2*window iterations ahead of the device
+    std::vector<hipEvent_t> evs;
+    int ran = 0;
+    for (int i = 0; i < n; ++i) {
+      if ((rc = launch_primal((R)tau))) return rc;
+      if ((rc = launch_dual((R)sigma, eps, k))) return rc;
+      if ((rc = launch_outer(eps, k))) return rc;
+      ++ran;
+      if ((i + 1) % window == 0 && i + 1 < n) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(e, stream));
+        evs.push_back(e);
+        if (evs.size() >= 2) {
+          hipEvent_t old = evs[evs.size() - 2];
+          HIP_TRY(hipEventSynchronize(old));
+          HIP_TRY(hipMemcpy(h_done, &kp.ctrl->done, sizeof(int), hipMemcpyDeviceToHost));
+          if (*h_done) break;
+        }
+      }
+    }
+    for (auto e : evs) hipEventDestroy(e);
+    Ctrl h;
+    if ((rc = read_ctrl(h))) return rc;
+    (void)ran;
+    if (st) {
+      st->iters_run = h.iters;
+      st->status = h.done;
+      st->inner_last = h.inner_count;
+      st->inner_total = h.inner_total;
+      st->err1 = h.err1;
+      st->err2 = h.err2;
+      st->err_inner = h.err_inner;
+      st->rho_min = NAN;
+      st->rho_max = NAN;
+      st->nan_seen = h.nan_seen;
+    }
+    primal_done = false;
+    return PDHG_OK;
+  }
+
+  // ---------------- state ----------------
+  bool live(int a, int comp, int n_ctrl) const {   // which (array, component) is stored
+    if (pb.ndim == 1 || pb.egno == 3) return a < 2 && comp == 0;
+    (void)n_ctrl;
+    return (a < 2) ? comp == 0 : comp == 1;
+  }
+  int n_ctrl() const { return (pb.ndim == 1 || pb.egno == 3) ? 1 : 2; }
+  int n_alp_ref() const { return pb.ndim == 1 ? 2 : 4; }
+
+  void compute_row0_sq(const std::vector<R>& row0) {
+    double s = 0.0;
+    for (R v : row0) s += (double)v * (double)v;
+    row0_sq = s;
+  }
+
+  int set_state(const double* phi, const double* rho, const double* alp) {
+    const size_t npl = plane();
+    const int T = pb.T;
+    const int cur = 0;
+    std::vector<R> buf((size_t)(T + 1) * npl);
+    if (phi) {
+      for (size_t i = 0; i < buf.size(); ++i) buf[i] = (R)phi[i];
+      HIP_TRY(hipMemcpy(kp.phi, buf.data(), buf.size() * sizeof(R), hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(kp.phibar, buf.data(), buf.size() * sizeof(R), hipMemcpyHostToDevice));
+      compute_row0_sq(std::vector<R>(buf.begin(), buf.begin() + npl));
+    }
+    const size_t n = (size_t)T * npl;
+    if (rho) {
+      for (size_t i = 0; i < n; ++i) buf[i] = (R)rho[i];
+      HIP_TRY(hipMemcpy(kp.rho[cur], buf.data(), n * sizeof(R), hipMemcpyHostToDevice));
+    }
+    if (alp) {
+      const int nc = n_ctrl(), nar = n_alp_ref();
+      for (int a = 0; a < nar; ++a)
+        for (int c = 0; c < nc; ++c)
+          if (!live(a, c, nc))
+            for (size_t i = 0; i < n; ++i)
+              if (alp[((size_t)a * n + i) * nc + c] != 0.0)
+                return fail(PDHG_ERR_UNSUPPORTED,
+                            "alp[%d][...][%d] is a dead control component (identically zero in the reference "
+                            "examples) but holds non-zero values; only live components are stored", a, c);
+      for (int a = 0; a < nar; ++a)
+        for (int c = 0; c < nc; ++c) {
+          if (!live(a, c, nc)) continue;
+          for (size_t i = 0; i < n; ++i) buf[i] = (R)alp[((size_t)a * n + i) * nc + c];
+          HIP_TRY(hipMemcpy(kp.alp[cur][a], buf.data(), n * sizeof(R), hipMemcpyHostToDevice));
+        }
+    }
+    Ctrl h{};
+    h.cur = cur;
+    HIP_TRY(hipMemcpy(kp.ctrl, &h, sizeof(Ctrl), hipMemcpyHostToDevice));
+    primal_done = false;
+    return PDHG_OK;
+  }
+
+  int set_phi_bar(const double* pbar) {
+    const size_t n = (size_t)(pb.T + 1) * plane();
+    std::vector<R> buf(n);
+    for (size_t i = 0; i < n; ++i) buf[i] = (R)pbar[i];
+    HIP_TRY(hipMemcpy(kp.phibar, buf.data(), n * sizeof(R), hipMemcpyHostToDevice));
+    return PDHG_OK;
+  }
+
+  int get_phi_bar(double* pbar) {
+    HIP_TRY(hipStreamSynchronize(stream));
+    const size_t n = (size_t)(pb.T + 1) * plane();
+    std::vector<R> buf(n);
+    HIP_TRY(hipMemcpy(buf.data(), kp.phibar, n * sizeof(R), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < n; ++i) pbar[i] = (double)buf[i];
+    return PDHG_OK;
+  }
+
+  int get_state(double* phi, double* rho, double* alp) {
+    HIP_TRY(hipStreamSynchronize(stream));
+    Ctrl h;
+    int rc;
+    if ((rc = read_ctrl(h))) return rc;
+    const int cur = h.cur;
+    const size_t npl = plane();
+    const int T = pb.T;
+    std::vector<R> buf((size_t)(T + 1) * npl);
+    if (phi) {
+      HIP_TRY(hipMemcpy(buf.data(), kp.phi, buf.size() * sizeof(R), hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < buf.size(); ++i) phi[i] = (double)buf[i];
+    }
+    const size_t n = (size_t)T * npl;
+    if (rho) {
+      HIP_TRY(hipMemcpy(buf.data(), kp.rho[cur], n * sizeof(R), hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < n; ++i) rho[i] = (double)buf[i];
+    }
+    if (alp) {
+      const int nc = n_ctrl(), nar = n_alp_ref();
+      std::memset(alp, 0, sizeof(double) * n * nc * nar);
+      for (int a = 0; a < nar; ++a)
+        for (int c = 0; c < nc; ++c) {
+          if (!live(a, c, nc)) continue;
+          HIP_TRY(hipMemcpy(buf.data(), kp.alp[cur][a], n * sizeof(R), hipMemcpyDeviceToHost));
+          for (size_t i = 0; i < n; ++i) alp[((size_t)a * n + i) * nc + c] = (double)buf[i];
+        }
+    }
+    return PDHG_OK;
+  }
+
+  int init_state(const double* g) {
+    const size_t npl = plane();
+    const int T = pb.T;
+    std::vector<R> row(npl);
+    for (size_t i = 0; i < npl; ++i) row[i] = (R)g[i];
+    compute_row0_sq(row);
+    R* d_row;
+    int rc;
+    HIP_TRY(hipMalloc((void**)&d_row, npl * sizeof(R)));
+    HIP_TRY(hipMemcpy(d_row, row.data(), npl * sizeof(R), hipMemcpyHostToDevice));
+    const int grid = 4096;
+    hipLaunchKernelGGL((k_bcast_rows<R>), dim3(grid), dim3(256), 0, stream, kp.phi, d_row, npl, T + 1);
+    hipLaunchKernelGGL((k_bcast_rows<R>), dim3(grid), dim3(256), 0, stream, kp.phibar, d_row, npl, T + 1);
+    hipLaunchKernelGGL((k_fill<R>), dim3(grid), dim3(256), 0, stream, kp.rho[0], (size_t)T * npl, (R)pb.c_on_rho);
+    for (int a = 0; a < na; ++a)
+      hipLaunchKernelGGL((k_fill<R>), dim3(grid), dim3(256), 0, stream, kp.alp[0][a], (size_t)T * npl, (R)0);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(stream));
+    hipFree(d_row);
+    Ctrl h{};
+    HIP_TRY(hipMemcpy(kp.ctrl, &h, sizeof(Ctrl), hipMemcpyHostToDevice));
+    (void)rc;
+    primal_done = false;
+    return PDHG_OK;
+  }
+
+  int update_primal(double tau) {
+    int rc;
+    if ((rc = reset_ctrl())) return rc;
+    if ((rc = launch_primal((R)tau))) return rc;
+    HIP_TRY(hipStreamSynchronize(stream));
+    primal_done = true;
+    return PDHG_OK;
+  }
+
+  int update_dual(double sigma, double eps, int k, int* inner_used) {
+    int rc;
+    Ctrl h;
+    if ((rc = read_ctrl(h))) return rc;
+    h.done = 0;
+    h.inner_done = 0;
+    h.inner_count = 0;
+    HIP_TRY(hipMemcpy(kp.ctrl, &h, sizeof(Ctrl), hipMemcpyHostToDevice));
+    if ((rc = launch_dual((R)sigma, eps, k))) return rc;
+    if (primal_done) {
+      if ((rc = launch_outer(eps, k))) return rc;
+    } else if (k > 1) {
+      // no primal in this pairing: still move the state to the current buffer set
+      hipLaunchKernelGGL(k_finalize_outer, dim3(1), dim3(256), 0, stream, kp.partials, 0, na, -1.0, 1, 0, 0, kp.ctrl);
+    }
+    if ((rc = read_ctrl(h))) return rc;
+    if (inner_used) *inner_used = h.inner_count;
+    primal_done = false;
+    return PDHG_OK;
+  }
+
+  int errors(double* e1, double* e2) {
+    Ctrl h;
+    int rc;
+    if ((rc = read_ctrl(h))) return rc;
+    if (e1) *e1 = h.err1;
+    if (e2) *e2 = h.err2;
+    return PDHG_OK;
+  }
+
+  double algorithmic_bytes(int k, const std::string& cls) const {
+    const double N = (double)pb.T * (double)plane();
+    const double S = (double)sizeof(R);
+    const bool d2 = pb.ndim == 2;
+    const double nr = 1.0 + na;   // rho + live alp arrays
+    if (cls == "iteration") {
+      // 2-D 4N(14 + 11k + 5[k>1]), 1-D 4N(12 + 7k + 3[k>1]); generalised to S and na
+      if (d2) return S * N * (14.0 + 11.0 * k + 5.0 * (k > 1));
+      return S * N * (12.0 + 7.0 * k + 3.0 * (k > 1));
+    }
+    if (cls == "dual") return S * N * (1.0 + 2.0 * nr);      // read phi_bar, rho, alp; write rho, alp
+    if (cls == "residual") return S * N * (nr + 1.0);        // read rho, alp; write spectrum
+    if (cls == "precond") return S * N * (d2 ? 4.0 : 2.0);   // 2-D: x-DHT+Thomas fwd (2N) + bwd+x-DHT (2N)
+    if (cls == "update") return S * N * 4.0;                 // read U, phi; write phi, phi_bar
+    return -1.0;
+  }
+};
+
+struct CtxBox {
+  int precision;
+  std::unique_ptr<ImplBase> impl;
+};
+
+template <typename F>
+int dispatch(pdhg_ctx* ctx, F&& f) {
+  if (!ctx) return fail(PDHG_ERR_ARG, "null context");
+  CtxBox* b = reinterpret_cast<CtxBox*>(ctx);
+  if (b->precision == 8) return f(*static_cast<Impl<double>*>(b->impl.get()));
+  return f(*static_cast<Impl<float>*>(b->impl.get()));
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* pdhg_last_error(void) { return g_err.c_str(); }
+int pdhg_abi_version(void) { return PDHG_ABI_VERSION; }
+
+int pdhg_device_count(int* count) {
+  if (!count) return fail(PDHG_ERR_ARG, "null count");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  *count = (e == hipSuccess) ? n : 0;
+  return PDHG_OK;
+}
+
+int pdhg_create(const pdhg_problem* prob, int device, pdhg_ctx** out) {
+  if (!prob || !out) return fail(PDHG_ERR_ARG, "null argument");
+  *out = nullptr;
+  const pdhg_problem& p = *prob;
+  if (p.ndim != 1 && p.ndim != 2) return fail(PDHG_ERR_ARG, "ndim %d not implemented", p.ndim);
+  if (p.egno < 1 || p.egno > 3) return fail(PDHG_ERR_ARG, "egno %d not implemented", p.egno);
+  if (p.egno == 3 && p.ndim != 2) return fail(PDHG_ERR_ARG, "egno 3 requires ndim 2 (set_fns.py:96)");
+  if (p.nx < 3 || (p.ndim == 2 && p.ny < 3)) return fail(PDHG_ERR_ARG, "grid must be at least 3 points per axis");
+  if (p.ndim == 1 && p.ny != 1) return fail(PDHG_ERR_ARG, "ndim 1 requires ny == 1");
+  if (p.T < 1) return fail(PDHG_ERR_ARG, "T must be >= 1");
+  if (!(p.dx > 0) || !(p.dt > 0) || (p.ndim == 2 && !(p.dy > 0))) return fail(PDHG_ERR_ARG, "grid spacings must be > 0");
+  if (!p.xs || (p.ndim == 2 && !p.ys)) return fail(PDHG_ERR_ARG, "grid coordinates required");
+  if (p.precision != 4 && p.precision != 8) return fail(PDHG_ERR_ARG, "precision must be 4 or 8");
+  if (p.rho_alp_iters < 1) return fail(PDHG_ERR_ARG, "rho_alp_iters must be >= 1");
+  // preconditioner boundary conditions (utils_precond.py:121-124, :157-163)
+  if (p.ndim == 1 && p.bc_x != 0) return fail(PDHG_ERR_UNSUPPORTED, "H1_precond_1d supports bc=0 only");
+  if (p.ndim == 2 && !(p.bc_x == 0 && p.bc_y == 0))
+    return fail(PDHG_ERR_UNSUPPORTED, "bc (%d,%d): only periodic (0,0) is implemented on the device (egno 3's "
+                                      "(1,0) DCT path is not built yet)", p.bc_x, p.bc_y);
+  if (p.ndim == 1 && p.Ct < 0) return fail(PDHG_ERR_ARG, "Ct must be >= 0");
+  if (p.C < 0) return fail(PDHG_ERR_ARG, "C must be >= 0");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(PDHG_ERR_HIP, "no HIP device available");
+  if (device < 0 || device >= ndev) return fail(PDHG_ERR_ARG, "device %d out of range (%d devices)", device, ndev);
+  auto box = std::make_unique<CtxBox>();
+  box->precision = p.precision;
+  int rc;
+  if (p.precision == 8) {
+    auto im = std::make_unique<Impl<double>>();
+    im->pb = p;
+    im->device = device;
+    rc = im->setup();
+    box->impl = std::move(im);
+  } else {
+    auto im = std::make_unique<Impl<float>>();
+    im->pb = p;
+    im->device = device;
+    rc = im->setup();
+    box->impl = std::move(im);
+  }
+  if (rc) return rc;
+  *out = reinterpret_cast<pdhg_ctx*>(box.release());
+  return PDHG_OK;
+}
+
+int pdhg_destroy(pdhg_ctx* ctx) {
+  if (!ctx) return PDHG_OK;
+  delete reinterpret_cast<CtxBox*>(ctx);
+  return PDHG_OK;
+}
+
+int pdhg_set_state(pdhg_ctx* ctx, const double* phi, const double* rho, const double* alp) {
+  return dispatch(ctx, [&](auto& im) { return im.set_state(phi, rho, alp); });
+}
+int pdhg_get_state(pdhg_ctx* ctx, double* phi, double* rho, double* alp) {
+  return dispatch(ctx, [&](auto& im) { return im.get_state(phi, rho, alp); });
+}
+int pdhg_get_phi_bar(pdhg_ctx* ctx, double* phi_bar) {
+  if (!phi_bar) return fail(PDHG_ERR_ARG, "null phi_bar");
+  return dispatch(ctx, [&](auto& im) { return im.get_phi_bar(phi_bar); });
+}
+int pdhg_set_phi_bar(pdhg_ctx* ctx, const double* phi_bar) {
+  if (!phi_bar) return fail(PDHG_ERR_ARG, "null phi_bar");
+  return dispatch(ctx, [&](auto& im) { return im.set_phi_bar(phi_bar); });
+}
+int pdhg_init_state(pdhg_ctx* ctx, const double* g) {
+  if (!g) return fail(PDHG_ERR_ARG, "null g");
+  return dispatch(ctx, [&](auto& im) { return im.init_state(g); });
+}
+int pdhg_update_primal(pdhg_ctx* ctx, double tau) {
+  return dispatch(ctx, [&](auto& im) { return im.update_primal(tau); });
+}
+int pdhg_update_dual(pdhg_ctx* ctx, double sigma, double eps, int rho_alp_iters, int* inner_used) {
+  if (rho_alp_iters < 1) return fail(PDHG_ERR_ARG, "rho_alp_iters must be >= 1");
+  return dispatch(ctx, [&](auto& im) { return im.update_dual(sigma, eps, rho_alp_iters, inner_used); });
+}
+int pdhg_errors(pdhg_ctx* ctx, double* err1, double* err2) {
+  return dispatch(ctx, [&](auto& im) { return im.errors(err1, err2); });
+}
+int pdhg_inner_error(pdhg_ctx* ctx, double* err) {
+  if (!err) return fail(PDHG_ERR_ARG, "null err");
+  return dispatch(ctx, [&](auto& im) {
+    Ctrl h;
+    int rc = im.read_ctrl(h);
+    if (rc) return rc;
+    *err = h.err_inner;
+    return (int)PDHG_OK;
+  });
+}
+int pdhg_iterate(pdhg_ctx* ctx, int n_iters, double tau, double sigma, double eps, int rho_alp_iters,
+                 pdhg_stats* out) {
+  if (n_iters < 0 || rho_alp_iters < 1) return fail(PDHG_ERR_ARG, "bad iteration counts");
+  return dispatch(ctx, [&](auto& im) { return im.iterate(n_iters, tau, sigma, eps, rho_alp_iters, out); });
+}
+int pdhg_set_stop_rules(pdhg_ctx* ctx, int stop_on_converge, int stop_on_nan) {
+  return dispatch(ctx, [&](auto& im) {
+    im.stop_conv = stop_on_converge ? 1 : 0;
+    im.stop_nan = stop_on_nan ? 1 : 0;
+    return (int)PDHG_OK;
+  });
+}
+int pdhg_synchronize(pdhg_ctx* ctx) {
+  return dispatch(ctx, [&](auto& im) {
+    HIP_TRY(hipStreamSynchronize(im.stream));
+    return (int)PDHG_OK;
+  });
+}
+int pdhg_device_bytes(pdhg_ctx* ctx, unsigned long long* bytes) {
+  if (!bytes) return fail(PDHG_ERR_ARG, "null bytes");
+  return dispatch(ctx, [&](auto& im) {
+    *bytes = im.dev_bytes;
+    return (int)PDHG_OK;
+  });
+}
+int pdhg_profile_enable(pdhg_ctx* ctx, int enable) {
+  return dispatch(ctx, [&](auto& im) {
+    HIP_TRY(hipStreamSynchronize(im.stream));
+    im.prof = enable != 0;
+    for (auto& kv : im.prof_ev) kv.second.used = 0;
+    return (int)PDHG_OK;
+  });
+}
+int pdhg_profile_query(pdhg_ctx* ctx, const char* cls, double* total_ms, int* launches) {
+  if (!cls || !total_ms || !launches) return fail(PDHG_ERR_ARG, "null argument");
+  return dispatch(ctx, [&](auto& im) {
+    HIP_TRY(hipStreamSynchronize(im.stream));
+    *total_ms = 0.0;
+    *launches = 0;
+    auto it = im.prof_ev.find(cls);
+    if (it == im.prof_ev.end()) return (int)PDHG_OK;
+    for (size_t i = 0; i < it->second.used; ++i) {
+      float ms = 0.f;
+      HIP_TRY(hipEventElapsedTime(&ms, it->second.ev[i].first, it->second.ev[i].second));
+      *total_ms += ms;
+    }
+    *launches = (int)it->second.used;
+    return (int)PDHG_OK;
+  });
+}
+int pdhg_algorithmic_bytes(pdhg_ctx* ctx, int k, const char* cls, double* bytes) {
+  if (!cls || !bytes) return fail(PDHG_ERR_ARG, "null argument");
+  return dispatch(ctx, [&](auto& im) {
+    *bytes = im.algorithmic_bytes(k, cls);
+    return *bytes < 0 ? fail(PDHG_ERR_ARG, "unknown kernel class %s", cls) : (int)PDHG_OK;
+  });
+}
+
+}  // extern "C"

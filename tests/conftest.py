@@ -1,0 +1,24 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "pdhg-optimal-control_amd"), os.path.join(ROOT, "oracle"), ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); parity tests through the C ABI")
+
+
+@pytest.fixture(scope="session")
+def native():
+    """The built HIP library; GPU tests fail loudly if it is missing (no CPU fallback)."""
+    import __graft_entry__
+    __graft_entry__.build()
+    from pdhg_amd import _native
+    if _native.device_count() < 1:
+        pytest.fail("gpu test selected but no HIP device is visible")
+    return _native

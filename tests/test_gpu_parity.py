@@ -1,0 +1,296 @@
+"""HIP kernels vs the float64 oracle, through the C ABI (pytest -m gpu).
+
+Tolerances (stated per SURVEY.md Appendix B.8):
+  * fp64 device path: relative L2 <= 1e-10 on every state array after 1 and 10 iterations
+    (same algorithm up to FFT/Hartley/closed-form-pivot roundoff);
+  * fp32 device path from the reference's own initial state (phi = g, rho = c, alp = 0;
+    utils_pdhg_solver.py:123-137): relative L2 of the primal update U = (phi' - phi)/tau <= 2e-6,
+    of phi after 10 iterations <= 1e-5 (the north-star "phi within 1e-5 rel-L2"), rho <= 1e-5;
+  * fp32 from the seeded rough state (uniform-noise rho, used to drive every mask/clip branch):
+    the residual is dominated by eps*Lap(noise) ~ 1e4, so fp32 input rounding alone gives
+    ~kappa*6e-8 ~ 1e-5 relative error in U; bounds there are 1e-4 (U, alp) and 2e-4 (rho).
+"""
+import numpy as np
+import pytest
+
+import pdhg_oracle as O
+from _problems import device_ctx, make_problem, oracle_fns, rel
+
+pytestmark = pytest.mark.gpu
+
+TAU, SIGMA = 0.1 / 1.5, 0.1 * 1.5
+
+CASES = [
+    # egno, ndim, nx, ny, T, epsl
+    (1, 1, 16, 1, 4, 0.0),
+    (2, 1, 160, 1, 5, 0.0),
+    (1, 1, 17, 1, 3, 0.1),      # odd nx
+    (2, 1, 32, 1, 1, 0.0),      # T = 1 (the window-marching default)
+    (1, 1, 256, 1, 8, 0.0),     # fixed-size FFT path in fp32
+    (1, 2, 16, 12, 4, 0.0),
+    (2, 2, 16, 16, 5, 0.1),
+    (1, 2, 20, 18, 3, 0.1),     # non power-of-two (mixed radix 5 / 3)
+    (2, 2, 15, 17, 2, 0.0),     # odd nx (zero-paired row) and odd ny (padded column block)
+    (1, 2, 32, 32, 1, 0.0),     # T = 1
+    (2, 2, 64, 48, 8, 0.1),
+    (1, 2, 256, 256, 3, 0.0),   # fixed-size FFT paths (rows 256, x-slab 256 x 8 lines) in fp32
+]
+IDS = ["e{}d{}_{}x{}_T{}_eps{}".format(*c) for c in CASES]
+
+
+def _oracle_primal(P, phi, rho, alp):
+    primal, _ = oracle_fns(P)
+    return primal(phi, rho, 70.0, alp, TAU, P["dt"], P["dsp"], P["fns"], P["fv"], P["epsl"], P["x_arr"], None)
+
+
+def _oracle_dual(P, phi_bar, rho, alp, k=1, eps=-1.0, stats=None):
+    _, dual = oracle_fns(P, rho_alp_iters=k, stats=stats)
+    return dual(phi_bar, rho, 70.0, alp, SIGMA, P["dt"], P["dsp"], P["epsl"], P["fns"], P["x_arr"], None, P["ndim"],
+                eps)
+
+
+@pytest.mark.parametrize("case", CASES, ids=IDS)
+@pytest.mark.parametrize("prec", ["fp64", "fp32"])
+def test_primal(native, case, prec):
+    P = make_problem(*case)
+    ctx = device_ctx(P, prec)
+    ctx.set_state(P["phi"], P["rho"], P["alp"])
+    ctx.update_primal(TAU)
+    phi_d = ctx.get_state()[0]
+    pbar_d = ctx.get_phi_bar()
+    phi_o = _oracle_primal(P, P["phi"], P["rho"], P["alp"])
+    U_o = (phi_o - P["phi"]) / TAU
+    U_d = (phi_d - P["phi"]) / TAU
+    if prec == "fp64":
+        assert rel(U_d, U_o) < 1e-10
+        assert rel(pbar_d, 2 * phi_o - P["phi"]) < 1e-12
+    else:
+        # U recovered from fp32 phi' carries phi's rounding / tau; phi' itself is the checked quantity
+        assert rel(U_d, U_o) < 5e-4
+        assert rel(phi_d, phi_o) < 1e-6
+        assert rel(pbar_d, 2 * phi_o - P["phi"]) < 1e-5
+    assert np.array_equal(phi_d[0], P["phi"][0].astype(np.float32 if prec == "fp32" else np.float64))
+    ctx.close()
+
+
+@pytest.mark.parametrize("case", CASES, ids=IDS)
+@pytest.mark.parametrize("prec", ["fp64", "fp32"])
+def test_dual_oneiter(native, case, prec):
+    P = make_problem(*case)
+    rng = np.random.default_rng(7)
+    phi_bar = P["phi"] + 0.05 * rng.standard_normal(P["phi"].shape)
+    ctx = device_ctx(P, prec)
+    ctx.set_state(P["phi"], P["rho"], P["alp"])
+    ctx.set_phi_bar(phi_bar)
+    ctx.update_dual(SIGMA, -np.inf, 1)
+    err_d = ctx.inner_error()
+    _, rho_d, alp_d = ctx.get_state()
+    rho_o, alp_o, err_o = O.update_dual_oneiter(phi_bar, P["rho"], 70.0, P["alp"], SIGMA, P["dt"], P["dsp"], P["epsl"],
+                                                P["x_arr"], None, P["bc"], P["fns"], P["ndim"])
+    tol = 1e-11 if prec == "fp64" else 1e-4
+    assert rel(rho_d, rho_o) < tol
+    for a_d, a_o in zip(alp_d, alp_o):
+        assert rel(a_d, a_o) < tol
+    assert abs(err_d - err_o) <= (1e-9 if prec == "fp64" else 1e-4) * abs(err_o)
+    ctx.close()
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c[4] > 1][:6], ids=[i for c, i in zip(CASES, IDS) if c[4] > 1][:6])
+def test_dual_alternative_early_exit(native, case):
+    """<= 10 sub-iterations with the err < eps early exit (update_fns_in_pdhg.py:167-180)."""
+    P = make_problem(*case)
+    phi_bar = P["phi"]
+    for eps in (1e-3, 1e-6):
+        stats = []
+        rho_o, alp_o = _oracle_dual(P, phi_bar, P["rho"], P["alp"], k=10, eps=eps, stats=stats)
+        ctx = device_ctx(P, "fp64", rho_alp_iters=10)
+        ctx.set_state(P["phi"], P["rho"], P["alp"])
+        ctx.set_phi_bar(phi_bar)
+        used = ctx.update_dual(SIGMA, eps, 10)
+        _, rho_d, alp_d = ctx.get_state()
+        assert used == stats[0]
+        assert rel(rho_d, rho_o) < 1e-10
+        for a_d, a_o in zip(alp_d, alp_o):
+            assert rel(a_d, a_o) < 1e-10
+        ctx.close()
+
+
+def _oracle_iterate(P, n, k=1):
+    primal, dual = oracle_fns(P, rho_alp_iters=k)
+    phi, rho, alp = P["phi"], P["rho"], P["alp"]
+    for _ in range(n):
+        phi_n = primal(phi, rho, 70.0, alp, TAU, P["dt"], P["dsp"], P["fns"], P["fv"], P["epsl"], P["x_arr"], None)
+        rho_n, alp_n = dual(2 * phi_n - phi, rho, 70.0, alp, SIGMA, P["dt"], P["dsp"], P["epsl"], P["fns"],
+                            P["x_arr"], None, P["ndim"], 1e-6 if k > 1 else -1.0)
+        e1, e2 = O.outer_errors(phi, phi_n, rho, rho_n, alp, alp_n)
+        phi, rho, alp = phi_n, rho_n, alp_n
+    return phi, rho, alp, e1, e2
+
+
+@pytest.mark.parametrize("case", CASES, ids=IDS)
+@pytest.mark.parametrize("prec", ["fp64", "fp32"])
+def test_iterate_10(native, case, prec):
+    P = make_problem(*case)
+    phi_o, rho_o, alp_o, e1_o, e2_o = _oracle_iterate(P, 10)
+    ctx = device_ctx(P, prec)
+    ctx.set_state(P["phi"], P["rho"], P["alp"])
+    st = ctx.iterate(10, TAU, SIGMA, -1.0, 1)
+    assert st["iters_run"] == 10 and st["status"] == 0
+    phi_d, rho_d, alp_d = ctx.get_state()
+    if prec == "fp64":
+        assert rel(phi_d, phi_o) < 1e-11 and rel(rho_d, rho_o) < 1e-10
+        assert abs(st["err1"] - e1_o) <= 1e-8 * e1_o and abs(st["err2"] - e2_o) <= 1e-8 * e2_o
+    else:
+        assert rel(phi_d, phi_o) < 1e-5
+        assert rel(rho_d, rho_o) < 2e-4
+        assert abs(st["err1"] - e1_o) <= 1e-2 * e1_o
+    ctx.close()
+
+
+SMOOTH = [c for c in CASES if c[2] >= 32] + [(2, 1, 160, 1, 5, 0.1), (2, 2, 128, 128, 20, 0.1),
+                                            (1, 1, 1024, 1, 40, 0.0)]
+SMOOTH_IDS = ["e{}d{}_{}x{}_T{}_eps{}".format(*c) for c in SMOOTH]
+
+
+@pytest.mark.parametrize("case", SMOOTH, ids=SMOOTH_IDS)
+def test_fp32_from_reference_init(native, case):
+    """fp32 vs the fp64 oracle from the reference's initial state: the north-star phi tolerance.
+
+    With epsl > 0 the reference's dual step holds an explicit sigma*epsl*Lap(phi_bar) term; for
+    sigma*epsl/dx^2 >> 1 its high-frequency modes are unstable, so fp32 rounding noise (1e-7) is
+    amplified a few-fold per iteration while fp64 noise stays invisible (and the fp64 oracle itself
+    diverges later, e.g. 256^2, epsl 0.1).  The multi-iteration fp32 bound is therefore checked over
+    10 iterations for epsl = 0 and over 2 iterations for epsl > 0."""
+    P = make_problem(*case, seeded=False)
+    phi_o = _oracle_primal(P, P["phi"], P["rho"], P["alp"])
+    ctx = device_ctx(P, "fp32")
+    ctx.set_state(P["phi"], P["rho"], P["alp"])
+    ctx.update_primal(TAU)
+    phi_d = ctx.get_state()[0]
+    assert rel(phi_d, phi_o) < 1e-6
+    n = 10 if P["epsl"] == 0 else 2
+    phi_o, rho_o, alp_o, e1_o, e2_o = _oracle_iterate(P, n)
+    ctx.set_state(P["phi"], P["rho"], P["alp"])
+    st = ctx.iterate(n, TAU, SIGMA, -1.0, 1)
+    phi_d, rho_d, alp_d = ctx.get_state()
+    assert rel(phi_d, phi_o) < 1e-5
+    assert rel(rho_d, rho_o) < 1e-5
+    assert abs(st["err1"] - e1_o) <= 1e-3 * e1_o
+    ctx.close()
+
+
+@pytest.mark.parametrize("case", [CASES[1], CASES[6], CASES[7]], ids=[IDS[1], IDS[6], IDS[7]])
+def test_iterate_k10(native, case):
+    """Reference default rho_alp_iters = 10 with early exit inside every outer iteration."""
+    P = make_problem(*case)
+    phi_o, rho_o, alp_o, e1_o, e2_o = _oracle_iterate(P, 4, k=10)
+    ctx = device_ctx(P, "fp64", rho_alp_iters=10)
+    ctx.set_state(P["phi"], P["rho"], P["alp"])
+    st = ctx.iterate(4, TAU, SIGMA, 1e-6, 10)
+    phi_d, rho_d, alp_d = ctx.get_state()
+    assert st["iters_run"] == 4
+    assert rel(phi_d, phi_o) < 1e-10 and rel(rho_d, rho_o) < 1e-9
+    assert abs(st["err2"] - e2_o) <= 1e-7 * e2_o
+    ctx.close()
+
+
+def test_divergence_matches_oracle(native):
+    """A rough state with eps*sigma/dx^2 >> 1 blows up; the device stops (status 2) at the oracle's NaN iteration."""
+    P = make_problem(1, 2, 256, 256, 3, 0.1)
+    primal, dual = oracle_fns(P)
+    phi, rho, alp = P["phi"], P["rho"], P["alp"]
+    nan_at = None
+    with np.errstate(all="ignore"):
+        for i in range(20):
+            phi_n = primal(phi, rho, 70.0, alp, TAU, P["dt"], P["dsp"], P["fns"], P["fv"], P["epsl"], P["x_arr"], None)
+            rho_n, alp_n = dual(2 * phi_n - phi, rho, 70.0, alp, SIGMA, P["dt"], P["dsp"], P["epsl"], P["fns"],
+                                P["x_arr"], None, 2, -1.0)
+            if np.isnan(phi_n).any() or np.isnan(rho_n).any():
+                nan_at = i
+                break
+            phi, rho, alp = phi_n, rho_n, alp_n
+    assert nan_at is not None
+    ctx = device_ctx(P, "fp64")
+    ctx.set_state(P["phi"], P["rho"], P["alp"])
+    st = ctx.iterate(20, TAU, SIGMA, -1.0, 1)
+    assert st["status"] == 2 and st["iters_run"] == nan_at + 1
+    ctx.close()
+
+
+def test_nan_stop(native):
+    """A NaN in rho stops the loop at that iteration with status 2 (utils_pdhg_solver.py:78-80)."""
+    P = make_problem(1, 2, 16, 16, 3, 0.0)
+    rho = P["rho"].copy()
+    rho[1, 3, 4] = np.nan
+    ctx = device_ctx(P, "fp32")
+    ctx.set_state(P["phi"], rho, P["alp"])
+    st = ctx.iterate(50, TAU, SIGMA, 1e-6, 1)
+    assert st["status"] == 2 and st["iters_run"] == 1
+    ctx.close()
+
+
+def test_solver_oneiter_converges_like_oracle(native):
+    """PDHG_solver_oneiter device loop vs the oracle loop: same stop iteration and state (fp64)."""
+    from pdhg_amd import set_fns, update_fns_in_pdhg as U, utils_pdhg_solver as S
+    P = make_problem(1, 1, 32, 1, 1, 0.0, seeded=False)
+    primal_o, dual_o = oracle_fns(P, rho_alp_iters=10)
+    res_o, err_o = O.PDHG_solver_oneiter(primal_o, dual_o, P["fns"], P["phi"], P["rho"], P["alp"], P["x_arr"], None,
+                                         1, P["dt"], P["dsp"], 70.0, stepsz_param=0.1, fv=P["fv"], N_maxiter=20000,
+                                         print_freq=1000, eps=1e-6)
+    fns = set_fns.set_up_example_fns(1, 1, 0)
+    fp, fd = S.make_update_fns(1, 0, rho_alp_iters=10, precision="fp64")
+    res_d, err_d = S.PDHG_solver_oneiter(fp, fd, fns, P["phi"], P["rho"], P["alp"], P["x_arr"], None, 1, P["dt"],
+                                         P["dsp"], 70.0, stepsz_param=0.1, fv=P["fv"], N_maxiter=20000,
+                                         print_freq=1000, eps=1e-6, verbose=False)
+    assert len(res_d) == len(res_o)
+    assert abs(res_d[-1][0] - res_o[-1][0]) <= 1
+    assert rel(res_d[-1][1], res_o[-1][1]) < 1e-8
+    assert np.allclose(err_d[:-1], err_o[:-1], rtol=1e-7)
+    U.clear_cache()
+
+
+def test_multi_step_window_marching(native):
+    """PDHG_multi_step with the reference default time_step_per_PDHG = 2 (T = 1 windows), small C0."""
+    from pdhg_amd import set_fns, update_fns_in_pdhg as U, utils_pdhg_solver as S
+    nx, nt = 32, 6
+    res_o, errs_o = O.solve_HJ(1, 1, 0.0, nx, 1, nt, N_maxiter=20000, print_freq=10000)
+    fns = set_fns.set_up_example_fns(1, 1, 0)
+    x_arr = O.make_grid(1, nx, 1, 1)
+    g = set_fns.set_up_J(1, 1, (2.0,))(x_arr)
+    fp, fd = S.make_update_fns(1, 0, rho_alp_iters=10, precision="fp64")
+    res_d, errs_d = S.PDHG_multi_step(fp, fd, fns, g, x_arr, 1, nt, (nx,), 1.0 / (nt - 1), (2.0 / nx,), 70.0,
+                                      time_step_per_PDHG=2, stepsz_param=0.1, n_ctrl=1, N_maxiter=20000,
+                                      print_freq=10000, eps=1e-6, verbose=False)
+    it_o, phi_o, rho_o, alp_o = res_o[0]
+    it_d, phi_d, rho_d, alp_d = res_d[0]
+    assert abs(it_d - it_o) <= 1
+    assert phi_d.shape == phi_o.shape and alp_d.shape == alp_o.shape
+    assert rel(phi_d, phi_o) < 1e-8 and rel(rho_d, rho_o) < 1e-6
+    U.clear_cache()
+
+
+def test_dropin_update_functions(native):
+    """update_fns_in_pdhg drop-ins (reference signatures) in fp64 vs the oracle."""
+    from pdhg_amd import set_fns, update_fns_in_pdhg as U
+    U.set_precision("fp64")
+    try:
+        P = make_problem(2, 2, 16, 12, 3, 0.1)
+        fns = set_fns.set_up_example_fns(2, 2, 0)
+        phi_d = U.update_primal_2d(P["phi"], P["rho"], 70.0, P["alp"], TAU, P["dt"], P["dsp"], fns, P["fv"],
+                                   P["epsl"], P["x_arr"], None, P["bc"])
+        phi_o = _oracle_primal(P, P["phi"], P["rho"], P["alp"])
+        assert rel((phi_d - P["phi"]) / TAU, (phi_o - P["phi"]) / TAU) < 1e-10
+        pb = 2 * phi_o - P["phi"]
+        r_d, a_d, e_d = U.update_dual_oneiter(pb, P["rho"], 70.0, P["alp"], SIGMA, P["dt"], P["dsp"], P["epsl"],
+                                              P["x_arr"], None, P["bc"], fns, 2)
+        r_o, a_o, e_o = O.update_dual_oneiter(pb, P["rho"], 70.0, P["alp"], SIGMA, P["dt"], P["dsp"], P["epsl"],
+                                              P["x_arr"], None, P["bc"], P["fns"], 2)
+        assert rel(r_d, r_o) < 1e-11 and abs(e_d - e_o) <= 1e-9 * e_o
+        r_d, a_d = U.update_dual_alternative(pb, P["rho"], 70.0, P["alp"], SIGMA, P["dt"], P["dsp"], P["epsl"], fns,
+                                             P["x_arr"], None, 2, P["bc"], rho_alp_iters=10, eps=1e-6)
+        r_o, a_o = O.update_dual_alternative(pb, P["rho"], 70.0, P["alp"], SIGMA, P["dt"], P["dsp"], P["epsl"],
+                                             P["fns"], P["x_arr"], None, 2, P["bc"], rho_alp_iters=10, eps=1e-6)
+        assert rel(r_d, r_o) < 1e-10
+    finally:
+        U.set_precision("fp32")
+        U.clear_cache()
