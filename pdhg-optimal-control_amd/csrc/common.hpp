@@ -43,6 +43,11 @@ struct Ctrl {
   double outer_sums[kNumSums];           // finalized outer (initial vs final) dual sums
 };
 
+// Workgroup barrier that waits only for this wave's LDS operations (lgkmcnt), not for its
+// outstanding global loads/stores: __syncthreads() emits s_waitcnt vmcnt(0) before s_barrier,
+// which would drain register prefetches and pending stores at every FFT pass.
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // Per-launch reductions: one row of kNumSums doubles per workgroup, reduced in
 // a fixed order by a single-workgroup finalize kernel (deterministic, no atomics).
 template <int NS>

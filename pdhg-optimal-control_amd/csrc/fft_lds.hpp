@@ -199,7 +199,7 @@ __device__ C* lds_fft(C* a, C* b, int nl, const FFTPlan& pl, const C* __restrict
       case 3: stockham_pass<C, 3>(src, dst, pl.n, nl, lnl, Ls, pl.pow2, tw); break;
       default: stockham_pass_generic<C>(src, dst, pl.n, nl, lnl, Ls, R, tw); break;
     }
-    __syncthreads();
+    lds_sync();
     C* t = src;
     src = dst;
     dst = t;
@@ -250,7 +250,7 @@ __device__ __forceinline__ C* fixed_passes(C* src, C* dst, const C* __restrict__
     constexpr int rem = N / LS;
     constexpr int R = (rem >= 16) ? 16 : rem;
     fixed_pass<C, N, NL, LS, R>(src, dst, tw);
-    __syncthreads();
+    lds_sync();
     return fixed_passes<C, N, NL, LS * R>(dst, src, tw);
   }
 }
@@ -258,6 +258,65 @@ __device__ __forceinline__ C* fixed_passes(C* src, C* dst, const C* __restrict__
 template <typename C, int N, int NL>
 __device__ __forceinline__ C* lds_fft_fixed(C* a, C* b, const C* __restrict__ tw) {
   return fixed_passes<C, N, NL, 1>(a, b, tw);
+}
+
+// ---------------- in-place multi-line FFT (register-staged, one LDS buffer) ----------------
+// NL lines stored line-major (element e of line l at a[l*N + e]).  Each pass: every thread
+// loads its butterflies into registers, barrier, writes them back in Stockham order, barrier.
+// N, NL, NT compile-time; (N/R)*NL butterflies per pass spread over NT threads.
+template <typename C, int N, int NL, int NT, int LS, int R>
+__device__ __forceinline__ void inplace_pass(C* __restrict__ a, const C* __restrict__ tw) {
+  constexpr int nR = N / R;
+  constexpr int tws = N / (LS * R);
+  constexpr int total = nR * NL;
+  constexpr int PER = (total + NT - 1) / NT;
+  C v[PER][R];
+  int base[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int idx = threadIdx.x + q * NT;
+    base[q] = -1;
+    if (total % NT == 0 || idx < total) {
+      const int l = idx / nR;          // nR is a power of two: shift
+      const int j = idx - l * nR;
+      const int k = j & (LS - 1);
+      const C* s = a + (size_t)l * N + j;
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[q][r] = s[r * nR];
+      if (LS > 1 && k != 0) {
+#pragma unroll
+        for (int r = 1; r < R; ++r) v[q][r] = cmul(v[q][r], tw[r * k * tws]);
+      }
+      base[q] = l * N + (j - k) * R + k;
+    }
+  }
+  lds_sync();
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    if (base[q] >= 0) {
+      dft_any<C, R>(v[q]);
+      C* d = a + base[q];
+#pragma unroll
+      for (int r = 0; r < R; ++r) d[r * LS] = v[q][r];
+    }
+  }
+  lds_sync();
+}
+
+template <typename C, int N, int NL, int NT, int LS>
+__device__ __forceinline__ void inplace_passes(C* a, const C* __restrict__ tw) {
+  if constexpr (LS < N) {
+    constexpr int rem = N / LS;
+    constexpr int R = (rem >= 16) ? 16 : rem;
+    inplace_pass<C, N, NL, NT, LS, R>(a, tw);
+    inplace_passes<C, N, NL, NT, LS * R>(a, tw);
+  }
+}
+
+// Forward FFT in place of NL line-major lines (element e of line l at a[l*N + e]).
+template <typename C, int N, int NL, int NT>
+__device__ __forceinline__ void lds_fft_inplace(C* a, const C* __restrict__ tw) {
+  inplace_passes<C, N, NL, NT, 1>(a, tw);
 }
 
 // FFT policies used as kernel template arguments.

@@ -1,0 +1,408 @@
+// Fast 2-D row-transform kernels (fp32, ny = N a power of two, nx % RW == 0).
+//
+//   k_res_fwdy_fast_2d     continuity residual + forward DHT along y for RW rows at once
+//   k_invy_update_fast_2d  inverse DHT along y + phi update for RW rows at once
+//
+// One workgroup owns an RW-row group of one time row: the RW/2 row pairs are RW/2 complex
+// lines (line-major in LDS) transformed together in place (lds_fft_inplace, RW/2 * N complex).  The
+// blocked spectral layout work[k][b][x][c] then has one contiguous RW*B-float chunk per
+// column block and row group, written / read by RW*B/4 neighbouring lanes with float4
+// (whole 64-B pieces instead of 8-B scattered stores).  The residual reads each input row
+// once per group with float4 loads over a sliding 3-row window (rows x-1, x, x+1).
+#pragma once
+#include "params.hpp"
+
+namespace pdhg {
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ float f4(const float4& v, int e) { return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w; }
+__device__ __forceinline__ void f4set(float4& v, int e, float x) {
+  if (e == 0) v.x = x; else if (e == 1) v.y = x; else if (e == 2) v.z = x; else v.w = x;
+}
+__device__ __forceinline__ float4 z4() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+
+template <int EGNO>
+__device__ __forceinline__ float m1f(float rho, float alp, float a) {   // (rho + 1e-4) f(alp)^+
+  return (rho + 1e-4f) * fpos<float>(fval<float, EGNO>(alp, a));
+}
+template <int EGNO>
+__device__ __forceinline__ float m2f(float rho, float alp, float a) {   // (rho + 1e-4) f(alp)^-
+  return (rho + 1e-4f) * fneg<float>(fval<float, EGNO>(alp, a));
+}
+
+// grid: T * nx/RW row-group tasks (XCD-aware); block NT = min(1024, N/4); LDS RW/2 * N * 8 B.
+template <int EGNO, int N, int RW, int NT>
+__global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const float2* __restrict__ twy) {
+  using C = float2;
+  constexpr int NL = RW / 2;
+  constexpr int GPT = (N / 4) / NT;   // float4 y-groups per thread
+  if (p.ctrl->done) return;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  C* A = reinterpret_cast<C*>(smem_raw);
+  const int cur = p.ctrl->cur;
+  const int nx = p.nx, T = p.T;
+  const int ngx = nx / RW;
+  const int task = xcd_remap(blockIdx.x, gridDim.x);
+  const int j = task / ngx;
+  const int x0 = (task - j * ngx) * RW;
+  const size_t plane = (size_t)nx * N;
+  const float* rj = p.rho[cur] + (size_t)j * plane;
+  const float* rn = (j + 1 < T) ? p.rho[cur] + (size_t)(j + 1) * plane : nullptr;
+  const float* a1x = p.alp[cur][0] + (size_t)j * plane;
+  const float* a2x = p.alp[cur][1] + (size_t)j * plane;
+  const float* a1y = (EGNO == 3) ? nullptr : p.alp[cur][2] + (size_t)j * plane;
+  const float* a2y = (EGNO == 3) ? nullptr : p.alp[cur][3] + (size_t)j * plane;
+  const float cdt = (j == T - 1) ? p.c_over_dt : 0.f;
+  const bool use_eps = p.epsl != 0.f;
+
+#pragma unroll
+  for (int gi = 0; gi < GPT; ++gi) {
+    const int y = 4 * (threadIdx.x + gi * NT);
+    const int ym = nb_index(y - 1, N, p.bcy), yp = nb_index(y + 4, N, p.bcy);
+    float4 ay4 = z4();
+    float aym = 0.f, ayp = 0.f;
+    if constexpr (EGNO != 3) {
+      ay4 = ld4(p.ay + y);
+      aym = ym >= 0 ? p.ay[ym] : 0.f;
+      ayp = yp >= 0 ? p.ay[yp] : 0.f;
+    }
+    const int xm = nb_index(x0 - 1, nx, p.bcx);
+    float4 r_m = xm >= 0 ? ld4(rj + (size_t)xm * N + y) : z4();
+    float4 a1_m = xm >= 0 ? ld4(a1x + (size_t)xm * N + y) : z4();
+    float ax_m = xm >= 0 ? p.ax[xm] : 0.f;
+    float4 r_c = ld4(rj + (size_t)x0 * N + y);
+    float4 a1_c = ld4(a1x + (size_t)x0 * N + y);
+    float4 a2_c = ld4(a2x + (size_t)x0 * N + y);
+    float ax_c = p.ax[x0];
+#pragma unroll 2
+    for (int r = 0; r < RW; ++r) {
+      const int x = x0 + r;
+      const int xp = nb_index(x + 1, nx, p.bcx);
+      const size_t ro = (size_t)x * N;
+      const float4 r_p = xp >= 0 ? ld4(rj + (size_t)xp * N + y) : z4();
+      const float4 a2_p = xp >= 0 ? ld4(a2x + (size_t)xp * N + y) : z4();
+      const float4 a1_n = (r + 1 < RW && xp >= 0) ? ld4(a1x + (size_t)xp * N + y) : z4();
+      const float ax_p = xp >= 0 ? p.ax[xp] : 0.f;
+      const float4 rn4 = rn ? ld4(rn + ro + y) : z4();
+      float4 a1y4 = z4(), a2y4 = z4();
+      float a1y_m = 0.f, a2y_p = 0.f;
+      if constexpr (EGNO != 3) {
+        a1y4 = ld4(a1y + ro + y);
+        a2y4 = ld4(a2y + ro + y);
+        a1y_m = ym >= 0 ? a1y[ro + ym] : 0.f;
+        a2y_p = yp >= 0 ? a2y[ro + yp] : 0.f;
+      }
+      const float r_ym = ym >= 0 ? rj[ro + ym] : 0.f;
+      const float r_yp = yp >= 0 ? rj[ro + yp] : 0.f;
+      float m1y[6], m2y[6], rr[6];   // index e+1 for e = -1..4
+      rr[0] = r_ym;
+      rr[5] = r_yp;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rr[e + 1] = f4(r_c, e);
+      if constexpr (EGNO == 3) {
+        const float f1 = fpos<float>(ax_c), f2 = fneg<float>(ax_c);
+#pragma unroll
+        for (int e = 0; e < 6; ++e) {
+          m1y[e] = (rr[e] + 1e-4f) * f1;
+          m2y[e] = (rr[e] + 1e-4f) * f2;
+        }
+        if (ym < 0) m1y[0] = 0.f;
+        if (yp < 0) m2y[5] = 0.f;
+      } else {
+        m1y[0] = ym >= 0 ? m1f<EGNO>(r_ym, a1y_m, aym) : 0.f;
+        m2y[5] = yp >= 0 ? m2f<EGNO>(r_yp, a2y_p, ayp) : 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          m1y[e + 1] = m1f<EGNO>(rr[e + 1], f4(a1y4, e), f4(ay4, e));
+          m2y[e + 1] = m2f<EGNO>(rr[e + 1], f4(a2y4, e), f4(ay4, e));
+        }
+      }
+      float out[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float r0 = rr[e + 1];
+        float res = (f4(rn4, e) - r0) * p.inv_dt;
+        if (use_eps) {
+          res = res + p.epsl * ((f4(r_p, e) + f4(r_m, e) - 2.f * r0) * p.inv_dx2);
+          res = res + p.epsl * ((rr[e + 2] + rr[e] - 2.f * r0) * p.inv_dy2);
+        }
+        const float m1x_c = m1f<EGNO>(r0, f4(a1_c, e), ax_c);
+        const float m1x_m = (r > 0 || xm >= 0) ? m1f<EGNO>(f4(r_m, e), f4(a1_m, e), ax_m) : 0.f;
+        const float m2x_c = m2f<EGNO>(r0, f4(a2_c, e), ax_c);
+        const float m2x_p = xp >= 0 ? m2f<EGNO>(f4(r_p, e), f4(a2_p, e), ax_p) : 0.f;
+        const float div = (m1x_c - m1x_m) * p.inv_dx + (m2x_p - m2x_c) * p.inv_dx +
+                          (m1y[e + 1] - m1y[e]) * p.inv_dy + (m2y[e + 2] - m2y[e + 1]) * p.inv_dy;
+        out[e] = res - div + cdt;
+      }
+      // residual row x -> line r/2, real (even r) or imaginary (odd r) part; 4 contiguous elements
+      float* Af = reinterpret_cast<float*>(A + (size_t)(r >> 1) * N + y) + (r & 1);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Af[2 * e] = out[e];
+      // slide the window
+      r_m = r_c;
+      a1_m = a1_c;
+      ax_m = ax_c;
+      r_c = r_p;
+      a1_c = a1_n;
+      a2_c = a2_p;
+      ax_c = ax_p;
+    }
+  }
+  __syncthreads();
+  lds_fft_inplace<C, N, NL, NT>(A, twy);
+  // Hartley unpack -> blocked layout: chunk (j, b, x0..x0+RW-1, 0..B-1) = RW*B contiguous floats
+  const int B = p.B;
+  const int CS4 = RW * B / 4;                 // float4 per chunk
+  const int nb = p.nb;
+  float* wk = p.work + (size_t)j * nb * nx * B;
+  for (int t = threadIdx.x; t < nb * CS4; t += NT) {
+    const int b = t / CS4, part = t - b * CS4;
+    float4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int f = part * 4 + e;
+      const int r = f / B, c = f - r * B;
+      const int ky = b * B + c;
+      float ha = 0.f, hb = 0.f;
+      if (ky < N) hartley_pair<C, float>(A + (size_t)(r >> 1) * N, N, 1, ky, 0, ha, hb);
+      f4set(v, e, (r & 1) ? hb : ha);
+    }
+    st4(wk + ((size_t)b * nx + x0) * B + part * 4, v);
+  }
+}
+
+// G workgroups striding over the T * nx/RW row-group tasks; block NT; LDS RW/2 * N * 8 B.
+// sums: [0] sum (phi'-phi)^2, [1] sum phi^2 (old), [2] sum phi'^2
+template <int N, int RW, int NT>
+__global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const float2* __restrict__ twy) {
+  using C = float2;
+  constexpr int NL = RW / 2;
+  constexpr int GPT = (N / 4) / NT;
+  if (p.ctrl->done) return;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  C* A = reinterpret_cast<C*>(smem_raw);
+  float* Af = reinterpret_cast<float*>(A);
+  const int nx = p.nx, B = p.B, nb = p.nb;
+  const int ngx = nx / RW;
+  const int ntask = ngx * p.T;
+  const size_t plane = (size_t)nx * N;
+  const float scale = p.tau * p.inv_n;
+  const int CS4 = RW * B / 4;
+  double s[3] = {0.0, 0.0, 0.0};
+  for (int task = xcd_remap(blockIdx.x, gridDim.x); task < ntask; task += gridDim.x) {
+    const int j = task / ngx;
+    const int x0 = (task - j * ngx) * RW;
+    const float* wk = p.work + (size_t)j * nb * nx * B;
+    for (int t = threadIdx.x; t < nb * CS4; t += NT) {
+      const int b = t / CS4, part = t - b * CS4;
+      const float4 v = ld4(wk + ((size_t)b * nx + x0) * B + part * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int f = part * 4 + e;
+        const int r = f / B, c = f - r * B;
+        const int ky = b * B + c;
+        if (ky < N) Af[((size_t)(r >> 1) * N + ky) * 2 + (r & 1)] = f4(v, e);
+      }
+    }
+    __syncthreads();
+    lds_fft_inplace<C, N, NL, NT>(A, twy);
+    float* phi = p.phi + (size_t)(j + 1) * plane;
+    float* pbar = p.phibar + (size_t)(j + 1) * plane;
+#pragma unroll
+    for (int gi = 0; gi < GPT; ++gi) {
+      const int y = 4 * (threadIdx.x + gi * NT);
+#pragma unroll 1
+      for (int r = 0; r < RW; ++r) {
+        const C* Z = A + (size_t)(r >> 1) * N;
+        const size_t idx = (size_t)(x0 + r) * N + y;
+        const float4 old = ld4(phi + idx);
+        float4 nw, pb;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float a, b2;
+          hartley_pair<C, float>(Z, N, 1, y + e, 0, a, b2);
+          const float o = f4(old, e);
+          const float n = o + scale * ((r & 1) ? b2 : a);
+          f4set(nw, e, n);
+          f4set(pb, e, 2.f * n - o);
+          const float d = n - o;
+          s[0] += (double)d * (double)d;
+          s[1] += (double)o * (double)o;
+          s[2] += (double)n * (double)n;
+        }
+        st4(phi + idx, nw);
+        st4(pbar + idx, pb);
+      }
+    }
+    __syncthreads();
+  }
+  block_reduce_store<3>(s, p.partials, blockIdx.x);
+}
+
+}  // namespace pdhg
+
+namespace pdhg {
+
+// expm1(x) for x <= 0 in fp32 without libm's range reduction: degree-7 Taylor for x > -1/4
+// (relative error < 2e-9), __expf(x) - 1 below (no cancellation there: |e^x - 1| > 0.22).
+__device__ __forceinline__ float expm1_neg(float x) {
+  const float p = x * (1.f + x * (0.5f + x * (1.f / 6 + x * (1.f / 24 + x * (1.f / 120 + x * (1.f / 720 + x * (1.f / 5040)))))));
+  return x > -0.25f ? p : __expf(x) - 1.f;
+}
+
+// Column-block x-transform + Thomas in t (fp32, nx = N a power of two).
+// A thread owns IT items (kx, l) of the block's NL complex lines; item (kx, l) carries the two
+// modes (kx, 2l) and (kx, 2l+1), which are exactly the real and imaginary parts of line l's
+// element kx, so the b' / x carries map 1:1 onto the in-place line-major FFT buffer.
+// LDS: FFT buffer N*NL complex + per-item carries theta, E, b' as float2 (3 * N*NL * 8 B);
+// N*NL = 4096 -> 128 KiB.  Barriers are LDS-only (lds_sync) so the register prefetch of the
+// next plane and the b'/x stores stay in flight across the FFT passes.
+// grid: nb; block NT.
+template <int N, int NL, int NT>
+__global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const float2* __restrict__ twx) {
+  using C = float2;
+  constexpr int IT = N * NL / NT;
+  constexpr int B = 2 * NL;
+  constexpr int NI = N * NL;            // items per block
+  constexpr int lnl = (NL == 1) ? 0 : (NL == 2) ? 1 : (NL == 4) ? 2 : 3;
+  if (p.ctrl->done) return;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  C* A = reinterpret_cast<C*>(smem_raw);
+  C* sth = A + NI;
+  C* sE = sth + NI;
+  C* sbp = sE + NI;
+  const int T = p.T, tid = threadIdx.x;
+  const int b = blockIdx.x;
+  constexpr int M = N * B;
+  float* wb = p.work + (size_t)b * M;
+  const size_t kstride = (size_t)p.nb * M;
+  const float ae = p.ae, inv_ae = 1.f / ae;
+  C pf[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int item = tid + i * NT;
+    const int kx = item >> lnl, l = item & (NL - 1);
+    float t2[2], e2[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float d0 = p.C - p.lamx[kx] - p.lamy[b * B + 2 * l + h];
+      const float delta = d0 / (2.f * ae);
+      t2[h] = log1pf(delta + sqrtf(delta * (delta + 2.f)));   // cosh(th) = 1 + d0/(2 ae)
+      e2[h] = expm1f(-2.f * t2[h]);                            // E_1, E_m = expm1(-2 th m)
+    }
+    sth[item] = make_float2(t2[0], t2[1]);
+    sE[item] = make_float2(e2[0], e2[1]);
+    sbp[item] = make_float2(0.f, 0.f);
+    pf[i] = reinterpret_cast<const C*>(wb)[item];
+  }
+  // ---------------- forward: DHT_x + elimination ----------------
+  for (int k = 0; k < T; ++k) {
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int item = tid + i * NT;
+      A[(item & (NL - 1)) * N + (item >> lnl)] = pf[i];
+    }
+    if (k + 1 < T) {
+      const C* sn = reinterpret_cast<const C*>(wb + (size_t)(k + 1) * kstride);
+#pragma unroll
+      for (int i = 0; i < IT; ++i) pf[i] = sn[tid + i * NT];
+    }
+    lds_sync();
+    lds_fft_inplace<C, N, NL, NT>(A, twx);
+    C* dst = reinterpret_cast<C*>(wb + (size_t)k * kstride);
+    const bool last = (k == T - 1);
+    const float kk1 = (float)(k + 1), kk2 = (float)(k + 2);
+#pragma unroll 2
+    for (int i = 0; i < IT; ++i) {
+      const int item = tid + i * NT;
+      const int kx = item >> lnl, l = item & (NL - 1);
+      float hv[2];
+      hartley_pair<C, float>(A + (size_t)l * N, N, 1, kx, 0, hv[0], hv[1]);
+      const C t2 = sth[item];
+      C e2 = sE[item];
+      C b2 = sbp[item];
+      const float tt[2] = {t2.x, t2.y};
+      float ee[2] = {e2.x, e2.y}, bb[2] = {b2.x, b2.y};
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float t = tt[h];
+        if (!last) {
+          // 1/u_k = e^-th E_{k+1} / (ae E_{k+2})   (closed form of the Thomas pivots)
+          const float E2 = expm1_neg(-2.f * t * kk2);
+          const float g = (t > 0.f) ? __expf(-t) * ee[h] * __frcp_rn(E2) : kk1 / kk2;
+          bb[h] = (hv[h] * inv_ae + bb[h]) * g;
+          ee[h] = E2;
+        } else {
+          // Neumann last row: u_{T-1} = d0 + ae expm1(-th)(1 + e^{-th(2T-1)}) / E_T
+          const float d0 = p.C - p.lamx[kx] - p.lamy[b * B + 2 * l + h];
+          const float u = (t > 0.f) ? d0 + ae * expm1f(-t) * (1.f + expf(-t * (float)(2 * T - 1))) /
+                                               expm1f(-2.f * t * (float)T)
+                                    : d0 + ae / (float)T;
+          bb[h] = (hv[h] + ae * bb[h]) / u;
+        }
+      }
+      sE[item] = make_float2(ee[0], ee[1]);
+      sbp[item] = make_float2(bb[0], bb[1]);
+      if (!last) dst[item] = make_float2(bb[0], bb[1]);
+    }
+    lds_sync();
+  }
+  // ---------------- backward: substitution + inverse DHT_x ----------------
+  // x_k = b'_k + g_k x_{k+1},  g_k = ae/u_k = e^-th E_{k+1}/E_{k+2}
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int item = tid + i * NT;
+    const C t2 = sth[item];
+    sE[item] = make_float2(expm1f(-2.f * t2.x * (float)T), expm1f(-2.f * t2.y * (float)T));   // E_{(T-2)+2}
+  }
+  if (T >= 2) {
+    const C* s0 = reinterpret_cast<const C*>(wb + (size_t)(T - 2) * kstride);
+#pragma unroll
+    for (int i = 0; i < IT; ++i) pf[i] = s0[tid + i * NT];
+  }
+  for (int k = T - 1; k >= 0; --k) {
+    const float kk1 = (float)(k + 1), kk2 = (float)(k + 2);
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int item = tid + i * NT;
+      C x2 = sbp[item];
+      if (k < T - 1) {
+        const C t2 = sth[item];
+        const C e2 = sE[item];
+        const float tt[2] = {t2.x, t2.y}, ee[2] = {e2.x, e2.y}, pv[2] = {pf[i].x, pf[i].y};
+        float xx[2] = {x2.x, x2.y}, en[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float t = tt[h];
+          const float E1 = expm1_neg(-2.f * t * kk1);
+          const float g = (t > 0.f) ? __expf(-t) * E1 * __frcp_rn(ee[h]) : kk1 / kk2;
+          xx[h] = pv[h] + g * xx[h];
+          en[h] = E1;
+        }
+        x2 = make_float2(xx[0], xx[1]);
+        sE[item] = make_float2(en[0], en[1]);
+        sbp[item] = x2;
+      }
+      A[(item & (NL - 1)) * N + (item >> lnl)] = x2;
+    }
+    if (k >= 1) {
+      const C* sn = reinterpret_cast<const C*>(wb + (size_t)(k - 1) * kstride);
+#pragma unroll
+      for (int i = 0; i < IT; ++i) pf[i] = sn[tid + i * NT];
+    }
+    lds_sync();
+    lds_fft_inplace<C, N, NL, NT>(A, twx);
+    C* wk = reinterpret_cast<C*>(wb + (size_t)k * kstride);
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int item = tid + i * NT;
+      float ha, hb;
+      hartley_pair<C, float>(A + (size_t)(item & (NL - 1)) * N, N, 1, item >> lnl, 0, ha, hb);
+      wk[item] = make_float2(ha, hb);
+    }
+    lds_sync();
+  }
+}
+
+}  // namespace pdhg

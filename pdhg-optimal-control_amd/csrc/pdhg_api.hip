@@ -8,11 +8,13 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/pdhg.h"
 #include "kernels_1d.hpp"
 #include "kernels_2d.hpp"
+#include "kernels_2d_fast.hpp"
 #include "kernels_common.hpp"
 
 using namespace pdhg;
@@ -97,6 +99,12 @@ struct Impl : ImplBase {
   int NT2 = 512;
   int gx1 = 0, gx4 = 0, g4 = 1, gx5 = 0, g5 = 1, g_outer = 1;
   size_t lds_res = 0, lds_xt = 0;
+  // fast row kernels (fp32, power-of-two ny): RW rows per workgroup, NTf threads
+  bool fast_rows = false;
+  bool fast_xt = false;            // fp32 power-of-two nx: k_precond_xt_fast_2d
+  size_t lds_fast_xt = 0;
+  int RWf = 8, NTf = 1024, g_fast_upd = 1;
+  size_t lds_fast = 0;
   size_t partial_rows = 0;
   bool primal_done = false;
   int stop_conv = 1, stop_nan = 1;   // reference stop rules (utils_pdhg_solver.py:74-80)
@@ -194,6 +202,19 @@ struct Impl : ImplBase {
       g4 = 1;
       gx5 = (ny + 255) / 256;
       g5 = std::max(1, std::min(T * nx, 8192 / std::max(1, gx5)));
+      if (sizeof(R) == 4 && plx.pow2 && nx * (B / 2) == 4096 && nx >= 512) {
+        fast_xt = true;
+        lds_fast_xt = (size_t)4 * 4096 * sizeof(C);   // FFT buffer + theta, E, b' (float2 per item)
+      }
+      if (sizeof(R) == 4 && ply.pow2 && ny >= 256 && ny <= 8192) {
+        RWf = (ny == 8192) ? 4 : 8;
+        NTf = std::min(1024, ny / 4);
+        if (nx % RWf == 0 && (RWf * B) % 4 == 0) {
+          fast_rows = true;
+          lds_fast = (size_t)(RWf / 2) * ny * sizeof(C);
+          g_fast_upd = std::min((nx / RWf) * T, 2048);
+        }
+      }
     } else {
       p.B = 1;
       p.lB = 0;
@@ -208,7 +229,7 @@ struct Impl : ImplBase {
       g5 = std::max(1, std::min(T, 8192 / std::max(1, gx5)));
     }
     g_outer = 2048;
-    partial_rows = std::max<size_t>({(size_t)gx4 * g4, (size_t)gx5 * g5, (size_t)g_outer, 1});
+    partial_rows = std::max<size_t>({(size_t)gx4 * g4, (size_t)gx5 * g5, (size_t)g_outer, (size_t)g_fast_upd, 1});
 
     // ---- device buffers ----
     const size_t npl = plane();
@@ -312,6 +333,29 @@ struct Impl : ImplBase {
     }
     return fn(FFTRt{pl, 1});
   }
+  // fast row-kernel dispatch on ny (compile-time N, RW, NT)
+  template <typename Fn>
+  int with_fast_rows(Fn&& fn) {
+    if constexpr (sizeof(R) == 4) {
+      switch (pb.ny) {
+        case 256: return fn(std::integral_constant<int, 256>{}, std::integral_constant<int, 8>{},
+                            std::integral_constant<int, 64>{});
+        case 512: return fn(std::integral_constant<int, 512>{}, std::integral_constant<int, 8>{},
+                            std::integral_constant<int, 128>{});
+        case 1024: return fn(std::integral_constant<int, 1024>{}, std::integral_constant<int, 8>{},
+                             std::integral_constant<int, 256>{});
+        case 2048: return fn(std::integral_constant<int, 2048>{}, std::integral_constant<int, 8>{},
+                             std::integral_constant<int, 512>{});
+        case 4096: return fn(std::integral_constant<int, 4096>{}, std::integral_constant<int, 8>{},
+                             std::integral_constant<int, 1024>{});
+        case 8192: return fn(std::integral_constant<int, 8192>{}, std::integral_constant<int, 4>{},
+                             std::integral_constant<int, 1024>{});
+        default: break;
+      }
+    }
+    return fail(PDHG_ERR_UNSUPPORTED, "no fast row kernel for ny=%d", pb.ny);
+  }
+
   template <typename Fn>
   int with_xt_fft(Fn&& fn) {
     const int nl = kp.B / 2;
@@ -357,7 +401,32 @@ struct Impl : ImplBase {
     const int T = pb.T;
     if (pb.ndim == 2) {
       int rc;
-      {
+      if (fast_rows) {
+        ProfScope ps(this, "residual");
+        rc = with_fast_rows([&](auto Nc, auto RWc, auto NTc) {
+          constexpr int N_ = decltype(Nc)::value, RW_ = decltype(RWc)::value, NT_ = decltype(NTc)::value;
+          const dim3 g((pb.nx / RW_) * T);
+          int r2;
+          if constexpr (sizeof(R) == 4) {
+            switch (pb.egno) {
+              case 1:
+                if ((r2 = ensure_lds(k_res_fwdy_fast_2d<1, N_, RW_, NT_>, lds_fast))) return r2;
+                hipLaunchKernelGGL((k_res_fwdy_fast_2d<1, N_, RW_, NT_>), g, dim3(NT_), lds_fast, stream, p, twy);
+                break;
+              case 2:
+                if ((r2 = ensure_lds(k_res_fwdy_fast_2d<2, N_, RW_, NT_>, lds_fast))) return r2;
+                hipLaunchKernelGGL((k_res_fwdy_fast_2d<2, N_, RW_, NT_>), g, dim3(NT_), lds_fast, stream, p, twy);
+                break;
+              default:
+                if ((r2 = ensure_lds(k_res_fwdy_fast_2d<3, N_, RW_, NT_>, lds_fast))) return r2;
+                hipLaunchKernelGGL((k_res_fwdy_fast_2d<3, N_, RW_, NT_>), g, dim3(NT_), lds_fast, stream, p, twy);
+                break;
+            }
+          }
+          return (int)PDHG_OK;
+        });
+        if (rc) return rc;
+      } else {
         ProfScope ps(this, "residual");
         dim3 g(gx1);
         rc = with_line_fft(ply, [&](auto f) {
@@ -381,7 +450,27 @@ struct Impl : ImplBase {
         });
         if (rc) return rc;
       }
-      {
+      if (fast_xt) {
+        ProfScope ps(this, "precond");
+        rc = PDHG_OK;
+        if constexpr (sizeof(R) == 4) {
+          const dim3 g(p.nb);
+          auto go = [&](auto kern) -> int {
+            int r2;
+            if ((r2 = ensure_lds(kern, lds_fast_xt))) return r2;
+            hipLaunchKernelGGL(kern, g, dim3(512), lds_fast_xt, stream, p, twx);
+            return (int)PDHG_OK;
+          };
+          switch (pb.nx) {
+            case 4096: rc = go(k_precond_xt_fast_2d<4096, 1, 512>); break;
+            case 2048: rc = go(k_precond_xt_fast_2d<2048, 2, 512>); break;
+            case 1024: rc = go(k_precond_xt_fast_2d<1024, 4, 512>); break;
+            case 512: rc = go(k_precond_xt_fast_2d<512, 8, 512>); break;
+            default: rc = fail(PDHG_ERR_UNSUPPORTED, "no fast x kernel for nx=%d", pb.nx);
+          }
+        }
+        if (rc) return rc;
+      } else {
         ProfScope ps(this, "precond");
         dim3 g(p.nb);
         rc = with_xt_fft([&](auto f) {
@@ -393,7 +482,22 @@ struct Impl : ImplBase {
         });
         if (rc) return rc;
       }
-      {
+      int upd_rows = gx4 * g4;
+      if (fast_rows) {
+        ProfScope ps(this, "update");
+        upd_rows = g_fast_upd;
+        rc = with_fast_rows([&](auto Nc, auto RWc, auto NTc) {
+          constexpr int N_ = decltype(Nc)::value, RW_ = decltype(RWc)::value, NT_ = decltype(NTc)::value;
+          int r2;
+          if constexpr (sizeof(R) == 4) {
+            if ((r2 = ensure_lds(k_invy_update_fast_2d<N_, RW_, NT_>, lds_fast))) return r2;
+            hipLaunchKernelGGL((k_invy_update_fast_2d<N_, RW_, NT_>), dim3(g_fast_upd), dim3(NT_), lds_fast, stream,
+                               p, twy);
+          }
+          return (int)PDHG_OK;
+        });
+        if (rc) return rc;
+      } else {
         ProfScope ps(this, "update");
         rc = with_line_fft(ply, [&](auto f) {
           using F = decltype(f);
@@ -404,7 +508,7 @@ struct Impl : ImplBase {
         });
         if (rc) return rc;
       }
-      hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(256), 0, stream, p.partials, gx4 * g4, row0_sq, p.ctrl);
+      hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(256), 0, stream, p.partials, upd_rows, row0_sq, p.ctrl);
     } else {
       int rc;
       {

@@ -1,0 +1,16 @@
+#!/bin/bash
+# rocprofv3 kernel trace + PMC passes for one bench config (run on the GPU box via gpurun).
+# usage: scripts/profile.sh <config> <tag>   -> gpurun_out/prof_<tag>/...
+set -o pipefail
+CFG=${1:-c3}; TAG=${2:-$CFG}
+REPO=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$REPO/gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+ARGS="$REPO/bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $ARGS > "$OUT/trace.log" 2>&1 || exit 1
+for C in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
+  N=$(echo $C | tr ' ' '_')
+  timeout -k 10 400 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_$N" -o run -- python3 $ARGS > "$OUT/pmc_$N.log" 2>&1 || exit 1
+done
+echo "profile done: $OUT"

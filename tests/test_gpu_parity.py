@@ -34,6 +34,7 @@ CASES = [
     (1, 2, 32, 32, 1, 0.0),     # T = 1
     (2, 2, 64, 48, 8, 0.1),
     (1, 2, 256, 256, 3, 0.0),   # fixed-size FFT paths (rows 256, x-slab 256 x 8 lines) in fp32
+    (2, 2, 512, 256, 2, 0.0),   # fp32 fast row kernels (8-row groups, in-place 4-line FFT)
 ]
 IDS = ["e{}d{}_{}x{}_T{}_eps{}".format(*c) for c in CASES]
 
@@ -148,7 +149,8 @@ def test_iterate_10(native, case, prec):
 
 
 SMOOTH = [c for c in CASES if c[2] >= 32] + [(2, 1, 160, 1, 5, 0.1), (2, 2, 128, 128, 20, 0.1),
-                                            (1, 1, 1024, 1, 40, 0.0)]
+                                            (1, 1, 1024, 1, 40, 0.0), (1, 2, 1024, 512, 2, 0.0),
+                                            (2, 2, 256, 1024, 3, 0.0)]
 SMOOTH_IDS = ["e{}d{}_{}x{}_T{}_eps{}".format(*c) for c in SMOOTH]
 
 
