@@ -1,0 +1,114 @@
+"""Host-side logic on CPU: persistence, the problem plugin, and the drivers' control flow.
+
+The driver tests pass the oracle's update callables into the product's PDHG_solver_oneiter /
+PDHG_multi_step (their generic "callables" loop), so the window marching, warm start, result
+assembly and NaN step back-off logic of the product is checked against the oracle's driver on the
+same arithmetic (utils_pdhg_solver.py:9-225)."""
+import numpy as np
+import pytest
+
+import pdhg_oracle as O
+from pdhg_amd import set_fns, solver, utils_pdhg_solver as S, utils_precond
+
+rng = np.random.default_rng(1)
+
+
+def test_save_load_roundtrip(tmp_path):
+    res = [(12, rng.standard_normal((3, 4)), rng.standard_normal((2, 4)), rng.standard_normal((2, 2, 4, 1)))]
+    errs = [np.array([[1e-3, 2e-3], [1e-7, 3e-7]])]
+    solver.save(str(tmp_path), "sol", (res, errs))
+    r2, e2 = solver.load_solution(str(tmp_path), "sol")
+    assert r2[0][0] == 12 and isinstance(r2[0], tuple)
+    for a, b in zip(res[0][1:], r2[0][1:]):
+        assert np.array_equal(a, b)
+    assert np.array_equal(errs[0], e2[0])
+    mid = [7, [rng.standard_normal((2, 4))], [rng.standard_normal((1, 4))], [rng.standard_normal((2, 1, 4, 1))], []]
+    solver.save(str(tmp_path), "mid", mid)
+    m2 = solver.load_middle_solution(str(tmp_path), "mid")
+    assert m2[0] == 7 and np.array_equal(m2[1][0], mid[1][0]) and m2[4] == []
+
+
+@pytest.mark.parametrize("egno,ndim", [(1, 1), (2, 1), (1, 2), (2, 2), (3, 2)])
+def test_plugin_matches_oracle(egno, ndim):
+    nx, ny, T = 6, 5, 3
+    x = O.make_grid(ndim, nx, ny, egno)
+    po, pp = O.set_up_example_fns(egno, ndim, 0), set_fns.set_up_example_fns(egno, ndim, 0)
+    assert pp.spec["egno"] == egno and "alp_update_fn" in pp._fields
+    nc = 1 if (ndim == 1 or egno == 3) else 2
+    sp = (T, nx) if ndim == 1 else (T, nx, ny)
+    alp = tuple(rng.standard_normal(sp + (nc,)) for _ in range(2 if ndim == 1 else 4))
+    if ndim == 2 and egno != 3:                      # dead components are zero in the examples
+        alp[0][..., 1] = alp[1][..., 1] = alp[2][..., 0] = alp[3][..., 0] = 0
+    if egno == 3:
+        alp = alp[:2] + (np.zeros_like(alp[0]), np.zeros_like(alp[0]))
+    rho = rng.uniform(1, 2, sp)
+    assert np.allclose(po.f_fn(alp[0], x, None), pp.f_fn(alp[0], x, None))
+    assert np.allclose(po.numerical_L_fn(alp, x, None), pp.numerical_L_fn(alp, x, None))
+    if ndim == 1:
+        D = rng.standard_normal(sp), rng.standard_normal(sp)
+        for a, b in zip(po.alp_update_fn(alp, *D, rho, 0.15, x, None), pp.alp_update_fn(alp, *D, rho, 0.15, x, None)):
+            assert np.allclose(a, b)
+    else:
+        D = tuple(rng.standard_normal(sp) for _ in range(4))
+        for a, b in zip(po.alp_update_fn(alp, D, rho, 0.15, x, None), pp.alp_update_fn(alp, D, rho, 0.15, x, None)):
+            assert np.allclose(a, b)
+    po_J = O.set_up_J(egno, ndim, (2.0, 2.0))(x)
+    assert np.allclose(po_J, set_fns.set_up_J(egno, ndim, (2.0, 2.0))(x))
+
+
+def test_symbol_matches_oracle():
+    assert np.allclose(utils_precond.compute_Dxx_fft_fv(1, (12,), (0.2,), 0), O.compute_Dxx_fft_fv(1, (12,), (0.2,), 0))
+    assert np.allclose(utils_precond.compute_Dxx_fft_fv(2, (8, 6), (0.2, 0.3), (0, 0)),
+                       O.compute_Dxx_fft_fv(2, (8, 6), (0.2, 0.3), (0, 0)))
+
+
+def _setup(nx=12, nt=5):
+    x = O.make_grid(1, nx, 1, 1)
+    fns = O.set_up_example_fns(1, 1, 0)
+    g = O.set_up_J(1, 1, (2.0,))(x)
+    fv = O.compute_Dxx_fft_fv(1, (nx,), (2.0 / nx,), 0)
+    return x, fns, g, fv
+
+
+def test_multi_step_driver_matches_oracle_driver():
+    nx, nt = 12, 5
+    x, fns, g, fv = _setup(nx, nt)
+    primal, dual = O.make_update_fns(1, 0, rho_alp_iters=10)
+    kw = dict(time_step_per_PDHG=3, stepsz_param=0.1, n_ctrl=1, fv=fv, N_maxiter=3000, print_freq=400, eps=1e-6)
+    res_o, errs_o = O.PDHG_multi_step(primal, dual, fns, g, x, 1, nt, (nx,), 0.25, (2.0 / nx,), 70.0, **kw)
+    res_p, errs_p = S.PDHG_multi_step(primal, dual, fns, g, x, 1, nt, (nx,), 0.25, (2.0 / nx,), 70.0, verbose=False,
+                                      **kw)
+    assert res_p[0][0] == res_o[0][0]
+    for a, b in zip(res_p[0][1:], res_o[0][1:]):
+        assert a.shape == b.shape and np.allclose(a, b, rtol=0, atol=0)
+    assert len(errs_p) == len(errs_o)
+    for a, b in zip(errs_p, errs_o):
+        assert np.array_equal(a, b)
+
+
+def test_nan_backoff_sequence_matches_oracle():
+    """A primal that blows up for step sizes above 0.055 triggers the back-off of utils_pdhg_solver.py:174-187."""
+    nx, nt = 8, 3
+    x, fns, g, fv = _setup(nx, nt)
+    primal, dual = O.make_update_fns(1, 0, rho_alp_iters=1)
+    tried = {"o": [], "p": []}
+
+    def mk(key):
+        def p2(phi, rho, c, alp, tau, dt, ds, f, fv_, epsl, xa, t):
+            tried[key].append(round(tau * 1.5, 12))
+            out = primal(phi, rho, c, alp, tau, dt, ds, f, fv_, epsl, xa, t)
+            return out * np.nan if tau * 1.5 > 0.055 else out
+        return p2
+    kw = dict(time_step_per_PDHG=2, stepsz_param=0.1, n_ctrl=1, fv=fv, N_maxiter=50, print_freq=10, eps=1e-6)
+    res_o, _ = O.PDHG_multi_step(mk("o"), dual, fns, g, x, 1, nt, (nx,), 0.5, (2.0 / nx,), 70.0, **kw)
+    res_p, _ = S.PDHG_multi_step(mk("p"), dual, fns, g, x, 1, nt, (nx,), 0.5, (2.0 / nx,), 70.0, verbose=False, **kw)
+    assert sorted(set(tried["p"])) == sorted(set(tried["o"]))
+    assert res_p[0][0] == res_o[0][0]
+    assert np.allclose(res_p[0][1], res_o[0][1])
+
+
+def test_update_fns_tagged_for_device_loop():
+    fp, fd = S.make_update_fns(2, (0, 0), rho_alp_iters=10)
+    assert fp._pdhg_native is fd._pdhg_native and fp._pdhg_native["rho_alp_iters"] == 10
+    assert S._native_tag(fp, fd) is not None
+    assert S._native_tag(fp, lambda *a: None) is None
