@@ -89,6 +89,54 @@ def cpu_baseline(cfg, T_sample, threads):
                           nx, ny, T_sample, T, reps, el, threads)}
 
 
+def pmc_traffic(args):
+    """HBM bytes per launch of every kernel class from rocprofv3 PMC counters, collected in two
+    separate child runs (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950) that are started
+    BEFORE this process touches the GPU (a process that initialised HIP must not fork+exec).
+    FETCH_SIZE is doubled per MI355X_MICROARCH.md §HBM (gfx950 reports half of a wide coalesced
+    stream; uncalibrated for 4-B loads); WRITE_SIZE is exact for 16-B streaming stores.
+    Returns ({class: {"bytes", "fetch_bytes_x2", "write_bytes"}}, None) or (None, reason)."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None, "rocprofv3 not found"
+    vals = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="pdhg_pmc_", dir="/tmp")
+        cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "run", "--",
+               sys.executable, os.path.abspath(__file__), "--config", args.config, "--steps", "2", "--warmup", "1",
+               "--rho-alp-iters", str(args.rho_alp_iters), "--no-cpu-baseline", "--no-pmc"]
+        try:
+            subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=600,
+                           env=dict(os.environ, TMPDIR="/tmp"))
+        except Exception as e:  # noqa: BLE001
+            return None, "rocprofv3 {} pass failed: {}".format(ctr, e)
+        for root, _, files in os.walk(d):
+            for f in files:
+                if f.endswith("counter_collection.csv"):
+                    with open(os.path.join(root, f)) as fh:
+                        for r in csv.DictReader(fh):
+                            if r["Counter_Name"] != ctr:
+                                continue
+                            for cls, sym in KERNEL_SYMBOL.items():
+                                if sym in r["Kernel_Name"]:
+                                    vals.setdefault((cls, ctr), []).append(float(r["Counter_Value"]) * 1024.0)
+        shutil.rmtree(d, ignore_errors=True)
+    out = {}
+    for cls in KERNEL_SYMBOL:
+        f, w = vals.get((cls, "FETCH_SIZE")), vals.get((cls, "WRITE_SIZE"))
+        if f and w:
+            fb, wb = 2.0 * sum(f) / len(f), sum(w) / len(w)
+            out[cls] = {"bytes": fb + wb, "fetch_bytes_x2": fb, "write_bytes": wb}
+    return (out, None) if out else (None, "no PMC rows matched")
+
+
+KERNEL_SYMBOL = {"dual": "k_dual_", "residual": "k_res_fwd", "precond": "k_precond_xt", "update": "k_inv"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -98,6 +146,7 @@ def main():
     ap.add_argument("--rho-alp-iters", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-T", type=int, default=2)
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -110,6 +159,10 @@ def main():
         torch.cuda.set_device(local_rank)
         tdist.init_process_group("nccl")
         dist = tdist
+
+    pmc, pmc_err = None, "disabled"
+    if world == 1 and not args.no_pmc:
+        pmc, pmc_err = pmc_traffic(args)   # before this process initialises the GPU
 
     from pdhg_amd.context import PDHGContext
 
@@ -199,6 +252,14 @@ def main():
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": None},
         "kernels": kern,
     }
+    if pmc and dom in pmc:
+        out["roofline"]["traffic"] = pmc[dom]["bytes"]
+        out["roofline"]["traffic_detail"] = pmc[dom]
+        for cls in kern:
+            if cls in pmc:
+                kern[cls]["pmc_bytes_per_launch"] = pmc[cls]["bytes"]
+    elif world == 1:
+        out["roofline"]["traffic_note"] = pmc_err
     if world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
         sample_cfg = CONFIGS[args.config]
