@@ -261,15 +261,51 @@ __device__ __forceinline__ C* lds_fft_fixed(C* a, C* b, const C* __restrict__ tw
 }
 
 // ---------------- in-place multi-line FFT (register-staged, one LDS buffer) ----------------
-// NL lines stored line-major (element e of line l at a[l*N + e]).  Each pass: every thread
-// loads its butterflies into registers, barrier, writes them back in Stockham order, barrier.
-// N, NL, NT compile-time; (N/R)*NL butterflies per pass spread over NT threads.
+// Line-major with one pad element per 16: element e of line l lives at a[l*PADN(N) + pix(e)],
+// pix(e) = e + e/16.  The first Stockham pass (LS = 1) writes 16 consecutive elements per lane;
+// unpadded that is a 128-B lane stride (16-way bank conflict), padded it is 136 B (conflict-free).
+// All other strides are multiples of 16 elements, so every offset stays a compile-time constant.
+template <int N>
+struct Pad {
+  static constexpr int LINE = N + N / 16;
+};
+__device__ __forceinline__ int pix(int e) { return e + (e >> 4); }
+
+// twiddles W^{r k} (W = exp(-2 pi i / (LS R))) for r = 1..R-1 from three table loads (W^k, W^4k,
+// W^8k) and at most three complex products each.
+template <typename C, int R>
+__device__ __forceinline__ void twiddles_from3(C* w, const C* __restrict__ tw, int kt) {
+  const C w1 = tw[kt];
+  if constexpr (R == 2) {
+    w[1] = w1;
+  } else {
+    w[1] = w1;
+    w[2] = cmul(w1, w1);
+    w[3] = cmul(w[2], w1);
+    if constexpr (R > 4) {
+      const C w4 = tw[4 * kt];
+      w[4] = w4;
+      w[5] = cmul(w4, w1);
+      w[6] = cmul(w4, w[2]);
+      w[7] = cmul(w4, w[3]);
+      if constexpr (R > 8) {
+        const C w8 = tw[8 * kt];
+        w[8] = w8;
+#pragma unroll
+        for (int r = 1; r < 8; ++r) w[8 + r] = cmul(w8, w[r]);
+      }
+    }
+  }
+}
+
 template <typename C, int N, int NL, int NT, int LS, int R>
 __device__ __forceinline__ void inplace_pass(C* __restrict__ a, const C* __restrict__ tw) {
   constexpr int nR = N / R;
   constexpr int tws = N / (LS * R);
   constexpr int total = nR * NL;
   constexpr int PER = (total + NT - 1) / NT;
+  constexpr int LINE = Pad<N>::LINE;
+  static_assert(nR % 16 == 0 && (LS == 1 || LS % 16 == 0) && (LS > 1 || R == 16), "padded schedule");
   C v[PER][R];
   int base[PER];
 #pragma unroll
@@ -280,14 +316,16 @@ __device__ __forceinline__ void inplace_pass(C* __restrict__ a, const C* __restr
       const int l = idx / nR;          // nR is a power of two: shift
       const int j = idx - l * nR;
       const int k = j & (LS - 1);
-      const C* s = a + (size_t)l * N + j;
+      const C* s = a + l * LINE + pix(j);
 #pragma unroll
-      for (int r = 0; r < R; ++r) v[q][r] = s[r * nR];
+      for (int r = 0; r < R; ++r) v[q][r] = s[r * (nR + nR / 16)];
       if (LS > 1 && k != 0) {
+        C w[R];
+        twiddles_from3<C, R>(w, tw, k * tws);
 #pragma unroll
-        for (int r = 1; r < R; ++r) v[q][r] = cmul(v[q][r], tw[r * k * tws]);
+        for (int r = 1; r < R; ++r) v[q][r] = cmul(v[q][r], w[r]);
       }
-      base[q] = l * N + (j - k) * R + k;
+      base[q] = l * LINE + pix((j - k) * R + k);
     }
   }
   lds_sync();
@@ -297,7 +335,7 @@ __device__ __forceinline__ void inplace_pass(C* __restrict__ a, const C* __restr
       dft_any<C, R>(v[q]);
       C* d = a + base[q];
 #pragma unroll
-      for (int r = 0; r < R; ++r) d[r * LS] = v[q][r];
+      for (int r = 0; r < R; ++r) d[(LS == 1) ? r : r * (LS + LS / 16)] = v[q][r];
     }
   }
   lds_sync();
@@ -313,10 +351,20 @@ __device__ __forceinline__ void inplace_passes(C* a, const C* __restrict__ tw) {
   }
 }
 
-// Forward FFT in place of NL line-major lines (element e of line l at a[l*N + e]).
+// Forward FFT in place of NL padded line-major lines (element e of line l at a[l*LINE + pix(e)]).
 template <typename C, int N, int NL, int NT>
 __device__ __forceinline__ void lds_fft_inplace(C* a, const C* __restrict__ tw) {
   inplace_passes<C, N, NL, NT, 1>(a, tw);
+}
+
+// Hartley unpack from a padded line (see hartley_pair).
+template <typename C, typename T>
+__device__ __forceinline__ void hartley_padded(const C* Z, int n, int k, T& ha, T& hb) {
+  const int km = (k == 0) ? 0 : n - k;
+  const C z = Z[pix(k)];
+  const C w = Z[pix(km)];
+  ha = (T)0.5 * ((z.x + w.x) - (z.y - w.y));
+  hb = (T)0.5 * ((z.y + w.y) - (w.x - z.x));
 }
 
 // FFT policies used as kernel template arguments.

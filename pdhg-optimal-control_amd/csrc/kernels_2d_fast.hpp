@@ -31,7 +31,7 @@ __device__ __forceinline__ float m2f(float rho, float alp, float a) {   // (rho 
   return (rho + 1e-4f) * fneg<float>(fval<float, EGNO>(alp, a));
 }
 
-// grid: T * nx/RW row-group tasks (XCD-aware); block NT = min(1024, N/4); LDS RW/2 * N * 8 B.
+// grid: T * nx/RW row-group tasks (XCD-aware); block NT = min(1024, N/4); LDS RW/2 * (N + N/16) * 8 B.
 template <int EGNO, int N, int RW, int NT>
 __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const float2* __restrict__ twy) {
   using C = float2;
@@ -136,7 +136,7 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const floa
         out[e] = res - div + cdt;
       }
       // residual row x -> line r/2, real (even r) or imaginary (odd r) part; 4 contiguous elements
-      float* Af = reinterpret_cast<float*>(A + (size_t)(r >> 1) * N + y) + (r & 1);
+      float* Af = reinterpret_cast<float*>(A + (r >> 1) * Pad<N>::LINE + pix(y)) + (r & 1);
 #pragma unroll
       for (int e = 0; e < 4; ++e) Af[2 * e] = out[e];
       // slide the window
@@ -165,14 +165,14 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const floa
       const int r = f / B, c = f - r * B;
       const int ky = b * B + c;
       float ha = 0.f, hb = 0.f;
-      if (ky < N) hartley_pair<C, float>(A + (size_t)(r >> 1) * N, N, 1, ky, 0, ha, hb);
+      if (ky < N) hartley_padded<C, float>(A + (r >> 1) * Pad<N>::LINE, N, ky, ha, hb);
       f4set(v, e, (r & 1) ? hb : ha);
     }
     st4(wk + ((size_t)b * nx + x0) * B + part * 4, v);
   }
 }
 
-// G workgroups striding over the T * nx/RW row-group tasks; block NT; LDS RW/2 * N * 8 B.
+// G workgroups striding over the T * nx/RW row-group tasks; block NT; LDS RW/2 * (N + N/16) * 8 B.
 // sums: [0] sum (phi'-phi)^2, [1] sum phi^2 (old), [2] sum phi'^2
 template <int N, int RW, int NT>
 __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const float2* __restrict__ twy) {
@@ -202,7 +202,7 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
         const int f = part * 4 + e;
         const int r = f / B, c = f - r * B;
         const int ky = b * B + c;
-        if (ky < N) Af[((size_t)(r >> 1) * N + ky) * 2 + (r & 1)] = f4(v, e);
+        if (ky < N) Af[((r >> 1) * Pad<N>::LINE + pix(ky)) * 2 + (r & 1)] = f4(v, e);
       }
     }
     __syncthreads();
@@ -214,14 +214,14 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
       const int y = 4 * (threadIdx.x + gi * NT);
 #pragma unroll 1
       for (int r = 0; r < RW; ++r) {
-        const C* Z = A + (size_t)(r >> 1) * N;
+        const C* Z = A + (r >> 1) * Pad<N>::LINE;
         const size_t idx = (size_t)(x0 + r) * N + y;
         const float4 old = ld4(phi + idx);
         float4 nw, pb;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float a, b2;
-          hartley_pair<C, float>(Z, N, 1, y + e, 0, a, b2);
+          hartley_padded<C, float>(Z, N, y + e, a, b2);
           const float o = f4(old, e);
           const float n = o + scale * ((r & 1) ? b2 : a);
           f4set(nw, e, n);
@@ -255,8 +255,8 @@ __device__ __forceinline__ float expm1_neg(float x) {
 // A thread owns IT items (kx, l) of the block's NL complex lines; item (kx, l) carries the two
 // modes (kx, 2l) and (kx, 2l+1), which are exactly the real and imaginary parts of line l's
 // element kx, so the b' / x carries map 1:1 onto the in-place line-major FFT buffer.
-// LDS: FFT buffer N*NL complex + per-item carries theta, E, b' as float2 (3 * N*NL * 8 B);
-// N*NL = 4096 -> 128 KiB.  Barriers are LDS-only (lds_sync) so the register prefetch of the
+// LDS: padded FFT buffer NL*(N + N/16) complex + per-item carries theta, E, b' as float2
+// (3 * N*NL * 8 B); N*NL = 4096 -> 130 KiB.  Barriers are LDS-only (lds_sync) so the register prefetch of the
 // next plane and the b'/x stores stay in flight across the FFT passes.
 // grid: nb; block NT.
 template <int N, int NL, int NT>
@@ -265,11 +265,12 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
   constexpr int IT = N * NL / NT;
   constexpr int B = 2 * NL;
   constexpr int NI = N * NL;            // items per block
+  constexpr int LINE = Pad<N>::LINE;
   constexpr int lnl = (NL == 1) ? 0 : (NL == 2) ? 1 : (NL == 4) ? 2 : 3;
   if (p.ctrl->done) return;
   extern __shared__ __align__(16) unsigned char smem_raw[];
   C* A = reinterpret_cast<C*>(smem_raw);
-  C* sth = A + NI;
+  C* sth = A + NL * LINE;
   C* sE = sth + NI;
   C* sbp = sE + NI;
   const int T = p.T, tid = threadIdx.x;
@@ -301,7 +302,7 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       const int item = tid + i * NT;
-      A[(item & (NL - 1)) * N + (item >> lnl)] = pf[i];
+      A[(item & (NL - 1)) * LINE + pix(item >> lnl)] = pf[i];
     }
     if (k + 1 < T) {
       const C* sn = reinterpret_cast<const C*>(wb + (size_t)(k + 1) * kstride);
@@ -318,7 +319,7 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
       const int item = tid + i * NT;
       const int kx = item >> lnl, l = item & (NL - 1);
       float hv[2];
-      hartley_pair<C, float>(A + (size_t)l * N, N, 1, kx, 0, hv[0], hv[1]);
+      hartley_padded<C, float>(A + l * LINE, N, kx, hv[0], hv[1]);
       const C t2 = sth[item];
       C e2 = sE[item];
       C b2 = sbp[item];
@@ -384,7 +385,7 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
         sE[item] = make_float2(en[0], en[1]);
         sbp[item] = x2;
       }
-      A[(item & (NL - 1)) * N + (item >> lnl)] = x2;
+      A[(item & (NL - 1)) * LINE + pix(item >> lnl)] = x2;
     }
     if (k >= 1) {
       const C* sn = reinterpret_cast<const C*>(wb + (size_t)(k - 1) * kstride);
@@ -398,7 +399,7 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
     for (int i = 0; i < IT; ++i) {
       const int item = tid + i * NT;
       float ha, hb;
-      hartley_pair<C, float>(A + (size_t)(item & (NL - 1)) * N, N, 1, item >> lnl, 0, ha, hb);
+      hartley_padded<C, float>(A + (item & (NL - 1)) * LINE, N, item >> lnl, ha, hb);
       wk[item] = make_float2(ha, hb);
     }
     lds_sync();

@@ -204,14 +204,14 @@ struct Impl : ImplBase {
       g5 = std::max(1, std::min(T * nx, 8192 / std::max(1, gx5)));
       if (sizeof(R) == 4 && plx.pow2 && nx * (B / 2) == 4096 && nx >= 512) {
         fast_xt = true;
-        lds_fast_xt = (size_t)4 * 4096 * sizeof(C);   // FFT buffer + theta, E, b' (float2 per item)
+        lds_fast_xt = (size_t)(4096 + 4096 / 16 + 3 * 4096) * sizeof(C);   // padded FFT buffer + theta, E, b' (float2)
       }
       if (sizeof(R) == 4 && ply.pow2 && ny >= 256 && ny <= 8192) {
         RWf = (ny == 8192) ? 4 : 8;
         NTf = std::min(1024, ny / 4);
         if (nx % RWf == 0 && (RWf * B) % 4 == 0) {
           fast_rows = true;
-          lds_fast = (size_t)(RWf / 2) * ny * sizeof(C);
+          lds_fast = (size_t)(RWf / 2) * (ny + ny / 16) * sizeof(C);
           g_fast_upd = std::min((nx / RWf) * T, 2048);
         }
       }
