@@ -320,6 +320,45 @@ __global__ void __launch_bounds__(256) k_invy_update_2d(KP<R> p, F ply, const cp
   block_reduce_store<3>(s, p.partials, blockIdx.x);
 }
 
+// One grid point of the dual step (update_fns_in_pdhg.py:150-165): alpha prox from the one-sided
+// differences of phi_bar at row j+1, HJ residual (:58-70), rho prox (update_rho_2d, :115-119).
+// pc/pxm/pxp/pym/pyp: phi_bar row j+1 at (x, y) and its 4 neighbours (0 outside a Dirichlet edge);
+// f0c: phi_bar row j at (x, y).
+template <typename R, int EGNO>
+__device__ __forceinline__ R dual_point(const KP<R>& p, R pc, R pxm, R pxp, R pym, R pyp, R f0c, R rho, const R* ao,
+                                        R axc, R ayc, R* an) {
+  const R DxR = (pxp - pc) * p.inv_dx;
+  const R DxL = (pc - pxm) * p.inv_dx;
+  const R DyR = (pyp - pc) * p.inv_dy;
+  const R DyL = (pc - pym) * p.inv_dy;
+  const R pinv = (rho + (R)1e-4) / p.sigma;              // param_inv, set_fns.py:127
+  an[0] = alp_prox<R, EGNO>(ao[0], DxR, axc, pinv, true);
+  an[1] = alp_prox<R, EGNO>(ao[1], DxL, axc, pinv, false);
+  const R f1x = fpos<R>(fval<R, EGNO>(an[0], axc));
+  const R f2x = fneg<R>(fval<R, EGNO>(an[1], axc));
+  R f1y, f2y, L;
+  if constexpr (EGNO == 3) {
+    f1y = fpos<R>(axc);
+    f2y = fneg<R>(axc);
+    L = lag<R, EGNO>(an[0] * an[0]) + lag<R, EGNO>(an[1] * an[1]);
+  } else {
+    an[2] = alp_prox<R, EGNO>(ao[2], DyR, ayc, pinv, true);
+    an[3] = alp_prox<R, EGNO>(ao[3], DyL, ayc, pinv, false);
+    f1y = fpos<R>(fval<R, EGNO>(an[2], ayc));
+    f2y = fneg<R>(fval<R, EGNO>(an[3], ayc));
+    L = lag<R, EGNO>(an[0] * an[0]) + lag<R, EGNO>(an[1] * an[1]) + lag<R, EGNO>(an[2] * an[2]) +
+        lag<R, EGNO>(an[3] * an[3]);
+  }
+  R vec = (pc - f0c) * p.inv_dt;
+  if (p.epsl != (R)0) {
+    vec = vec - p.epsl * ((pxp + pxm - (R)2 * pc) * p.inv_dx2);
+    vec = vec - p.epsl * ((pyp + pym - (R)2 * pc) * p.inv_dy2);
+  }
+  vec = vec - (DxR * f1x + DxL * f2x + DyR * f1y + DyL * f2y);
+  vec = vec - L;
+  return nmax<R>(rho + p.sigma * vec, (R)0);
+}
+
 // grid: (ceil(ny/256), G) where the G workgroup rows stride over the T*nx (j, x) rows; block 256
 // sums: [0] sum (rho'-rho)^2 [1] sum rho'^2 [2] sum rho^2, then per live alpha array a:
 //       [3+3a] sum (alp'-alp)^2 [4+3a] sum alp'^2 [5+3a] sum alp^2
@@ -352,46 +391,12 @@ __global__ void __launch_bounds__(256) k_dual_2d(KP<R> p) {
     const R pxp = (xp >= 0) ? f1[(size_t)xp * ny + y] : (R)0;
     const R pym = (ym >= 0) ? f1[(size_t)x * ny + ym] : (R)0;
     const R pyp = (yp >= 0) ? f1[(size_t)x * ny + yp] : (R)0;
-    // one-sided differences of phi_bar at row j+1 (utils_diff_op.py:9-162)
-    const R DxR = (pxp - pc) * p.inv_dx;
-    const R DxL = (pc - pxm) * p.inv_dx;
-    const R DyR = (pyp - pc) * p.inv_dy;
-    const R DyL = (pc - pym) * p.inv_dy;
     const size_t o = (size_t)j * plane + c;
     const R rho = p.rho[src_set][o];
-    const R pinv = (rho + (R)1e-4) / p.sigma;              // param_inv, set_fns.py:127
-    const R axc = p.ax[x];
     R an[4], ao[4];
-    ao[0] = p.alp[src_set][0][o];
-    ao[1] = p.alp[src_set][1][o];
-    an[0] = alp_prox<R, EGNO>(ao[0], DxR, axc, pinv, true);
-    an[1] = alp_prox<R, EGNO>(ao[1], DxL, axc, pinv, false);
-    const R f1x = fpos<R>(fval<R, EGNO>(an[0], axc));
-    const R f2x = fneg<R>(fval<R, EGNO>(an[1], axc));
-    R f1y, f2y, L;
-    if constexpr (EGNO == 3) {
-      f1y = fpos<R>(axc);
-      f2y = fneg<R>(axc);
-      L = lag<R, EGNO>(an[0] * an[0]) + lag<R, EGNO>(an[1] * an[1]);
-    } else {
-      ao[2] = p.alp[src_set][2][o];
-      ao[3] = p.alp[src_set][3][o];
-      an[2] = alp_prox<R, EGNO>(ao[2], DyR, ayc, pinv, true);
-      an[3] = alp_prox<R, EGNO>(ao[3], DyL, ayc, pinv, false);
-      f1y = fpos<R>(fval<R, EGNO>(an[2], ayc));
-      f2y = fneg<R>(fval<R, EGNO>(an[3], ayc));
-      L = lag<R, EGNO>(an[0] * an[0]) + lag<R, EGNO>(an[1] * an[1]) + lag<R, EGNO>(an[2] * an[2]) +
-          lag<R, EGNO>(an[3] * an[3]);
-    }
-    // HJ residual (update_fns_in_pdhg.py:58-70)
-    R vec = (pc - f0[c]) * p.inv_dt;
-    if (p.epsl != (R)0) {
-      vec = vec - p.epsl * ((pxp + pxm - (R)2 * pc) * p.inv_dx2);
-      vec = vec - p.epsl * ((pyp + pym - (R)2 * pc) * p.inv_dy2);
-    }
-    vec = vec - (DxR * f1x + DxL * f2x + DyR * f1y + DyL * f2y);
-    vec = vec - L;
-    const R rn = nmax<R>(rho + p.sigma * vec, (R)0);       // update_rho_2d, :115-119
+#pragma unroll
+    for (int a = 0; a < NA; ++a) ao[a] = p.alp[src_set][a][o];
+    const R rn = dual_point<R, EGNO>(p, pc, pxm, pxp, pym, pyp, f0[c], rho, ao, p.ax[x], ayc, an);
     p.rho[dst_set][o] = rn;
     const double dr = (double)rn - (double)rho;
     s[0] += dr * dr;

@@ -406,4 +406,95 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
   }
 }
 
+// ---- dual step, fp32, time-marching (update_fns_in_pdhg.py:150-165) ----
+// grid: (nx/RX x-groups [XCD-aware], ceil(ny/4/NT) y-chunks, nJ time chunks); block NT = min(256, ny/4).
+// A thread owns 4 consecutive y (float4) of RX consecutive x rows and marches over its chunk of
+// time rows: phi_bar row j+1 (RX rows + 2 halo rows, sliding window in x) is loaded once and kept
+// as phi_bar "row j" of the next step, so phi_bar is read ~once per iteration instead of twice.
+// y neighbours at the 4-wide edges are scalar loads of lines the wave is reading anyway (L1).
+// Sums as in k_dual_2d (double per point).
+template <int EGNO, int RX>
+__global__ void __launch_bounds__(256) k_dual_fast_2d(KP<float> p, int jchunk) {
+  if (p.ctrl->done || p.ctrl->inner_done) return;
+  constexpr int NA = (EGNO == 3) ? 2 : 4;
+  constexpr int NS = 3 + 3 * NA;
+  const int cur = p.ctrl->cur;
+  const int src_set = (p.inplace || p.sub == 0) ? cur : 1 - cur;
+  const int dst_set = p.inplace ? cur : 1 - cur;
+  const int nx = p.nx, ny = p.ny;
+  const size_t plane = (size_t)nx * ny;
+  const int gxs = xcd_remap(blockIdx.x, gridDim.x);
+  const int x0 = gxs * RX;
+  const int y = 4 * (blockIdx.y * blockDim.x + threadIdx.x);
+  const int j0 = blockIdx.z * jchunk;
+  const int j1 = min(p.T, j0 + jchunk);
+  double s[NS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) s[i] = 0.0;
+  if (y < ny) {
+    const int ym = nb_index(y - 1, ny, p.bcy), yp = nb_index(y + 4, ny, p.bcy);
+    const float4 ay4 = ld4(p.ay + y);
+    const int xm0 = nb_index(x0 - 1, nx, p.bcx);
+    float4 f0[RX];   // phi_bar row j at the RX rows
+#pragma unroll
+    for (int r = 0; r < RX; ++r) f0[r] = ld4(p.phibar + (size_t)j0 * plane + (size_t)(x0 + r) * ny + y);
+    const float* rs = p.rho[src_set];
+    float* rd = p.rho[dst_set];
+#pragma unroll 1
+    for (int j = j0; j < j1; ++j) {
+      const float* f1 = p.phibar + (size_t)(j + 1) * plane;
+      float4 pm = xm0 >= 0 ? ld4(f1 + (size_t)xm0 * ny + y) : z4();
+      float4 pc = ld4(f1 + (size_t)x0 * ny + y);
+#pragma unroll
+      for (int r = 0; r < RX; ++r) {
+        const int x = x0 + r;
+        const int xp = (r + 1 < RX) ? x + 1 : nb_index(x + 1, nx, p.bcx);
+        const float4 pp = xp >= 0 ? ld4(f1 + (size_t)xp * ny + y) : z4();
+        const float* frow = f1 + (size_t)x * ny;
+        const float pyl = ym >= 0 ? frow[ym] : 0.f;
+        const float pyr = yp >= 0 ? frow[yp] : 0.f;
+        const size_t o = (size_t)j * plane + (size_t)x * ny + y;
+        const float4 rho4 = ld4(rs + o);
+        float4 ao4[NA];
+#pragma unroll
+        for (int a = 0; a < NA; ++a) ao4[a] = ld4(p.alp[src_set][a] + o);
+        const float axc = p.ax[x];
+        float4 rn4, an4[NA];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float c = f4(pc, e);
+          const float lft = e == 0 ? pyl : f4(pc, e - 1);
+          const float rgt = e == 3 ? pyr : f4(pc, e + 1);
+          float ao[4], an[4];
+#pragma unroll
+          for (int a = 0; a < NA; ++a) ao[a] = f4(ao4[a], e);
+          const float rho = f4(rho4, e);
+          const float rn = dual_point<float, EGNO>(p, c, f4(pm, e), f4(pp, e), lft, rgt, f4(f0[r], e), rho, ao, axc,
+                                                   f4(ay4, e), an);
+          f4set(rn4, e, rn);
+          const double dr = (double)rn - (double)rho;
+          s[0] += dr * dr;
+          s[1] += (double)rn * (double)rn;
+          s[2] += (double)rho * (double)rho;
+#pragma unroll
+          for (int a = 0; a < NA; ++a) {
+            f4set(an4[a], e, an[a]);
+            const double da = (double)an[a] - (double)ao[a];
+            s[3 + 3 * a] += da * da;
+            s[4 + 3 * a] += (double)an[a] * (double)an[a];
+            s[5 + 3 * a] += (double)ao[a] * (double)ao[a];
+          }
+        }
+        st4(rd + o, rn4);
+#pragma unroll
+        for (int a = 0; a < NA; ++a) st4(p.alp[dst_set][a] + o, an4[a]);
+        f0[r] = pc;
+        pm = pc;
+        pc = pp;
+      }
+    }
+  }
+  block_reduce_store<NS>(s, p.partials, ((int)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x);
+}
+
 }  // namespace pdhg

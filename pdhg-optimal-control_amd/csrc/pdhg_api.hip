@@ -98,6 +98,8 @@ struct Impl : ImplBase {
   // launch geometry
   int NT2 = 512;
   int gx1 = 0, gx4 = 0, g4 = 1, gx5 = 0, g5 = 1, g_outer = 1;
+  bool fast_dual = false;                 // fp32 time-marching float4 dual kernel (k_dual_fast_2d)
+  int RXd = 8, NTd = 256, gxd = 0, gyd = 0, gzd = 0, jchunk_d = 1;
   size_t lds_res = 0, lds_xt = 0;
   // fast row kernels (fp32, power-of-two ny): RW rows per workgroup, NTf threads
   bool fast_rows = false;
@@ -206,6 +208,20 @@ struct Impl : ImplBase {
         fast_xt = true;
         lds_fast_xt = (size_t)(4096 + 4096 / 16 + 3 * 4096) * sizeof(C);   // padded FFT buffer + theta, E, b' (float2)
       }
+      if (sizeof(R) == 4 && ny % 256 == 0) {
+        fast_dual = true;
+        RXd = 1;   // measured on C3: RX 1/2/4/8 -> 25.8/26.4/32.1/32.2 ms (register pressure at RX >= 4)
+        if (const char* e = getenv("PDHG_DUAL_RX")) {   // tuning override
+          const int v = atoi(e);
+          if ((v == 1 || v == 2 || v == 4 || v == 8) && nx % v == 0) RXd = v;
+        }
+        NTd = std::min(256, ny / 4);
+        gxd = nx / RXd;
+        gyd = (ny / 4 + NTd - 1) / NTd;
+        const int nJ0 = std::max(1, std::min(T, (2048 + gxd * gyd - 1) / (gxd * gyd)));
+        jchunk_d = (T + nJ0 - 1) / nJ0;
+        gzd = (T + jchunk_d - 1) / jchunk_d;
+      }
       if (sizeof(R) == 4 && ply.pow2 && ny >= 256 && ny <= 8192) {
         RWf = (ny == 8192) ? 4 : 8;
         NTf = std::min(1024, ny / 4);
@@ -229,7 +245,8 @@ struct Impl : ImplBase {
       g5 = std::max(1, std::min(T, 8192 / std::max(1, gx5)));
     }
     g_outer = 2048;
-    partial_rows = std::max<size_t>({(size_t)gx4 * g4, (size_t)gx5 * g5, (size_t)g_outer, (size_t)g_fast_upd, 1});
+    partial_rows = std::max<size_t>(
+        {(size_t)gx4 * g4, (size_t)gx5 * g5, (size_t)g_outer, (size_t)g_fast_upd, (size_t)gxd * gyd * gzd, 1});
 
     // ---- device buffers ----
     const size_t npl = plane();
@@ -548,6 +565,24 @@ struct Impl : ImplBase {
     return PDHG_OK;
   }
 
+  template <int EGNO>
+  void launch_dual_fast_rx(const KP<R>& p) {
+    if constexpr (std::is_same<R, float>::value) {
+      const dim3 g(gxd, gyd, gzd), b(NTd);
+      switch (RXd) {
+        case 8: hipLaunchKernelGGL((k_dual_fast_2d<EGNO, 8>), g, b, 0, stream, p, jchunk_d); break;
+        case 4: hipLaunchKernelGGL((k_dual_fast_2d<EGNO, 4>), g, b, 0, stream, p, jchunk_d); break;
+        case 2: hipLaunchKernelGGL((k_dual_fast_2d<EGNO, 2>), g, b, 0, stream, p, jchunk_d); break;
+        default: hipLaunchKernelGGL((k_dual_fast_2d<EGNO, 1>), g, b, 0, stream, p, jchunk_d); break;
+      }
+    }
+  }
+  void launch_dual_fast(const KP<R>& p) {
+    if (pb.egno == 1) launch_dual_fast_rx<1>(p);
+    else if (pb.egno == 2) launch_dual_fast_rx<2>(p);
+    else launch_dual_fast_rx<3>(p);
+  }
+
   int launch_dual(R sigma, double eps, int k) {
     KP<R> p = kp;
     p.sigma = sigma;
@@ -559,7 +594,9 @@ struct Impl : ImplBase {
       {
         ProfScope ps(this, "dual");
         dim3 g(gx5, g5);
-        if (pb.ndim == 2) {
+        if (pb.ndim == 2 && fast_dual) {
+          launch_dual_fast(p);
+        } else if (pb.ndim == 2) {
           switch (pb.egno) {
             case 1: hipLaunchKernelGGL((k_dual_2d<R, 1>), g, dim3(256), 0, stream, p); break;
             case 2: hipLaunchKernelGGL((k_dual_2d<R, 2>), g, dim3(256), 0, stream, p); break;
@@ -572,7 +609,8 @@ struct Impl : ImplBase {
             hipLaunchKernelGGL((k_dual_1d<R, 2>), g, dim3(256), 0, stream, p);
         }
       }
-      hipLaunchKernelGGL(k_finalize_dual, dim3(1), dim3(256), 0, stream, p.partials, gx5 * g5, na, n_dead, eps, s,
+      const int nrows_d = (pb.ndim == 2 && fast_dual) ? gxd * gyd * gzd : gx5 * g5;
+      hipLaunchKernelGGL(k_finalize_dual, dim3(1), dim3(256), 0, stream, p.partials, nrows_d, na, n_dead, eps, s,
                          p.ctrl);
     }
     HIP_TRY(hipGetLastError());
