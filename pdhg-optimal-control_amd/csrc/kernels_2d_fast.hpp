@@ -279,25 +279,22 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
   float* wb = p.work + (size_t)b * M;
   const size_t kstride = (size_t)p.nb * M;
   const float ae = p.ae, inv_ae = 1.f / ae;
+  // forward carries per item (2 modes): sth = dd = 2 delta = d0/ae, sE = h = 1 - g (h_{-1} = 1), sbp = b'
   C pf[IT];
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
     const int item = tid + i * NT;
     const int kx = item >> lnl, l = item & (NL - 1);
-    float t2[2], e2[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const float d0 = p.C - p.lamx[kx] - p.lamy[b * B + 2 * l + h];
-      const float delta = d0 / (2.f * ae);
-      t2[h] = log1pf(delta + sqrtf(delta * (delta + 2.f)));   // cosh(th) = 1 + d0/(2 ae)
-      e2[h] = expm1f(-2.f * t2[h]);                            // E_1, E_m = expm1(-2 th m)
-    }
-    sth[item] = make_float2(t2[0], t2[1]);
-    sE[item] = make_float2(e2[0], e2[1]);
+    const float lx = p.lamx[kx];
+    sth[item] = make_float2((p.C - lx - p.lamy[b * B + 2 * l]) * inv_ae, (p.C - lx - p.lamy[b * B + 2 * l + 1]) * inv_ae);
+    sE[item] = make_float2(1.f, 1.f);
     sbp[item] = make_float2(0.f, 0.f);
     pf[i] = reinterpret_cast<const C*>(wb)[item];
   }
   // ---------------- forward: DHT_x + elimination ----------------
+  // Thomas pivots in the cancellation-free form (all terms >= 0, contractive):
+  //   s = dd + h_{k-1},  g_k = ae/u_k = 1/(1+s),  h_k = 1 - g_k = s g_k,  b'_k = (rhs/ae + b'_{k-1}) g_k
+  //   last (Neumann) row: u_{T-1} = ae (dd + h_{T-2}).
   for (int k = 0; k < T; ++k) {
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
@@ -312,40 +309,31 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
     lds_sync();
     lds_fft_inplace<C, N, NL, NT>(A, twx);
     C* dst = reinterpret_cast<C*>(wb + (size_t)k * kstride);
-    const bool last = (k == T - 1);
-    const float kk1 = (float)(k + 1), kk2 = (float)(k + 2);
-#pragma unroll 2
-    for (int i = 0; i < IT; ++i) {
-      const int item = tid + i * NT;
-      const int kx = item >> lnl, l = item & (NL - 1);
-      float hv[2];
-      hartley_padded<C, float>(A + l * LINE, N, kx, hv[0], hv[1]);
-      const C t2 = sth[item];
-      C e2 = sE[item];
-      C b2 = sbp[item];
-      const float tt[2] = {t2.x, t2.y};
-      float ee[2] = {e2.x, e2.y}, bb[2] = {b2.x, b2.y};
+    if (k < T - 1) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const float t = tt[h];
-        if (!last) {
-          // 1/u_k = e^-th E_{k+1} / (ae E_{k+2})   (closed form of the Thomas pivots)
-          const float E2 = expm1_neg(-2.f * t * kk2);
-          const float g = (t > 0.f) ? __expf(-t) * ee[h] * __frcp_rn(E2) : kk1 / kk2;
-          bb[h] = (hv[h] * inv_ae + bb[h]) * g;
-          ee[h] = E2;
-        } else {
-          // Neumann last row: u_{T-1} = d0 + ae expm1(-th)(1 + e^{-th(2T-1)}) / E_T
-          const float d0 = p.C - p.lamx[kx] - p.lamy[b * B + 2 * l + h];
-          const float u = (t > 0.f) ? d0 + ae * expm1f(-t) * (1.f + expf(-t * (float)(2 * T - 1))) /
-                                               expm1f(-2.f * t * (float)T)
-                                    : d0 + ae / (float)T;
-          bb[h] = (hv[h] + ae * bb[h]) / u;
-        }
+      for (int i = 0; i < IT; ++i) {
+        const int item = tid + i * NT;
+        const int kx = item >> lnl, l = item & (NL - 1);
+        float ha, hb;
+        hartley_padded<C, float>(A + l * LINE, N, kx, ha, hb);
+        const C dd = sth[item], h = sE[item], bp = sbp[item];
+        const float s0 = dd.x + h.x, s1 = dd.y + h.y;
+        const float g0 = __frcp_rn(1.f + s0), g1 = __frcp_rn(1.f + s1);
+        const C bn = make_float2((ha * inv_ae + bp.x) * g0, (hb * inv_ae + bp.y) * g1);
+        sE[item] = make_float2(s0 * g0, s1 * g1);
+        sbp[item] = bn;
+        dst[item] = bn;
       }
-      sE[item] = make_float2(ee[0], ee[1]);
-      sbp[item] = make_float2(bb[0], bb[1]);
-      if (!last) dst[item] = make_float2(bb[0], bb[1]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < IT; ++i) {
+        const int item = tid + i * NT;
+        const int kx = item >> lnl, l = item & (NL - 1);
+        float ha, hb;
+        hartley_padded<C, float>(A + l * LINE, N, kx, ha, hb);
+        const C dd = sth[item], h = sE[item], bp = sbp[item];
+        sbp[item] = make_float2((ha * inv_ae + bp.x) / (dd.x + h.x), (hb * inv_ae + bp.y) / (dd.y + h.y));
+      }
     }
     lds_sync();
   }
@@ -354,8 +342,13 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
     const int item = tid + i * NT;
-    const C t2 = sth[item];
-    sE[item] = make_float2(expm1f(-2.f * t2.x * (float)T), expm1f(-2.f * t2.y * (float)T));   // E_{(T-2)+2}
+    const C dd = sth[item];
+    float t2[2];
+    const float dl[2] = {0.5f * dd.x, 0.5f * dd.y};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) t2[h] = log1pf(dl[h] + sqrtf(dl[h] * (dl[h] + 2.f)));   // cosh(th) = 1 + delta
+    sth[item] = make_float2(t2[0], t2[1]);
+    sE[item] = make_float2(expm1f(-2.f * t2[0] * (float)T), expm1f(-2.f * t2[1] * (float)T));   // E_{(T-2)+2}
   }
   if (T >= 2) {
     const C* s0 = reinterpret_cast<const C*>(wb + (size_t)(T - 2) * kstride);
@@ -363,7 +356,7 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
     for (int i = 0; i < IT; ++i) pf[i] = s0[tid + i * NT];
   }
   for (int k = T - 1; k >= 0; --k) {
-    const float kk1 = (float)(k + 1), kk2 = (float)(k + 2);
+    const float kk1 = (float)(k + 1), gz = (float)(k + 1) / (float)(k + 2);   // theta = 0: g_k = (k+1)/(k+2)
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       const int item = tid + i * NT;
@@ -377,7 +370,7 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
         for (int h = 0; h < 2; ++h) {
           const float t = tt[h];
           const float E1 = expm1_neg(-2.f * t * kk1);
-          const float g = (t > 0.f) ? __expf(-t) * E1 * __frcp_rn(ee[h]) : kk1 / kk2;
+          const float g = (t > 0.f) ? __expf(-t) * E1 * __frcp_rn(ee[h]) : gz;
           xx[h] = pv[h] + g * xx[h];
           en[h] = E1;
         }
