@@ -298,8 +298,18 @@ __device__ __forceinline__ void twiddles_from3(C* w, const C* __restrict__ tw, i
   }
 }
 
-template <typename C, int N, int NL, int NT, int LS, int R>
-__device__ __forceinline__ void inplace_pass(C* __restrict__ a, const C* __restrict__ tw) {
+// LDS twiddle seeds: a kernel that runs many transforms keeps (W^k, W^4k, W^8k) for every k of each
+// twiddled pass in a small LDS table (TwLds<N>::SIZE complex; 816 for N = 4096), so the passes read
+// their seeds at LDS latency instead of from L2; the 15 per-butterfly twiddles are rebuilt with <= 3
+// complex products (as twiddles_from3).  Pass LS = 16 at offset 0, LS = 256 at 48, LS = 4096 at 816.
+template <int N>
+struct TwLds {
+  static constexpr int SIZE = 3 * ((N > 16 ? 16 : 0) + (N > 256 ? 256 : 0) + (N > 4096 ? 4096 : 0));
+};
+__host__ __device__ constexpr int twlds_off(int LS) { return LS >= 4096 ? 816 : LS >= 256 ? 48 : 0; }
+
+template <typename C, int N, int NL, int NT, int LS, int R, bool REG>
+__device__ __forceinline__ void inplace_pass(C* __restrict__ a, const C* __restrict__ tw, const C* twl) {
   constexpr int nR = N / R;
   constexpr int tws = N / (LS * R);
   constexpr int total = nR * NL;
@@ -321,7 +331,27 @@ __device__ __forceinline__ void inplace_pass(C* __restrict__ a, const C* __restr
       for (int r = 0; r < R; ++r) v[q][r] = s[r * (nR + nR / 16)];
       if (LS > 1 && k != 0) {
         C w[R];
-        twiddles_from3<C, R>(w, tw, k * tws);
+        if constexpr (REG) {
+          const C* t3 = twl + twlds_off(LS) + 3 * k;
+          w[1] = t3[0];
+          if constexpr (R > 2) {
+            w[2] = cmul(t3[0], t3[0]);
+            w[3] = cmul(w[2], t3[0]);
+          }
+          if constexpr (R > 4) {
+            w[4] = t3[1];
+            w[5] = cmul(t3[1], t3[0]);
+            w[6] = cmul(t3[1], w[2]);
+            w[7] = cmul(t3[1], w[3]);
+          }
+          if constexpr (R > 8) {
+            w[8] = t3[2];
+#pragma unroll
+            for (int r = 1; r < 8; ++r) w[8 + r] = cmul(t3[2], w[r]);
+          }
+        } else {
+          twiddles_from3<C, R>(w, tw, k * tws);
+        }
 #pragma unroll
         for (int r = 1; r < R; ++r) v[q][r] = cmul(v[q][r], w[r]);
       }
@@ -341,20 +371,40 @@ __device__ __forceinline__ void inplace_pass(C* __restrict__ a, const C* __restr
   lds_sync();
 }
 
-template <typename C, int N, int NL, int NT, int LS>
-__device__ __forceinline__ void inplace_passes(C* a, const C* __restrict__ tw) {
+template <typename C, int N, int NL, int NT, int LS, bool REG>
+__device__ __forceinline__ void inplace_passes(C* a, const C* __restrict__ tw, const C* twl) {
   if constexpr (LS < N) {
     constexpr int rem = N / LS;
     constexpr int R = (rem >= 16) ? 16 : rem;
-    inplace_pass<C, N, NL, NT, LS, R>(a, tw);
-    inplace_passes<C, N, NL, NT, LS * R>(a, tw);
+    inplace_pass<C, N, NL, NT, LS, R, REG>(a, tw, twl);
+    inplace_passes<C, N, NL, NT, LS * R, REG>(a, tw, twl);
   }
 }
 
 // Forward FFT in place of NL padded line-major lines (element e of line l at a[l*LINE + pix(e)]).
 template <typename C, int N, int NL, int NT>
 __device__ __forceinline__ void lds_fft_inplace(C* a, const C* __restrict__ tw) {
-  inplace_passes<C, N, NL, NT, 1>(a, tw);
+  inplace_passes<C, N, NL, NT, 1, false>(a, tw, nullptr);
+}
+
+// Same transform with the twiddle seeds read from an LDS table filled by fill_twlds.
+template <typename C, int N, int NL, int NT>
+__device__ __forceinline__ void lds_fft_inplace_tl(C* a, const C* twl) {
+  inplace_passes<C, N, NL, NT, 1, true>(a, nullptr, twl);
+}
+
+// Fill the TwLds<N> table from the global twiddle table (W_N^m at tw[m]); caller syncs before use.
+template <typename C, int N>
+__device__ __forceinline__ void fill_twlds(C* twl, const C* __restrict__ tw) {
+  for (int i = threadIdx.x; i < TwLds<N>::SIZE; i += blockDim.x) {
+    const int LS = i >= 816 ? 4096 : i >= 48 ? 256 : 16;
+    const int e = i - twlds_off(LS);
+    const int k = e / 3, m = e - 3 * k;
+    const int R = (N / LS >= 16) ? 16 : N / LS;
+    const int tws = N / (LS * R);
+    const int mult = (m == 0) ? 1 : (m == 1) ? 4 : 8;
+    twl[i] = tw[(mult * k * tws) & (N - 1)];
+  }
 }
 
 // Hartley unpack from a padded line (see hartley_pair).

@@ -280,6 +280,8 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
   const size_t kstride = (size_t)p.nb * M;
   const float ae = p.ae, inv_ae = 1.f / ae;
   // forward carries per item (2 modes): sth = dd = 2 delta = d0/ae, sE = h = 1 - g (h_{-1} = 1), sbp = b'
+  C* twl = sbp + NI;   // TwLds<N> twiddle seeds
+  fill_twlds<C, N>(twl, twx);
   C pf[IT];
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
@@ -307,7 +309,7 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
       for (int i = 0; i < IT; ++i) pf[i] = sn[tid + i * NT];
     }
     lds_sync();
-    lds_fft_inplace<C, N, NL, NT>(A, twx);
+    if (!(p.dbg & 1)) lds_fft_inplace_tl<C, N, NL, NT>(A, twl);
     C* dst = reinterpret_cast<C*>(wb + (size_t)k * kstride);
     if (k < T - 1) {
 #pragma unroll
@@ -361,7 +363,7 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
     for (int i = 0; i < IT; ++i) {
       const int item = tid + i * NT;
       C x2 = sbp[item];
-      if (k < T - 1) {
+      if (k < T - 1 && !(p.dbg & 4)) {
         const C t2 = sth[item];
         const C e2 = sE[item];
         const float tt[2] = {t2.x, t2.y}, ee[2] = {e2.x, e2.y}, pv[2] = {pf[i].x, pf[i].y};
@@ -386,7 +388,7 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
       for (int i = 0; i < IT; ++i) pf[i] = sn[tid + i * NT];
     }
     lds_sync();
-    lds_fft_inplace<C, N, NL, NT>(A, twx);
+    if (!(p.dbg & 2)) lds_fft_inplace_tl<C, N, NL, NT>(A, twl);
     C* wk = reinterpret_cast<C*>(wb + (size_t)k * kstride);
 #pragma unroll
     for (int i = 0; i < IT; ++i) {

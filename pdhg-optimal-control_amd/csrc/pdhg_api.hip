@@ -204,9 +204,11 @@ struct Impl : ImplBase {
       g4 = 1;
       gx5 = (ny + 255) / 256;
       g5 = std::max(1, std::min(T * nx, 8192 / std::max(1, gx5)));
+      if (const char* e = getenv("PDHG_DBG")) p.dbg = atoi(e);   // timing experiments only
       if (sizeof(R) == 4 && plx.pow2 && nx * (B / 2) == 4096 && nx >= 512) {
         fast_xt = true;
-        lds_fast_xt = (size_t)(4096 + 4096 / 16 + 3 * 4096) * sizeof(C);   // padded FFT buffer + theta, E, b' (float2)
+        // padded FFT buffer + theta, E, b' (float2 per item) + twiddle seeds (TwLds<nx>)
+        lds_fast_xt = (size_t)(4096 + 4096 / 16 + 3 * 4096 + 816) * sizeof(C);
       }
       if (sizeof(R) == 4 && ny % 256 == 0) {
         fast_dual = true;
