@@ -76,6 +76,18 @@ __device__ __forceinline__ void block_reduce_store(double (&v)[NS], double* __re
   __syncthreads();
 }
 
+// Cross-lane neighbour values over the whole 64-lane wave (GFX9 DPP wave shifts).
+// lane_from_prev(v): lane i receives v of lane i-1 (lane 0 receives `edge`);
+// lane_from_next(v): lane i receives v of lane i+1 (lane 63 receives `edge`).
+__device__ __forceinline__ float lane_from_prev(float v, float edge) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, edge), __builtin_bit_cast(int, v),
+                                                               0x138 /* wave_shr:1 */, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float lane_from_next(float v, float edge) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, edge), __builtin_bit_cast(int, v),
+                                                               0x130 /* wave_shl:1 */, 0xF, 0xF, false));
+}
+
 // XCD-aware block index remap: hardware deals consecutive workgroups round-robin
 // over the 8 XCDs; remap so each XCD walks a contiguous range of logical blocks
 // (neighbouring tiles share that XCD's L2).  Speed only, never correctness.

@@ -44,11 +44,22 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const floa
   const int nx = p.nx, T = p.T;
   const int ngx = nx / RW;
   const int task = xcd_remap(blockIdx.x, gridDim.x);
-  const int j = task / ngx;
-  const int x0 = (task - j * ngx) * RW;
+  int j, gx;
+  if (p.tile_j > 1) {
+    // tiles of 4 row groups x TJ time rows: the ~32 tasks an XCD runs together share rho row j+1
+    // and the x-halo rows in that XCD's L2 (needs ngx % 4 == 0, T % TJ == 0; checked on the host)
+    const int TJ = p.tile_j, tsz = 4 * TJ, ngt = ngx >> 2;
+    const int tile = task / tsz, w = task - tile * tsz;
+    const int tjx = tile / ngt, tg = tile - tjx * ngt;
+    j = tjx * TJ + (w >> 2);
+    gx = tg * 4 + (w & 3);
+  } else {
+    j = task / ngx;
+    gx = task - j * ngx;
+  }
+  const int x0 = gx * RW;
   const size_t plane = (size_t)nx * N;
   const float* rj = p.rho[cur] + (size_t)j * plane;
-  const float* rn = (j + 1 < T) ? p.rho[cur] + (size_t)(j + 1) * plane : nullptr;
   const float* a1x = p.alp[cur][0] + (size_t)j * plane;
   const float* a2x = p.alp[cur][1] + (size_t)j * plane;
   const float* a1y = (EGNO == 3) ? nullptr : p.alp[cur][2] + (size_t)j * plane;
@@ -56,45 +67,102 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const floa
   const float cdt = (j == T - 1) ? p.c_over_dt : 0.f;
   const bool use_eps = p.epsl != 0.f;
 
+  // Branch-free row loop: every load reads a valid address (rows/columns outside a Dirichlet edge
+  // are clamped and zeroed by a select afterwards), so the loads of consecutive rows stay in
+  // flight together instead of each conditional load draining the queue.
+  const int xm0 = nb_index(x0 - 1, nx, p.bcx);          // row above the group (uniform)
+  const int xpl = nb_index(x0 + RW, nx, p.bcx);         // row below the group (uniform)
+  const bool zm = xm0 < 0, zpl = xpl < 0;
+  const int xm0c = zm ? x0 : xm0, xplc = zpl ? x0 + RW - 1 : xpl;
+  const bool last_j = (j + 1 >= T);
+  const float* rnx = last_j ? rj : p.rho[cur] + (size_t)(j + 1) * plane;   // rho row j+1 (zeroed if last)
+  const int lane = threadIdx.x & (kWave - 1);
 #pragma unroll
   for (int gi = 0; gi < GPT; ++gi) {
     const int y = 4 * (threadIdx.x + gi * NT);
-    const int ym = nb_index(y - 1, N, p.bcy), yp = nb_index(y + 4, N, p.bcy);
+    // wave-edge y neighbours (uniform per wave): y0-1 for lane 0, y63+4 for lane 63
+    const int yw0 = __builtin_amdgcn_readfirstlane(y);
+    const int ywm = nb_index(yw0 - 1, N, p.bcy), ywp = nb_index(yw0 + 4 * kWave, N, p.bcy);
+    const bool zym = ywm < 0, zyp = ywp < 0;
+    const int ywmc = zym ? 0 : ywm, ywpc = zyp ? 0 : ywp;
     float4 ay4 = z4();
     float aym = 0.f, ayp = 0.f;
     if constexpr (EGNO != 3) {
       ay4 = ld4(p.ay + y);
-      aym = ym >= 0 ? p.ay[ym] : 0.f;
-      ayp = yp >= 0 ? p.ay[yp] : 0.f;
+      aym = lane_from_prev(ay4.w, zym ? 0.f : p.ay[ywmc]);
+      ayp = lane_from_next(ay4.x, zyp ? 0.f : p.ay[ywpc]);
     }
-    const int xm = nb_index(x0 - 1, nx, p.bcx);
-    float4 r_m = xm >= 0 ? ld4(rj + (size_t)xm * N + y) : z4();
-    float4 a1_m = xm >= 0 ? ld4(a1x + (size_t)xm * N + y) : z4();
-    float ax_m = xm >= 0 ? p.ax[xm] : 0.f;
+    float4 r_m = ld4(rj + (size_t)xm0c * N + y);
+    float4 a1_m = ld4(a1x + (size_t)xm0c * N + y);
+    float ax_m = p.ax[xm0c];
+    if (zm) {
+      r_m = z4();
+      a1_m = z4();
+      ax_m = 0.f;
+    }
     float4 r_c = ld4(rj + (size_t)x0 * N + y);
-    float4 a1_c = ld4(a1x + (size_t)x0 * N + y);
     float4 a2_c = ld4(a2x + (size_t)x0 * N + y);
     float ax_c = p.ax[x0];
-#pragma unroll 2
-    for (int r = 0; r < RW; ++r) {
+    // flux carries: m1x at the row above, m2x at the current row
+    float m1x_prev[4], m2x_cur[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      m1x_prev[e] = zm ? 0.f : m1f<EGNO>(f4(r_m, e), f4(a1_m, e), ax_m);
+      m2x_cur[e] = m2f<EGNO>(f4(r_c, e), f4(a2_c, e), ax_c);
+    }
+    // software pipeline: the loads of row r+1 are issued before row r is computed
+    struct RowIn {
+      float4 r_p, a2_p, a1_c, rn4, a1y4, a2y4;
+      float ax_p, e_rm, e_rp, e_a1m, e_a2p;
+    };
+    auto load_row = [&](int r) {
+      RowIn in;
       const int x = x0 + r;
-      const int xp = nb_index(x + 1, nx, p.bcx);
+      const int xpc = (r + 1 == RW) ? xplc : x + 1;
       const size_t ro = (size_t)x * N;
-      const float4 r_p = xp >= 0 ? ld4(rj + (size_t)xp * N + y) : z4();
-      const float4 a2_p = xp >= 0 ? ld4(a2x + (size_t)xp * N + y) : z4();
-      const float4 a1_n = (r + 1 < RW && xp >= 0) ? ld4(a1x + (size_t)xp * N + y) : z4();
-      const float ax_p = xp >= 0 ? p.ax[xp] : 0.f;
-      const float4 rn4 = rn ? ld4(rn + ro + y) : z4();
-      float4 a1y4 = z4(), a2y4 = z4();
-      float a1y_m = 0.f, a2y_p = 0.f;
+      in.r_p = ld4(rj + (size_t)xpc * N + y);
+      in.a2_p = ld4(a2x + (size_t)xpc * N + y);
+      in.ax_p = p.ax[xpc];
+      in.a1_c = ld4(a1x + ro + y);
+      in.rn4 = ld4(rnx + ro + y);
+      in.e_rm = rj[ro + ywmc];
+      in.e_rp = rj[ro + ywpc];
       if constexpr (EGNO != 3) {
-        a1y4 = ld4(a1y + ro + y);
-        a2y4 = ld4(a2y + ro + y);
-        a1y_m = ym >= 0 ? a1y[ro + ym] : 0.f;
-        a2y_p = yp >= 0 ? a2y[ro + yp] : 0.f;
+        in.a1y4 = ld4(a1y + ro + y);
+        in.a2y4 = ld4(a2y + ro + y);
+        in.e_a1m = a1y[ro + ywmc];
+        in.e_a2p = a2y[ro + ywpc];
+      } else {
+        in.a1y4 = in.a2y4 = z4();
+        in.e_a1m = in.e_a2p = 0.f;
       }
-      const float r_ym = ym >= 0 ? rj[ro + ym] : 0.f;
-      const float r_yp = yp >= 0 ? rj[ro + yp] : 0.f;
+      return in;
+    };
+    RowIn nxt = load_row(0);
+#pragma unroll
+    for (int r = 0; r < RW; ++r) {
+      const RowIn in = nxt;
+      if (r + 1 < RW) nxt = load_row(r + 1);
+      const bool zp = (r + 1 == RW) && zpl;
+      float4 r_p = in.r_p, a2_p = in.a2_p, rn4 = in.rn4;
+      float ax_p = in.ax_p;
+      const float4 a1_c = in.a1_c;
+      if (zp) {
+        r_p = z4();
+        a2_p = z4();
+        ax_p = 0.f;
+      }
+      if (last_j) rn4 = z4();
+      const float4 a1y4 = in.a1y4, a2y4 = in.a2y4;
+      float a1y_m = 0.f, a2y_p = 0.f;
+      // y neighbours: from the adjacent lanes (DPP); the wave-edge values are uniform loads
+      if constexpr (EGNO != 3) {
+        a1y_m = lane_from_prev(a1y4.w, zym ? 0.f : in.e_a1m);
+        a2y_p = lane_from_next(a2y4.x, zyp ? 0.f : in.e_a2p);
+      }
+      const float r_ym = lane_from_prev(r_c.w, zym ? 0.f : in.e_rm);
+      const float r_yp = lane_from_next(r_c.x, zyp ? 0.f : in.e_rp);
+      const bool edge_m = zym && lane == 0, edge_p = zyp && lane == kWave - 1;
       float m1y[6], m2y[6], rr[6];   // index e+1 for e = -1..4
       rr[0] = r_ym;
       rr[5] = r_yp;
@@ -107,17 +175,17 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const floa
           m1y[e] = (rr[e] + 1e-4f) * f1;
           m2y[e] = (rr[e] + 1e-4f) * f2;
         }
-        if (ym < 0) m1y[0] = 0.f;
-        if (yp < 0) m2y[5] = 0.f;
       } else {
-        m1y[0] = ym >= 0 ? m1f<EGNO>(r_ym, a1y_m, aym) : 0.f;
-        m2y[5] = yp >= 0 ? m2f<EGNO>(r_yp, a2y_p, ayp) : 0.f;
+        m1y[0] = m1f<EGNO>(r_ym, a1y_m, aym);
+        m2y[5] = m2f<EGNO>(r_yp, a2y_p, ayp);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           m1y[e + 1] = m1f<EGNO>(rr[e + 1], f4(a1y4, e), f4(ay4, e));
           m2y[e + 1] = m2f<EGNO>(rr[e + 1], f4(a2y4, e), f4(ay4, e));
         }
       }
+      if (edge_m) m1y[0] = 0.f;   // zero flux outside a Dirichlet edge
+      if (edge_p) m2y[5] = 0.f;
       float out[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -128,12 +196,12 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const floa
           res = res + p.epsl * ((rr[e + 2] + rr[e] - 2.f * r0) * p.inv_dy2);
         }
         const float m1x_c = m1f<EGNO>(r0, f4(a1_c, e), ax_c);
-        const float m1x_m = (r > 0 || xm >= 0) ? m1f<EGNO>(f4(r_m, e), f4(a1_m, e), ax_m) : 0.f;
-        const float m2x_c = m2f<EGNO>(r0, f4(a2_c, e), ax_c);
-        const float m2x_p = xp >= 0 ? m2f<EGNO>(f4(r_p, e), f4(a2_p, e), ax_p) : 0.f;
-        const float div = (m1x_c - m1x_m) * p.inv_dx + (m2x_p - m2x_c) * p.inv_dx +
+        const float m2x_p = zp ? 0.f : m2f<EGNO>(f4(r_p, e), f4(a2_p, e), ax_p);
+        const float div = (m1x_c - m1x_prev[e]) * p.inv_dx + (m2x_p - m2x_cur[e]) * p.inv_dx +
                           (m1y[e + 1] - m1y[e]) * p.inv_dy + (m2y[e + 2] - m2y[e + 1]) * p.inv_dy;
         out[e] = res - div + cdt;
+        m1x_prev[e] = m1x_c;
+        m2x_cur[e] = m2x_p;
       }
       // residual row x -> line r/2, real (even r) or imaginary (odd r) part; 4 contiguous elements
       float* Af = reinterpret_cast<float*>(A + (r >> 1) * Pad<N>::LINE + pix(y)) + (r & 1);
@@ -141,16 +209,12 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const floa
       for (int e = 0; e < 4; ++e) Af[2 * e] = out[e];
       // slide the window
       r_m = r_c;
-      a1_m = a1_c;
-      ax_m = ax_c;
       r_c = r_p;
-      a1_c = a1_n;
-      a2_c = a2_p;
       ax_c = ax_p;
     }
   }
   __syncthreads();
-  lds_fft_inplace<C, N, NL, NT>(A, twy);
+  if (!(p.dbg & 8)) lds_fft_inplace<C, N, NL, NT>(A, twy);
   // Hartley unpack -> blocked layout: chunk (j, b, x0..x0+RW-1, 0..B-1) = RW*B contiguous floats
   const int B = p.B;
   const int CS4 = RW * B / 4;                 // float4 per chunk
@@ -206,7 +270,7 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
       }
     }
     __syncthreads();
-    lds_fft_inplace<C, N, NL, NT>(A, twy);
+    if (!(p.dbg & 16)) lds_fft_inplace<C, N, NL, NT>(A, twy);
     float* phi = p.phi + (size_t)(j + 1) * plane;
     float* pbar = p.phibar + (size_t)(j + 1) * plane;
 #pragma unroll
@@ -446,8 +510,9 @@ __global__ void __launch_bounds__(256) k_dual_fast_2d(KP<float> p, int jchunk) {
         const int xp = (r + 1 < RX) ? x + 1 : nb_index(x + 1, nx, p.bcx);
         const float4 pp = xp >= 0 ? ld4(f1 + (size_t)xp * ny + y) : z4();
         const float* frow = f1 + (size_t)x * ny;
-        const float pyl = ym >= 0 ? frow[ym] : 0.f;
-        const float pyr = yp >= 0 ? frow[yp] : 0.f;
+        const int lane = threadIdx.x & (kWave - 1);
+        const float pyl = lane_from_prev(pc.w, (lane == 0 && ym >= 0) ? frow[ym] : 0.f);
+        const float pyr = lane_from_next(pc.x, (lane == kWave - 1 && yp >= 0) ? frow[yp] : 0.f);
         const size_t o = (size_t)j * plane + (size_t)x * ny + y;
         const float4 rho4 = ld4(rs + o);
         float4 ao4[NA];

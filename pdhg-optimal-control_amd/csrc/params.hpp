@@ -15,6 +15,7 @@ struct KP {
   int inplace;             // dual updates rho/alp in place (rho_alp_iters == 1)
   int sub;                 // dual sub-iteration index of this launch
   int dbg;                 // timing experiments only (env PDHG_DBG); 0 in production
+  int tile_j;              // residual task tiling: TJ time rows x 4 row groups per tile (1 = off)
   R inv_dx, inv_dy, inv_dt, inv_dx2, inv_dy2;
   R epsl, c_over_dt;
   R ae;                    // Ct/dt^2 (1-D) or 1/dt^2 (2-D): off-diagonal magnitude of the t-Laplacian

@@ -98,6 +98,7 @@ struct Impl : ImplBase {
   // launch geometry
   int NT2 = 512;
   int gx1 = 0, gx4 = 0, g4 = 1, gx5 = 0, g5 = 1, g_outer = 1;
+  int rows_var = 0;                       // row-kernel shape variant (see with_fast_rows)
   bool fast_dual = false;                 // fp32 time-marching float4 dual kernel (k_dual_fast_2d)
   int RXd = 8, NTd = 256, gxd = 0, gyd = 0, gzd = 0, jchunk_d = 1;
   size_t lds_res = 0, lds_xt = 0;
@@ -224,11 +225,27 @@ struct Impl : ImplBase {
         jchunk_d = (T + nJ0 - 1) / nJ0;
         gzd = (T + jchunk_d - 1) / jchunk_d;
       }
+      if (const char* e = getenv("PDHG_ROWS_VAR")) rows_var = atoi(e);   // tuning override
       if (sizeof(R) == 4 && ply.pow2 && ny >= 256 && ny <= 8192) {
         RWf = (ny == 8192) ? 4 : 8;
         NTf = std::min(1024, ny / 4);
+        if (rows_var == 1 && (ny == 4096 || ny == 2048)) {   // 4 rows / block, 2 blocks per CU
+          RWf = 4;
+          NTf = ny / 8;
+        }
         if (nx % RWf == 0 && (RWf * B) % 4 == 0) {
           fast_rows = true;
+          p.tile_j = 1;
+          if ((nx / RWf) % 4 == 0)
+            for (int tj : {8, 4, 2})
+              if (T % tj == 0) {
+                p.tile_j = tj;
+                break;
+              }
+          if (const char* e = getenv("PDHG_TILE_J")) {   // tuning override (must divide T)
+            const int v = atoi(e);
+            if (v >= 1 && T % v == 0 && (v == 1 || (nx / RWf) % 4 == 0)) p.tile_j = v;
+          }
           lds_fast = (size_t)(RWf / 2) * (ny + ny / 16) * sizeof(C);
           g_fast_upd = std::min((nx / RWf) * T, 2048);
         }
@@ -363,10 +380,18 @@ struct Impl : ImplBase {
                             std::integral_constant<int, 128>{});
         case 1024: return fn(std::integral_constant<int, 1024>{}, std::integral_constant<int, 8>{},
                              std::integral_constant<int, 256>{});
-        case 2048: return fn(std::integral_constant<int, 2048>{}, std::integral_constant<int, 8>{},
-                             std::integral_constant<int, 512>{});
-        case 4096: return fn(std::integral_constant<int, 4096>{}, std::integral_constant<int, 8>{},
-                             std::integral_constant<int, 1024>{});
+        case 2048:
+          if (rows_var == 1)
+            return fn(std::integral_constant<int, 2048>{}, std::integral_constant<int, 4>{},
+                      std::integral_constant<int, 256>{});
+          return fn(std::integral_constant<int, 2048>{}, std::integral_constant<int, 8>{},
+                    std::integral_constant<int, 512>{});
+        case 4096:
+          if (rows_var == 1)
+            return fn(std::integral_constant<int, 4096>{}, std::integral_constant<int, 4>{},
+                      std::integral_constant<int, 512>{});
+          return fn(std::integral_constant<int, 4096>{}, std::integral_constant<int, 8>{},
+                    std::integral_constant<int, 1024>{});
         case 8192: return fn(std::integral_constant<int, 8192>{}, std::integral_constant<int, 4>{},
                              std::integral_constant<int, 1024>{});
         default: break;
