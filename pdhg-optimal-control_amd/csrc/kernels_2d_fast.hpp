@@ -466,13 +466,15 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
 }
 
 // ---- dual step, fp32, time-marching (update_fns_in_pdhg.py:150-165) ----
-// grid: (nx/RX x-groups [XCD-aware], ceil(ny/4/NT) y-chunks, nJ time chunks); block NT = min(256, ny/4).
-// A thread owns 4 consecutive y (float4) of RX consecutive x rows and marches over its chunk of
-// time rows: phi_bar row j+1 (RX rows + 2 halo rows, sliding window in x) is loaded once and kept
-// as phi_bar "row j" of the next step, so phi_bar is read ~once per iteration instead of twice.
-// y neighbours at the 4-wide edges are scalar loads of lines the wave is reading anyway (L1).
-// Sums as in k_dual_2d (double per point).
-template <int EGNO, int RX>
+// grid: (nx rows [XCD-aware], ny/4/NT y-chunks, nJ time chunks); block NT = min(256, ny/4), ny % 256 == 0
+// (so every wave is fully inside [0, ny)).
+// A thread owns 4 consecutive y (float4) of one x row and marches over its chunk of time rows:
+// phi_bar row j+1 is loaded once and kept as phi_bar "row j" of the next step, so phi_bar is read
+// about once per iteration instead of twice.  The loads of step j+1 are issued before step j is
+// computed; every load reads a valid address (rows outside a Dirichlet edge are clamped, then
+// zeroed by a select), so nothing drains the load queue.  y neighbours come from the adjacent
+// lanes (DPP), the wave-edge ones from uniform loads.  Sums as in k_dual_2d (double per point).
+template <int EGNO>
 __global__ void __launch_bounds__(256) k_dual_fast_2d(KP<float> p, int jchunk) {
   if (p.ctrl->done || p.ctrl->inner_done) return;
   constexpr int NA = (EGNO == 3) ? 2 : 4;
@@ -482,8 +484,7 @@ __global__ void __launch_bounds__(256) k_dual_fast_2d(KP<float> p, int jchunk) {
   const int dst_set = p.inplace ? cur : 1 - cur;
   const int nx = p.nx, ny = p.ny;
   const size_t plane = (size_t)nx * ny;
-  const int gxs = xcd_remap(blockIdx.x, gridDim.x);
-  const int x0 = gxs * RX;
+  const int x = xcd_remap(blockIdx.x, gridDim.x);
   const int y = 4 * (blockIdx.y * blockDim.x + threadIdx.x);
   const int j0 = blockIdx.z * jchunk;
   const int j1 = min(p.T, j0 + jchunk);
@@ -491,67 +492,82 @@ __global__ void __launch_bounds__(256) k_dual_fast_2d(KP<float> p, int jchunk) {
 #pragma unroll
   for (int i = 0; i < NS; ++i) s[i] = 0.0;
   if (y < ny) {
-    const int ym = nb_index(y - 1, ny, p.bcy), yp = nb_index(y + 4, ny, p.bcy);
+    const int yw0 = __builtin_amdgcn_readfirstlane(y);
+    const int ywm = nb_index(yw0 - 1, ny, p.bcy), ywp = nb_index(yw0 + 4 * kWave, ny, p.bcy);
+    const bool zym = ywm < 0, zyp = ywp < 0;
+    const int ywmc = zym ? 0 : ywm, ywpc = zyp ? 0 : ywp;
+    const int xm = nb_index(x - 1, nx, p.bcx), xp = nb_index(x + 1, nx, p.bcx);
+    const bool zxm = xm < 0, zxp = xp < 0;
+    const size_t rxm = (size_t)(zxm ? x : xm) * ny, rxc = (size_t)x * ny, rxp = (size_t)(zxp ? x : xp) * ny;
     const float4 ay4 = ld4(p.ay + y);
-    const int xm0 = nb_index(x0 - 1, nx, p.bcx);
-    float4 f0[RX];   // phi_bar row j at the RX rows
-#pragma unroll
-    for (int r = 0; r < RX; ++r) f0[r] = ld4(p.phibar + (size_t)j0 * plane + (size_t)(x0 + r) * ny + y);
+    const float axc = p.ax[x];
     const float* rs = p.rho[src_set];
     float* rd = p.rho[dst_set];
+    const float* as[NA];
+    float* ad[NA];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) {
+      as[a] = p.alp[src_set][a];
+      ad[a] = p.alp[dst_set][a];
+    }
+    struct In {
+      float4 pm, pc, pp, rho, al[NA];
+      float el, er;
+    };
+    auto load = [&](int j) {
+      In in;
+      const float* f1 = p.phibar + (size_t)(j + 1) * plane;
+      in.pm = ld4(f1 + rxm + y);
+      in.pc = ld4(f1 + rxc + y);
+      in.pp = ld4(f1 + rxp + y);
+      in.el = f1[rxc + ywmc];
+      in.er = f1[rxc + ywpc];
+      const size_t o = (size_t)j * plane + rxc + y;
+      in.rho = ld4(rs + o);
+#pragma unroll
+      for (int a = 0; a < NA; ++a) in.al[a] = ld4(as[a] + o);
+      return in;
+    };
+    float4 f0 = ld4(p.phibar + (size_t)j0 * plane + rxc + y);   // phi_bar row j
+    In nxt = load(j0);
 #pragma unroll 1
     for (int j = j0; j < j1; ++j) {
-      const float* f1 = p.phibar + (size_t)(j + 1) * plane;
-      float4 pm = xm0 >= 0 ? ld4(f1 + (size_t)xm0 * ny + y) : z4();
-      float4 pc = ld4(f1 + (size_t)x0 * ny + y);
+      const In in = nxt;
+      nxt = load(min(j + 1, j1 - 1));   // (the last step reloads its own row: keeps the loop branch-free)
+      const float4 pm = zxm ? z4() : in.pm, pp = zxp ? z4() : in.pp, pc = in.pc;
+      const float pyl = lane_from_prev(pc.w, zym ? 0.f : in.el);
+      const float pyr = lane_from_next(pc.x, zyp ? 0.f : in.er);
+      float4 rn4, an4[NA];
 #pragma unroll
-      for (int r = 0; r < RX; ++r) {
-        const int x = x0 + r;
-        const int xp = (r + 1 < RX) ? x + 1 : nb_index(x + 1, nx, p.bcx);
-        const float4 pp = xp >= 0 ? ld4(f1 + (size_t)xp * ny + y) : z4();
-        const float* frow = f1 + (size_t)x * ny;
-        const int lane = threadIdx.x & (kWave - 1);
-        const float pyl = lane_from_prev(pc.w, (lane == 0 && ym >= 0) ? frow[ym] : 0.f);
-        const float pyr = lane_from_next(pc.x, (lane == kWave - 1 && yp >= 0) ? frow[yp] : 0.f);
-        const size_t o = (size_t)j * plane + (size_t)x * ny + y;
-        const float4 rho4 = ld4(rs + o);
-        float4 ao4[NA];
+      for (int e = 0; e < 4; ++e) {
+        const float c = f4(pc, e);
+        const float lft = e == 0 ? pyl : f4(pc, e - 1);
+        const float rgt = e == 3 ? pyr : f4(pc, e + 1);
+        float ao[4], an[4];
 #pragma unroll
-        for (int a = 0; a < NA; ++a) ao4[a] = ld4(p.alp[src_set][a] + o);
-        const float axc = p.ax[x];
-        float4 rn4, an4[NA];
+        for (int a = 0; a < NA; ++a) ao[a] = f4(in.al[a], e);
+        const float rho = f4(in.rho, e);
+        const float rn = dual_point<float, EGNO>(p, c, f4(pm, e), f4(pp, e), lft, rgt, f4(f0, e), rho, ao, axc,
+                                                 f4(ay4, e), an);
+        f4set(rn4, e, rn);
+        const double dr = (double)rn - (double)rho;
+        s[0] += dr * dr;
+        s[1] += (double)rn * (double)rn;
+        s[2] += (double)rho * (double)rho;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float c = f4(pc, e);
-          const float lft = e == 0 ? pyl : f4(pc, e - 1);
-          const float rgt = e == 3 ? pyr : f4(pc, e + 1);
-          float ao[4], an[4];
-#pragma unroll
-          for (int a = 0; a < NA; ++a) ao[a] = f4(ao4[a], e);
-          const float rho = f4(rho4, e);
-          const float rn = dual_point<float, EGNO>(p, c, f4(pm, e), f4(pp, e), lft, rgt, f4(f0[r], e), rho, ao, axc,
-                                                   f4(ay4, e), an);
-          f4set(rn4, e, rn);
-          const double dr = (double)rn - (double)rho;
-          s[0] += dr * dr;
-          s[1] += (double)rn * (double)rn;
-          s[2] += (double)rho * (double)rho;
-#pragma unroll
-          for (int a = 0; a < NA; ++a) {
-            f4set(an4[a], e, an[a]);
-            const double da = (double)an[a] - (double)ao[a];
-            s[3 + 3 * a] += da * da;
-            s[4 + 3 * a] += (double)an[a] * (double)an[a];
-            s[5 + 3 * a] += (double)ao[a] * (double)ao[a];
-          }
+        for (int a = 0; a < NA; ++a) {
+          f4set(an4[a], e, an[a]);
+          const double da = (double)an[a] - (double)ao[a];
+          s[3 + 3 * a] += da * da;
+          s[4 + 3 * a] += (double)an[a] * (double)an[a];
+          s[5 + 3 * a] += (double)ao[a] * (double)ao[a];
         }
-        st4(rd + o, rn4);
-#pragma unroll
-        for (int a = 0; a < NA; ++a) st4(p.alp[dst_set][a] + o, an4[a]);
-        f0[r] = pc;
-        pm = pc;
-        pc = pp;
       }
+      const size_t o = (size_t)j * plane + rxc + y;
+      st4(rd + o, rn4);
+#pragma unroll
+      for (int a = 0; a < NA; ++a) st4(ad[a] + o, an4[a]);
+      f0 = pc;
     }
   }
   block_reduce_store<NS>(s, p.partials, ((int)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x);

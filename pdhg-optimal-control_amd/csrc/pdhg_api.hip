@@ -100,7 +100,7 @@ struct Impl : ImplBase {
   int gx1 = 0, gx4 = 0, g4 = 1, gx5 = 0, g5 = 1, g_outer = 1;
   int rows_var = 0;                       // row-kernel shape variant (see with_fast_rows)
   bool fast_dual = false;                 // fp32 time-marching float4 dual kernel (k_dual_fast_2d)
-  int RXd = 8, NTd = 256, gxd = 0, gyd = 0, gzd = 0, jchunk_d = 1;
+  int NTd = 256, gxd = 0, gyd = 0, gzd = 0, jchunk_d = 1;
   size_t lds_res = 0, lds_xt = 0;
   // fast row kernels (fp32, power-of-two ny): RW rows per workgroup, NTf threads
   bool fast_rows = false;
@@ -213,13 +213,8 @@ struct Impl : ImplBase {
       }
       if (sizeof(R) == 4 && ny % 256 == 0) {
         fast_dual = true;
-        RXd = 1;   // measured on C3: RX 1/2/4/8 -> 25.8/26.4/32.1/32.2 ms (register pressure at RX >= 4)
-        if (const char* e = getenv("PDHG_DUAL_RX")) {   // tuning override
-          const int v = atoi(e);
-          if ((v == 1 || v == 2 || v == 4 || v == 8) && nx % v == 0) RXd = v;
-        }
         NTd = std::min(256, ny / 4);
-        gxd = nx / RXd;
+        gxd = nx;
         gyd = (ny / 4 + NTd - 1) / NTd;
         const int nJ0 = std::max(1, std::min(T, (2048 + gxd * gyd - 1) / (gxd * gyd)));
         jchunk_d = (T + nJ0 - 1) / nJ0;
@@ -593,21 +588,14 @@ struct Impl : ImplBase {
   }
 
   template <int EGNO>
-  void launch_dual_fast_rx(const KP<R>& p) {
-    if constexpr (std::is_same<R, float>::value) {
-      const dim3 g(gxd, gyd, gzd), b(NTd);
-      switch (RXd) {
-        case 8: hipLaunchKernelGGL((k_dual_fast_2d<EGNO, 8>), g, b, 0, stream, p, jchunk_d); break;
-        case 4: hipLaunchKernelGGL((k_dual_fast_2d<EGNO, 4>), g, b, 0, stream, p, jchunk_d); break;
-        case 2: hipLaunchKernelGGL((k_dual_fast_2d<EGNO, 2>), g, b, 0, stream, p, jchunk_d); break;
-        default: hipLaunchKernelGGL((k_dual_fast_2d<EGNO, 1>), g, b, 0, stream, p, jchunk_d); break;
-      }
-    }
+  void launch_dual_fast_e(const KP<R>& p) {
+    if constexpr (std::is_same<R, float>::value)
+      hipLaunchKernelGGL((k_dual_fast_2d<EGNO>), dim3(gxd, gyd, gzd), dim3(NTd), 0, stream, p, jchunk_d);
   }
   void launch_dual_fast(const KP<R>& p) {
-    if (pb.egno == 1) launch_dual_fast_rx<1>(p);
-    else if (pb.egno == 2) launch_dual_fast_rx<2>(p);
-    else launch_dual_fast_rx<3>(p);
+    if (pb.egno == 1) launch_dual_fast_e<1>(p);
+    else if (pb.egno == 2) launch_dual_fast_e<2>(p);
+    else launch_dual_fast_e<3>(p);
   }
 
   int launch_dual(R sigma, double eps, int k) {
