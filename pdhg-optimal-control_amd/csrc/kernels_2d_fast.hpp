@@ -269,37 +269,57 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
         if (ky < N) Af[((r >> 1) * Pad<N>::LINE + pix(ky)) * 2 + (r & 1)] = f4(v, e);
       }
     }
-    __syncthreads();
-    if (!(p.dbg & 16)) lds_fft_inplace<C, N, NL, NT>(A, twy);
     float* phi = p.phi + (size_t)(j + 1) * plane;
     float* pbar = p.phibar + (size_t)(j + 1) * plane;
+    // old phi of rows (0, 1): issued now, consumed after the transform (LDS-only barriers keep
+    // them in flight); each row pair prefetches the next pair while it computes
+    auto ldpair = [&](int gi, int l, float4& o0, float4& o1) {
+      const size_t idx = (size_t)(x0 + 2 * l) * N + 4 * (threadIdx.x + gi * NT);
+      o0 = ld4(phi + idx);
+      o1 = ld4(phi + idx + N);
+    };
+    float4 nx0, nx1;
+    ldpair(0, 0, nx0, nx1);
+    lds_sync();
+    if (!(p.dbg & 16)) lds_fft_inplace<C, N, NL, NT>(A, twy);
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
       const int y = 4 * (threadIdx.x + gi * NT);
-#pragma unroll 1
-      for (int r = 0; r < RW; ++r) {
-        const C* Z = A + (r >> 1) * Pad<N>::LINE;
-        const size_t idx = (size_t)(x0 + r) * N + y;
-        const float4 old = ld4(phi + idx);
-        float4 nw, pb;
+#pragma unroll
+      for (int l = 0; l < NL; ++l) {   // rows 2l (real part) and 2l+1 (imaginary part) of line l
+        const float4 o4[2] = {nx0, nx1};
+        if (l + 1 < NL) ldpair(gi, l + 1, nx0, nx1);
+        else if (gi + 1 < GPT) ldpair(gi + 1, 0, nx0, nx1);
+        const C* Z = A + l * Pad<N>::LINE;
+        float4 u[2];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float a, b2;
           hartley_padded<C, float>(Z, N, y + e, a, b2);
-          const float o = f4(old, e);
-          const float n = o + scale * ((r & 1) ? b2 : a);
-          f4set(nw, e, n);
-          f4set(pb, e, 2.f * n - o);
-          const float d = n - o;
-          s[0] += (double)d * (double)d;
-          s[1] += (double)o * (double)o;
-          s[2] += (double)n * (double)n;
+          f4set(u[0], e, a);
+          f4set(u[1], e, b2);
         }
-        st4(phi + idx, nw);
-        st4(pbar + idx, pb);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const size_t idx = (size_t)(x0 + 2 * l + h) * N + y;
+          float4 nw, pb;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float o = f4(o4[h], e);
+            const float n = o + scale * f4(u[h], e);
+            f4set(nw, e, n);
+            f4set(pb, e, 2.f * n - o);
+            const float d = n - o;
+            s[0] += (double)d * (double)d;
+            s[1] += (double)o * (double)o;
+            s[2] += (double)n * (double)n;
+          }
+          st4(phi + idx, nw);
+          st4(pbar + idx, pb);
+        }
       }
     }
-    __syncthreads();
+    lds_sync();
   }
   block_reduce_store<3>(s, p.partials, blockIdx.x);
 }
