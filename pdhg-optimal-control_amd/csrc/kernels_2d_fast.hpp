@@ -366,7 +366,14 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
   // forward carries per item (2 modes): sth = dd = 2 delta = d0/ae, sE = h = 1 - g (h_{-1} = 1), sbp = b'
   C* twl = sbp + NI;   // TwLds<N> twiddle seeds
   fill_twlds<C, N>(twl, twx);
-  C pf[IT];
+  // two-step register prefetch (pf: step k+1, pf2: step k+2; row indices clamped, so the loads are
+  // branch-free): 64 KiB per CU in flight instead of 32
+  C pf[IT], pf2[IT];
+  auto ldrow = [&](C (&dstv)[IT], int kk) {
+    const C* sn = reinterpret_cast<const C*>(wb + (size_t)kk * kstride);
+#pragma unroll
+    for (int i = 0; i < IT; ++i) dstv[i] = sn[tid + i * NT];
+  };
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
     const int item = tid + i * NT;
@@ -375,8 +382,9 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
     sth[item] = make_float2((p.C - lx - p.lamy[b * B + 2 * l]) * inv_ae, (p.C - lx - p.lamy[b * B + 2 * l + 1]) * inv_ae);
     sE[item] = make_float2(1.f, 1.f);
     sbp[item] = make_float2(0.f, 0.f);
-    pf[i] = reinterpret_cast<const C*>(wb)[item];
   }
+  ldrow(pf, 0);
+  ldrow(pf2, min(1, T - 1));
   // ---------------- forward: DHT_x + elimination ----------------
   // Thomas pivots in the cancellation-free form (all terms >= 0, contractive):
   //   s = dd + h_{k-1},  g_k = ae/u_k = 1/(1+s),  h_k = 1 - g_k = s g_k,  b'_k = (rhs/ae + b'_{k-1}) g_k
@@ -387,11 +395,9 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
       const int item = tid + i * NT;
       A[(item & (NL - 1)) * LINE + pix(item >> lnl)] = pf[i];
     }
-    if (k + 1 < T) {
-      const C* sn = reinterpret_cast<const C*>(wb + (size_t)(k + 1) * kstride);
 #pragma unroll
-      for (int i = 0; i < IT; ++i) pf[i] = sn[tid + i * NT];
-    }
+    for (int i = 0; i < IT; ++i) pf[i] = pf2[i];
+    ldrow(pf2, min(k + 2, T - 1));
     lds_sync();
     if (!(p.dbg & 1)) lds_fft_inplace_tl<C, N, NL, NT>(A, twl);
     C* dst = reinterpret_cast<C*>(wb + (size_t)k * kstride);
@@ -436,11 +442,8 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
     sth[item] = make_float2(t2[0], t2[1]);
     sE[item] = make_float2(expm1f(-2.f * t2[0] * (float)T), expm1f(-2.f * t2[1] * (float)T));   // E_{(T-2)+2}
   }
-  if (T >= 2) {
-    const C* s0 = reinterpret_cast<const C*>(wb + (size_t)(T - 2) * kstride);
-#pragma unroll
-    for (int i = 0; i < IT; ++i) pf[i] = s0[tid + i * NT];
-  }
+  // backward prefetch: step k consumes pf = b'_k (k < T-1); after each step pf <- pf2, pf2 <- b'_{k-2}
+  ldrow(pf2, max(T - 2, 0));
   for (int k = T - 1; k >= 0; --k) {
     const float kk1 = (float)(k + 1), gz = (float)(k + 1) / (float)(k + 2);   // theta = 0: g_k = (k+1)/(k+2)
 #pragma unroll
@@ -466,11 +469,9 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
       }
       A[(item & (NL - 1)) * LINE + pix(item >> lnl)] = x2;
     }
-    if (k >= 1) {
-      const C* sn = reinterpret_cast<const C*>(wb + (size_t)(k - 1) * kstride);
 #pragma unroll
-      for (int i = 0; i < IT; ++i) pf[i] = sn[tid + i * NT];
-    }
+    for (int i = 0; i < IT; ++i) pf[i] = pf2[i];
+    ldrow(pf2, max(k - 2, 0));
     lds_sync();
     if (!(p.dbg & 2)) lds_fft_inplace_tl<C, N, NL, NT>(A, twl);
     C* wk = reinterpret_cast<C*>(wb + (size_t)k * kstride);
