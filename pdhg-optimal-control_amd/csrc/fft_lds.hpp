@@ -407,6 +407,86 @@ __device__ __forceinline__ void fill_twlds(C* twl, const C* __restrict__ tw) {
   }
 }
 
+// ---------------- split passes for warp-specialised kernels ----------------
+// Pass P (LS = 16^P) of the padded in-place schedule executed by a group of NTF threads, split at
+// its barrier into a read half (loads + twiddles into registers) and a write half (DFT + stores),
+// so another wave group can run between the barriers.  Twiddle seeds from the TwLds table.
+template <int N, int NL, int NTF, int P>
+struct SplitPass {
+  static constexpr int LS = (P == 0) ? 1 : (P == 1) ? 16 : (P == 2) ? 256 : 4096;
+  static constexpr int R = (N / LS >= 16) ? 16 : N / LS;
+  static constexpr int nR = N / R;
+  static constexpr int total = nR * NL;
+  static constexpr int PER = (total + NTF - 1) / NTF;
+  static_assert(nR % 16 == 0 && (LS == 1 || LS % 16 == 0) && (LS > 1 || R == 16), "padded schedule");
+};
+
+// v: flat register array of at least PER*R complex (element (q, r) at q*R + r); callers may alias it
+// with other per-wave state (a warp-specialised kernel shares one array between its roles).
+template <typename C, int N, int NL, int NTF, int P, int NV>
+__device__ __forceinline__ void split_read(const C* __restrict__ a, const C* twl, int t, C (&v)[NV],
+                                           int (&base)[SplitPass<N, NL, NTF, P>::PER]) {
+  using SP = SplitPass<N, NL, NTF, P>;
+  constexpr int R = SP::R, nR = SP::nR, LS = SP::LS, LINE = Pad<N>::LINE;
+  static_assert(SP::PER * R <= NV, "register array too small");
+#pragma unroll
+  for (int q = 0; q < SP::PER; ++q) {
+    const int idx = t + q * NTF;
+    base[q] = -1;
+    if (SP::total % NTF == 0 || idx < SP::total) {
+      const int l = idx / nR;
+      const int j = idx - l * nR;
+      const int k = j & (LS - 1);
+      const C* s = a + l * LINE + pix(j);
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[q * R + r] = s[r * (nR + nR / 16)];
+      if (LS > 1 && k != 0) {
+        const C* t3 = twl + twlds_off(LS) + 3 * k;
+        C w[R];
+        w[1] = t3[0];
+        if constexpr (R > 2) {
+          w[2] = cmul(t3[0], t3[0]);
+          w[3] = cmul(w[2], t3[0]);
+        }
+        if constexpr (R > 4) {
+          w[4] = t3[1];
+          w[5] = cmul(t3[1], t3[0]);
+          w[6] = cmul(t3[1], w[2]);
+          w[7] = cmul(t3[1], w[3]);
+        }
+        if constexpr (R > 8) {
+          w[8] = t3[2];
+#pragma unroll
+          for (int r = 1; r < 8; ++r) w[8 + r] = cmul(t3[2], w[r]);
+        }
+#pragma unroll
+        for (int r = 1; r < R; ++r) v[q * R + r] = cmul(v[q * R + r], w[r]);
+      }
+      base[q] = l * LINE + pix((j - k) * R + k);
+    }
+  }
+}
+
+template <typename C, int N, int NL, int NTF, int P, int NV>
+__device__ __forceinline__ void split_write(C* __restrict__ a, C (&v)[NV],
+                                            const int (&base)[SplitPass<N, NL, NTF, P>::PER]) {
+  using SP = SplitPass<N, NL, NTF, P>;
+  constexpr int R = SP::R, LS = SP::LS;
+  static_assert(SP::PER * R <= NV, "register array too small");
+#pragma unroll
+  for (int q = 0; q < SP::PER; ++q) {
+    if (base[q] >= 0) {
+      C u[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) u[r] = v[q * R + r];
+      dft_any<C, R>(u);
+      C* d = a + base[q];
+#pragma unroll
+      for (int r = 0; r < R; ++r) d[(LS == 1) ? r : r * (LS + LS / 16)] = u[r];
+    }
+  }
+}
+
 // Hartley unpack from a padded line (see hartley_pair).
 template <typename C, typename T>
 __device__ __forceinline__ void hartley_padded(const C* Z, int n, int k, T& ha, T& hb) {

@@ -10,6 +10,7 @@
 // (whole 64-B pieces instead of 8-B scattered stores).  The residual reads each input row
 // once per group with float4 loads over a sliding 3-row window (rows x-1, x, x+1).
 #pragma once
+#include <type_traits>
 #include "params.hpp"
 
 namespace pdhg {
@@ -335,6 +336,22 @@ __device__ __forceinline__ float expm1_neg(float x) {
   return x > -0.25f ? p : __expf(x) - 1.f;
 }
 
+// expm1 of two non-positive arguments: exp path everywhere, the cancellation-free Taylor
+// polynomial only in waves where some lane has |x| < 0.25 (the low-frequency modes, a few
+// waves) -- the branch is wave-uniform.
+__device__ __forceinline__ float2 expm1_neg2(float a, float b) {
+  float ea = __expf(a) - 1.f, eb = __expf(b) - 1.f;
+  const bool sa = a > -0.25f, sb = b > -0.25f;
+  if (__ballot(sa || sb) != 0) {
+    auto poly = [](float x) {
+      return x * (1.f + x * (0.5f + x * (1.f / 6 + x * (1.f / 24 + x * (1.f / 120 + x * (1.f / 720 + x * (1.f / 5040)))))));
+    };
+    if (sa) ea = poly(a);
+    if (sb) eb = poly(b);
+  }
+  return make_float2(ea, eb);
+}
+
 // Column-block x-transform + Thomas in t (fp32, nx = N a power of two).
 // A thread owns IT items (kx, l) of the block's NL complex lines; item (kx, l) carries the two
 // modes (kx, 2l) and (kx, 2l+1), which are exactly the real and imaginary parts of line l's
@@ -438,14 +455,14 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
     float t2[2];
     const float dl[2] = {0.5f * dd.x, 0.5f * dd.y};
 #pragma unroll
-    for (int h = 0; h < 2; ++h) t2[h] = log1pf(dl[h] + sqrtf(dl[h] * (dl[h] + 2.f)));   // cosh(th) = 1 + delta
+    for (int h = 0; h < 2; ++h) t2[h] = fmaxf(log1pf(dl[h] + sqrtf(dl[h] * (dl[h] + 2.f))), 1e-20f);   // cosh(th) = 1 + delta
     sth[item] = make_float2(t2[0], t2[1]);
     sE[item] = make_float2(expm1f(-2.f * t2[0] * (float)T), expm1f(-2.f * t2[1] * (float)T));   // E_{(T-2)+2}
   }
   // backward prefetch: step k consumes pf = b'_k (k < T-1); after each step pf <- pf2, pf2 <- b'_{k-2}
   ldrow(pf2, max(T - 2, 0));
   for (int k = T - 1; k >= 0; --k) {
-    const float kk1 = (float)(k + 1), gz = (float)(k + 1) / (float)(k + 2);   // theta = 0: g_k = (k+1)/(k+2)
+    const float kk1 = (float)(k + 1);
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       const int item = tid + i * NT;
@@ -453,18 +470,12 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
       if (k < T - 1 && !(p.dbg & 4)) {
         const C t2 = sth[item];
         const C e2 = sE[item];
-        const float tt[2] = {t2.x, t2.y}, ee[2] = {e2.x, e2.y}, pv[2] = {pf[i].x, pf[i].y};
-        float xx[2] = {x2.x, x2.y}, en[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const float t = tt[h];
-          const float E1 = expm1_neg(-2.f * t * kk1);
-          const float g = (t > 0.f) ? __expf(-t) * E1 * __frcp_rn(ee[h]) : gz;
-          xx[h] = pv[h] + g * xx[h];
-          en[h] = E1;
-        }
-        x2 = make_float2(xx[0], xx[1]);
-        sE[item] = make_float2(en[0], en[1]);
+        // theta >= 1e-20 (clamped at the sweep start): the closed form tends to (k+1)/(k+2) as theta -> 0
+        const float2 E1 = expm1_neg2(-2.f * t2.x * kk1, -2.f * t2.y * kk1);
+        const float g0 = __expf(-t2.x) * E1.x * __frcp_rn(e2.x);
+        const float g1 = __expf(-t2.y) * E1.y * __frcp_rn(e2.y);
+        x2 = make_float2(pf[i].x + g0 * x2.x, pf[i].y + g1 * x2.y);
+        sE[item] = E1;
         sbp[item] = x2;
       }
       A[(item & (NL - 1)) * LINE + pix(item >> lnl)] = x2;
@@ -482,6 +493,244 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
       hartley_padded<C, float>(A + (item & (NL - 1)) * LINE, N, item >> lnl, ha, hb);
       wk[item] = make_float2(ha, hb);
     }
+    lds_sync();
+  }
+}
+
+// ---- x-transform + Thomas, warp-specialised (fp32, nx = N a power of two, N*NL = 4096) ----
+// Waves 0-3 (the FFT group, 256 threads) run the three Stockham passes on buffer X while waves 4-7
+// (the Thomas group, 256 threads x 16 items) unpack buffer Y -- the previous t-row's transform --,
+// do that row's Thomas step, store it, and stage the next row into Y.  X and Y swap every step, so
+// a step costs max(FFT, Thomas) instead of their sum.  Each pass is split at its barrier
+// (split_read / split_write); both groups execute the same 6 LDS-only barriers per step.
+// Forward, step s = 0..T:   FFT(row s) | unpack FFT(row s-1) -> Thomas(s-1) -> b'_{s-1}; stage row s+1.
+// Backward, step s = 0..T+1: FFT(x_{T-s}) | unpack FFT(x_{T+1-s}) -> work; x_{T-1-s} = b' + g x -> Y.
+// Thomas carries (registers, per item of 2 modes): forward dd = 2 delta, h = 1 - g, b';
+// backward theta, E, x (same arithmetic as k_precond_xt_fast_2d).
+// LDS: 2 padded FFT buffers NL*(N + N/16) complex + twiddle seeds (~76 KiB).  grid: nb; block 512.
+template <int N, int NL>
+__global__ void __launch_bounds__(512) k_precond_xt_ws_2d(KP<float> p, const float2* __restrict__ twx) {
+  using C = float2;
+  constexpr int NTF = 256, NTT = 256;
+  constexpr int NI = N * NL;
+  constexpr int IT = NI / NTT;
+  constexpr int B = 2 * NL;
+  constexpr int LINE = Pad<N>::LINE;
+  constexpr int lnl = (NL == 1) ? 0 : (NL == 2) ? 1 : (NL == 4) ? 2 : 3;
+  constexpr int CH0 = (IT + 2) / 3, CH1 = (2 * IT + 2) / 3;   // Thomas chunks [0,CH0) [CH0,CH1) [CH1,IT)
+  static_assert(NI == 4096 && IT == 16, "sized for 4096 items per block");
+  using P0 = SplitPass<N, NL, NTF, 0>;
+  using P1 = SplitPass<N, NL, NTF, 1>;
+  using P2 = SplitPass<N, NL, NTF, 2>;
+  if (p.ctrl->done) return;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  C* buf0 = reinterpret_cast<C*>(smem_raw);
+  C* buf1 = buf0 + NL * LINE;
+  C* twl = buf1 + NL * LINE;
+  fill_twlds<C, N>(twl, twx);
+  const int T = p.T, tid = threadIdx.x;
+  const bool fftg = tid < NTF;                 // wave-uniform role
+  const int tt = fftg ? 0 : tid - NTF;         // Thomas-group thread
+  const int b = blockIdx.x;
+  constexpr int M = N * B;
+  float* wb = p.work + (size_t)b * M;
+  const size_t kstride = (size_t)p.nb * M;
+  const float ae = p.ae, inv_ae = 1.f / ae;
+  const int l = tt & (NL - 1);                 // line of every item of this thread (NTT % NL == 0)
+  const int loff = l * LINE;
+  auto kx_of = [&](int i) { return (tt + i * NTT) >> lnl; };
+  // one register set for both roles: the FFT group's butterfly values live in c1 (16 complex),
+  // which the Thomas group uses for its first carry -- each wave only ever takes one role
+  C c1[IT], c2[IT], c3[IT], pf[IT];
+  C (&vf)[IT] = c1;
+  auto ldrow = [&](int kk) {
+    const C* sn = reinterpret_cast<const C*>(wb + (size_t)kk * kstride);
+#pragma unroll
+    for (int i = 0; i < IT; ++i) pf[i] = sn[tt + i * NTT];
+  };
+  auto stage = [&](C* Y) {
+#pragma unroll
+    for (int i = 0; i < IT; ++i) Y[loff + pix(kx_of(i))] = pf[i];
+  };
+  int bs0[P0::PER], bs1[P1::PER], bs2[P2::PER];
+
+  if (!fftg) {
+    const float cm0 = p.C - p.lamy[b * B + 2 * l], cm1 = p.C - p.lamy[b * B + 2 * l + 1];
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const float lx = p.lamx[kx_of(i)];
+      c1[i] = make_float2((cm0 - lx) * inv_ae, (cm1 - lx) * inv_ae);
+      c2[i] = make_float2(1.f, 1.f);
+      c3[i] = make_float2(0.f, 0.f);
+    }
+    ldrow(0);
+    stage(buf0);
+    ldrow(min(1, T - 1));
+  }
+  lds_sync();
+
+  // ---------------- forward sweep ----------------
+  for (int s = 0; s <= T; ++s) {
+    C* X = (s & 1) ? buf1 : buf0;
+    C* Y = (s & 1) ? buf0 : buf1;
+    const bool fft_on = s < T && !(p.dbg & 1);
+    const int kr = (p.dbg & 4) ? -1 : s - 1;                        // row finished by the Thomas group this step
+    C* dst = reinterpret_cast<C*>(wb + (size_t)max(kr, 0) * kstride);
+    // one Thomas chunk [I0, I1): the uniform row test sits outside the item loop, so each chunk is
+    // straight-line code (all its LDS reads issue together)
+    auto thomas = [&](auto I0c, auto I1c) {
+      constexpr int I0 = decltype(I0c)::value, I1 = decltype(I1c)::value;
+      float ha[I1 - I0], hb[I1 - I0];
+#pragma unroll
+      for (int i = I0; i < I1; ++i) hartley_padded<C, float>(Y + loff, N, kx_of(i), ha[i - I0], hb[i - I0]);
+      if (kr < T - 1) {
+#pragma unroll
+        for (int i = I0; i < I1; ++i) {
+          const float s0 = c1[i].x + c2[i].x, s1 = c1[i].y + c2[i].y;
+          const float g0 = __frcp_rn(1.f + s0), g1 = __frcp_rn(1.f + s1);
+          c3[i] = make_float2((ha[i - I0] * inv_ae + c3[i].x) * g0, (hb[i - I0] * inv_ae + c3[i].y) * g1);
+          c2[i] = make_float2(s0 * g0, s1 * g1);
+          dst[tt + i * NTT] = c3[i];
+        }
+      } else {   // Neumann last row: u_{T-1} = ae (dd + h_{T-2})
+#pragma unroll
+        for (int i = I0; i < I1; ++i)
+          c3[i] = make_float2((ha[i - I0] * inv_ae + c3[i].x) / (c1[i].x + c2[i].x),
+                              (hb[i - I0] * inv_ae + c3[i].y) / (c1[i].y + c2[i].y));
+      }
+    };
+    using Z0 = std::integral_constant<int, 0>;
+    using ZA = std::integral_constant<int, CH0>;
+    using ZB = std::integral_constant<int, CH1>;
+    using ZC = std::integral_constant<int, IT>;
+    // P1
+    if (fftg) {
+      if (fft_on) split_read<C, N, NL, NTF, 0>(X, twl, tid, vf, bs0);
+    } else if (kr >= 0) {
+      thomas(Z0{}, ZA{});
+    }
+    lds_sync();
+    // P2
+    if (fftg) {
+      if (fft_on) split_write<C, N, NL, NTF, 0>(X, vf, bs0);
+    } else if (kr >= 0) {
+      thomas(ZA{}, ZB{});
+    }
+    lds_sync();
+    // P3
+    if (fftg) {
+      if (fft_on) split_read<C, N, NL, NTF, 1>(X, twl, tid, vf, bs1);
+    } else if (kr >= 0) {
+      thomas(ZB{}, ZC{});
+    }
+    lds_sync();
+    // P4: Y is no longer read -> stage row s+1 into it, prefetch row s+2
+    if (fftg) {
+      if (fft_on) split_write<C, N, NL, NTF, 1>(X, vf, bs1);
+    } else if (s + 1 < T) {
+      stage(Y);
+      ldrow(min(s + 2, T - 1));
+    }
+    lds_sync();
+    // P5
+    if (fftg && fft_on) split_read<C, N, NL, NTF, 2>(X, twl, tid, vf, bs2);
+    lds_sync();
+    // P6
+    if (fftg && fft_on) split_write<C, N, NL, NTF, 2>(X, vf, bs2);
+    lds_sync();
+  }
+
+  // ---------------- backward sweep ----------------
+  // x_k = b'_k + g_k x_{k+1},  g_k = ae/u_k = e^-th E_{k+1}/E_{k+2},  E_m = expm1(-2 th m)
+  if (!fftg) {
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const float dl0 = 0.5f * c1[i].x, dl1 = 0.5f * c1[i].y;
+      c1[i] = make_float2(fmaxf(log1pf(dl0 + sqrtf(dl0 * (dl0 + 2.f))), 1e-20f),
+                          fmaxf(log1pf(dl1 + sqrtf(dl1 * (dl1 + 2.f))), 1e-20f));
+      c2[i] = make_float2(expm1f(-2.f * c1[i].x * (float)T), expm1f(-2.f * c1[i].y * (float)T));   // E_{(T-2)+2}
+    }
+    ldrow(max(T - 2, 0));
+  }
+  for (int s = 0; s <= T + 1; ++s) {
+    C* X = (s & 1) ? buf1 : buf0;
+    C* Y = (s & 1) ? buf0 : buf1;
+    const bool fft_on = s >= 1 && s <= T && !(p.dbg & 1);
+    const int ku = T + 1 - s;                    // row unpacked by the Thomas group (if s >= 2)
+    const int kn = T - 1 - s;                    // x row computed by the Thomas group (if s <= T-1)
+    C* wk = reinterpret_cast<C*>(wb + (size_t)max(min(ku, T - 1), 0) * kstride);
+    const float kk1 = (float)(kn + 1);
+    auto unpack = [&](int i) {
+      float ha, hb;
+      hartley_padded<C, float>(Y + loff, N, kx_of(i), ha, hb);
+      wk[tt + i * NTT] = make_float2(ha, hb);
+    };
+    auto subst = [&](int i) {
+      // theta >= 1e-20 (clamped at the sweep start): the closed form tends to (k+1)/(k+2) as theta -> 0
+      const float2 E1 = expm1_neg2(-2.f * c1[i].x * kk1, -2.f * c1[i].y * kk1);
+      const float g0 = __expf(-c1[i].x) * E1.x * __frcp_rn(c2[i].x);
+      const float g1 = __expf(-c1[i].y) * E1.y * __frcp_rn(c2[i].y);
+      c3[i] = make_float2(pf[i].x + g0 * c3[i].x, pf[i].y + g1 * c3[i].y);
+      c2[i] = E1;
+    };
+    const bool do_unpack = s >= 2 && !(p.dbg & 4), do_subst = s >= 1 && s <= T - 1 && !(p.dbg & 4),
+               do_stage = s <= T - 1;
+    // P1
+    if (fftg) {
+      if (fft_on) split_read<C, N, NL, NTF, 0>(X, twl, tid, vf, bs0);
+    } else {
+      if (do_unpack) {
+#pragma unroll
+        for (int i = 0; i < CH0; ++i) unpack(i);
+      }
+      if (do_subst) {
+#pragma unroll
+        for (int i = 0; i < CH0; ++i) subst(i);
+      }
+    }
+    lds_sync();
+    // P2
+    if (fftg) {
+      if (fft_on) split_write<C, N, NL, NTF, 0>(X, vf, bs0);
+    } else {
+      if (do_unpack) {
+#pragma unroll
+        for (int i = CH0; i < CH1; ++i) unpack(i);
+      }
+      if (do_subst) {
+#pragma unroll
+        for (int i = CH0; i < CH1; ++i) subst(i);
+      }
+    }
+    lds_sync();
+    // P3
+    if (fftg) {
+      if (fft_on) split_read<C, N, NL, NTF, 1>(X, twl, tid, vf, bs1);
+    } else {
+      if (do_unpack) {
+#pragma unroll
+        for (int i = CH1; i < IT; ++i) unpack(i);
+      }
+      if (do_subst) {
+#pragma unroll
+        for (int i = CH1; i < IT; ++i) subst(i);
+      }
+    }
+    lds_sync();
+    // P4: Y is no longer read -> stage x_{kn} into it, prefetch b'_{kn-1}
+    if (fftg) {
+      if (fft_on) split_write<C, N, NL, NTF, 1>(X, vf, bs1);
+    } else if (do_stage) {
+#pragma unroll
+      for (int i = 0; i < IT; ++i) Y[loff + pix(kx_of(i))] = c3[i];
+      ldrow(max(kn - 1, 0));
+    }
+    lds_sync();
+    // P5
+    if (fftg && fft_on) split_read<C, N, NL, NTF, 2>(X, twl, tid, vf, bs2);
+    lds_sync();
+    // P6
+    if (fftg && fft_on) split_write<C, N, NL, NTF, 2>(X, vf, bs2);
     lds_sync();
   }
 }

@@ -104,7 +104,8 @@ struct Impl : ImplBase {
   size_t lds_res = 0, lds_xt = 0;
   // fast row kernels (fp32, power-of-two ny): RW rows per workgroup, NTf threads
   bool fast_rows = false;
-  bool fast_xt = false;            // fp32 power-of-two nx: k_precond_xt_fast_2d
+  bool fast_xt = false;
+  bool ws_xt = false;             // warp-specialised variant (k_precond_xt_ws_2d)            // fp32 power-of-two nx: k_precond_xt_fast_2d
   size_t lds_fast_xt = 0;
   int RWf = 8, NTf = 1024, g_fast_upd = 1;
   size_t lds_fast = 0;
@@ -208,8 +209,11 @@ struct Impl : ImplBase {
       if (const char* e = getenv("PDHG_DBG")) p.dbg = atoi(e);   // timing experiments only
       if (sizeof(R) == 4 && plx.pow2 && nx * (B / 2) == 4096 && nx >= 512) {
         fast_xt = true;
+        ws_xt = (nx == 4096);   // the other widths spill registers in the warp-specialised form
+        if (const char* e = getenv("PDHG_XT_WS")) ws_xt = atoi(e) != 0;   // tuning override
         // padded FFT buffer + theta, E, b' (float2 per item) + twiddle seeds (TwLds<nx>)
-        lds_fast_xt = (size_t)(4096 + 4096 / 16 + 3 * 4096 + 816) * sizeof(C);
+        lds_fast_xt = ws_xt ? (size_t)(2 * (4096 + 4096 / 16) + 816) * sizeof(C)
+                            : (size_t)(4096 + 4096 / 16 + 3 * 4096 + 816) * sizeof(C);
       }
       if (sizeof(R) == 4 && ny % 256 == 0) {
         fast_dual = true;
@@ -500,7 +504,15 @@ struct Impl : ImplBase {
             hipLaunchKernelGGL(kern, g, dim3(512), lds_fast_xt, stream, p, twx);
             return (int)PDHG_OK;
           };
-          switch (pb.nx) {
+          if (ws_xt) {
+            switch (pb.nx) {
+              case 4096: rc = go(k_precond_xt_ws_2d<4096, 1>); break;
+              case 2048: rc = go(k_precond_xt_ws_2d<2048, 2>); break;
+              case 1024: rc = go(k_precond_xt_ws_2d<1024, 4>); break;
+              case 512: rc = go(k_precond_xt_ws_2d<512, 8>); break;
+              default: rc = fail(PDHG_ERR_UNSUPPORTED, "no fast x kernel for nx=%d", pb.nx);
+            }
+          } else switch (pb.nx) {
             case 4096: rc = go(k_precond_xt_fast_2d<4096, 1, 512>); break;
             case 2048: rc = go(k_precond_xt_fast_2d<2048, 2, 512>); break;
             case 1024: rc = go(k_precond_xt_fast_2d<1024, 4, 512>); break;
