@@ -1,0 +1,45 @@
+"""t-slab decomposition (multi-GPU design) -- CPU checks.
+
+The partitioned Thomas sweep (oracle/slab_oracle.py) must reproduce the monolithic reference-form
+solve for every slab count, including uneven slabs and one-row slabs."""
+import numpy as np
+import pytest
+
+import pdhg_oracle as O
+import slab_oracle as S
+
+rng = np.random.default_rng(7)
+
+
+@pytest.mark.parametrize("T,P", [(1, 1), (5, 1), (5, 2), (7, 3), (8, 8), (13, 4), (40, 8)])
+def test_thomas_slabs_equals_monolithic(T, P):
+    M = 17
+    ae = 1.0 / (0.05 ** 2)
+    lam = -rng.uniform(0, 5e3, M)
+    diag = np.tile(1.0 - lam + 2 * ae, (T, 1))
+    diag[-1] -= ae
+    r = rng.standard_normal((T, M)) + 1j * rng.standard_normal((T, M))
+    ref = S.monolithic_tridiag(diag.astype(complex), r, ae)
+    out = S.thomas_slabs(diag, r, ae, P)
+    assert np.allclose(out, ref, rtol=1e-11, atol=1e-12 * np.abs(ref).max())
+
+
+def test_slab_bounds_cover_rows():
+    for T in (1, 7, 200):
+        for P in (1, 2, 3, 8):
+            if P > T:
+                continue
+            b = S.slab_bounds(T, P)
+            assert b[0][0] == 0 and b[-1][1] == T
+            assert all(b[q][1] == b[q + 1][0] and b[q][1] > b[q][0] for q in range(P - 1))
+
+
+@pytest.mark.parametrize("P", [2, 3, 5])
+def test_h1_precond_2d_slabs_equals_oracle(P):
+    nt, nx, ny = 11, 8, 6
+    dx, dy, dt = 2 / nx, 2 / ny, 0.02
+    fv = O.compute_Dxx_fft_fv(2, (nx, ny), (dx, dy), (0, 0))
+    src = rng.standard_normal((nt, nx, ny))
+    ref = O.H1_precond_2d(src, fv, dt, (0, 0), C=1.0)
+    out = S.h1_precond_2d_slabs(src, fv, dt, 1.0, P)
+    assert np.allclose(out, ref, rtol=1e-10, atol=1e-12)
