@@ -28,7 +28,7 @@ __device__ __forceinline__ R cont_residual_2d(const KP<R>& p, const R* __restric
   const int ym = nb_index(y - 1, ny, p.bcy), yp = nb_index(y + 1, ny, p.bcy);
   const R eps = (R)1e-4;
   const R r0 = rj[c];
-  const R rnext = (j + 1 < p.T) ? rho[(size_t)(j + 1) * plane + c] : (R)0;
+  const R rnext = (j + 1 < p.T) ? rho[(size_t)(j + 1) * plane + c] : p.last_slab ? (R)0 : p.rho_halo[c];
   // Dt_increasedim (utils_diff_op.py:193-206)
   R res = (rnext - r0) * p.inv_dt;
   if (p.epsl != (R)0) {   // Dxx/Dyy_increasedim (:241-253, :287-299)
@@ -81,7 +81,7 @@ __device__ __forceinline__ R cont_residual_2d(const KP<R>& p, const R* __restric
   const R div = (m1x_c - m1x_m) * p.inv_dx + (m2x_p - m2x_c) * p.inv_dx + (m1y_c - m1y_m) * p.inv_dy +
                 (m2y_p - m2y_c) * p.inv_dy;
   res = res - div;
-  if (j == p.T - 1) res = res + p.c_over_dt;   // update_fns_in_pdhg.py:95
+  if (j == p.T - 1 && p.last_slab) res = res + p.c_over_dt;   // update_fns_in_pdhg.py:95 (window's last row)
   return res;
 }
 

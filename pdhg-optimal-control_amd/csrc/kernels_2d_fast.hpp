@@ -65,7 +65,7 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const floa
   const float* a2x = p.alp[cur][1] + (size_t)j * plane;
   const float* a1y = (EGNO == 3) ? nullptr : p.alp[cur][2] + (size_t)j * plane;
   const float* a2y = (EGNO == 3) ? nullptr : p.alp[cur][3] + (size_t)j * plane;
-  const float cdt = (j == T - 1) ? p.c_over_dt : 0.f;
+  const float cdt = (j == T - 1 && p.last_slab) ? p.c_over_dt : 0.f;   // +c/dt on the window's last row
   const bool use_eps = p.epsl != 0.f;
 
   // Branch-free row loop: every load reads a valid address (rows/columns outside a Dirichlet edge
@@ -75,8 +75,10 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const floa
   const int xpl = nb_index(x0 + RW, nx, p.bcx);         // row below the group (uniform)
   const bool zm = xm0 < 0, zpl = xpl < 0;
   const int xm0c = zm ? x0 : xm0, xplc = zpl ? x0 + RW - 1 : xpl;
-  const bool last_j = (j + 1 >= T);
-  const float* rnx = last_j ? rj : p.rho[cur] + (size_t)(j + 1) * plane;   // rho row j+1 (zeroed if last)
+  // rho row j+1: local, or the next slab's first row (halo), or zero after the window's last row
+  const bool halo_j = (j + 1 >= T) && !p.last_slab;
+  const bool last_j = (j + 1 >= T) && p.last_slab;
+  const float* rnx = last_j ? rj : halo_j ? p.rho_halo : p.rho[cur] + (size_t)(j + 1) * plane;
   const int lane = threadIdx.x & (kWave - 1);
 #pragma unroll
   for (int gi = 0; gi < GPT; ++gi) {
@@ -352,6 +354,15 @@ __device__ __forceinline__ float2 expm1_neg2(float a, float b) {
   return make_float2(ea, eb);
 }
 
+// Thomas pivot state entering row j0 (t-slab decomposition): h_{j0-1} = 1 - g_{j0-1} in closed form,
+// h_k = expm1(-th) (1 + e^{-th (2k+3)}) / E_{k+2} (no cancellation; h_{-1} = 1; theta -> 0: 1/(k+2)).
+__device__ __forceinline__ float h_entry(float dd, int j0) {
+  if (j0 == 0) return 1.f;
+  const float dl = 0.5f * dd;
+  const float th = fmaxf(log1pf(dl + sqrtf(dl * (dl + 2.f))), 1e-20f);
+  return expm1f(-th) * (1.f + expf(-th * (float)(2 * j0 + 1))) / expm1f(-2.f * th * (float)(j0 + 1));
+}
+
 // Column-block x-transform + Thomas in t (fp32, nx = N a power of two).
 // A thread owns IT items (kx, l) of the block's NL complex lines; item (kx, l) carries the two
 // modes (kx, 2l) and (kx, 2l+1), which are exactly the real and imaginary parts of line l's
@@ -396,10 +407,12 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
     const int item = tid + i * NT;
     const int kx = item >> lnl, l = item & (NL - 1);
     const float lx = p.lamx[kx];
-    sth[item] = make_float2((p.C - lx - p.lamy[b * B + 2 * l]) * inv_ae, (p.C - lx - p.lamy[b * B + 2 * l + 1]) * inv_ae);
-    sE[item] = make_float2(1.f, 1.f);
+    const float dd0 = (p.C - lx - p.lamy[b * B + 2 * l]) * inv_ae, dd1 = (p.C - lx - p.lamy[b * B + 2 * l + 1]) * inv_ae;
+    sth[item] = make_float2(dd0, dd1);
+    sE[item] = make_float2(h_entry(dd0, p.j0), h_entry(dd1, p.j0));
     sbp[item] = make_float2(0.f, 0.f);
   }
+  if (p.xt_phase != 2) {
   ldrow(pf, 0);
   ldrow(pf2, min(1, T - 1));
   // ---------------- forward: DHT_x + elimination ----------------
@@ -418,7 +431,7 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
     lds_sync();
     if (!(p.dbg & 1)) lds_fft_inplace_tl<C, N, NL, NT>(A, twl);
     C* dst = reinterpret_cast<C*>(wb + (size_t)k * kstride);
-    if (k < T - 1) {
+    if (k < T - 1 || !p.last_slab) {
 #pragma unroll
       for (int i = 0; i < IT; ++i) {
         const int item = tid + i * NT;
@@ -441,11 +454,15 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
         float ha, hb;
         hartley_padded<C, float>(A + l * LINE, N, kx, ha, hb);
         const C dd = sth[item], h = sE[item], bp = sbp[item];
-        sbp[item] = make_float2((ha * inv_ae + bp.x) / (dd.x + h.x), (hb * inv_ae + bp.y) / (dd.y + h.y));
+        const C bn = make_float2((ha * inv_ae + bp.x) / (dd.x + h.x), (hb * inv_ae + bp.y) / (dd.y + h.y));
+        sbp[item] = bn;
+        if (p.slab) dst[item] = bn;   // re-read (after the carry fix-up) by the backward sweep
       }
     }
     lds_sync();
   }
+  }   // xt_phase != 2
+  if (p.xt_phase == 1) return;   // forward sweep only (t-slab: the carry fix-up runs in between)
   // ---------------- backward: substitution + inverse DHT_x ----------------
   // x_k = b'_k + g_k x_{k+1},  g_k = ae/u_k = e^-th E_{k+1}/E_{k+2}
 #pragma unroll
@@ -457,17 +474,22 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
 #pragma unroll
     for (int h = 0; h < 2; ++h) t2[h] = fmaxf(log1pf(dl[h] + sqrtf(dl[h] * (dl[h] + 2.f))), 1e-20f);   // cosh(th) = 1 + delta
     sth[item] = make_float2(t2[0], t2[1]);
-    sE[item] = make_float2(expm1f(-2.f * t2[0] * (float)T), expm1f(-2.f * t2[1] * (float)T));   // E_{(T-2)+2}
+    // E_{k+2} for the first substituted row: k = T-2 (single context) or T-1 (slab, from the right carry)
+    const float e0 = (float)(p.j0 + T + (p.slab ? 1 : 0));
+    sE[item] = make_float2(expm1f(-2.f * t2[0] * e0), expm1f(-2.f * t2[1] * e0));
+    if (p.slab) sbp[item] = p.carry_y ? reinterpret_cast<const C*>(p.carry_y + (size_t)b * M)[item] : make_float2(0.f, 0.f);
   }
-  // backward prefetch: step k consumes pf = b'_k (k < T-1); after each step pf <- pf2, pf2 <- b'_{k-2}
+  // backward prefetch: step k consumes pf = b'_k (k < T-1; slab: every k, from the fixed-up rows);
+  // after each step pf <- pf2, pf2 <- b'_{k-2}
+  if (p.slab) ldrow(pf, T - 1);
   ldrow(pf2, max(T - 2, 0));
   for (int k = T - 1; k >= 0; --k) {
-    const float kk1 = (float)(k + 1);
+    const float kk1 = (float)(p.j0 + k + 1);   // global row index
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       const int item = tid + i * NT;
       C x2 = sbp[item];
-      if (k < T - 1 && !(p.dbg & 4)) {
+      if ((k < T - 1 || p.slab) && !(p.dbg & 4)) {
         const C t2 = sth[item];
         const C e2 = sE[item];
         // theta >= 1e-20 (clamped at the sweep start): the closed form tends to (k+1)/(k+2) as theta -> 0
@@ -560,17 +582,22 @@ __global__ void __launch_bounds__(512) k_precond_xt_ws_2d(KP<float> p, const flo
     for (int i = 0; i < IT; ++i) {
       const float lx = p.lamx[kx_of(i)];
       c1[i] = make_float2((cm0 - lx) * inv_ae, (cm1 - lx) * inv_ae);
-      c2[i] = make_float2(1.f, 1.f);
-      c3[i] = make_float2(0.f, 0.f);
     }
-    ldrow(0);
-    stage(buf0);
-    ldrow(min(1, T - 1));
+    if (p.xt_phase != 2) {
+#pragma unroll
+      for (int i = 0; i < IT; ++i) {
+        c2[i] = make_float2(h_entry(c1[i].x, p.j0), h_entry(c1[i].y, p.j0));
+        c3[i] = make_float2(0.f, 0.f);
+      }
+      ldrow(0);
+      stage(buf0);
+      ldrow(min(1, T - 1));
+    }
   }
   lds_sync();
 
   // ---------------- forward sweep ----------------
-  for (int s = 0; s <= T; ++s) {
+  for (int s = 0; s <= T && p.xt_phase != 2; ++s) {
     C* X = (s & 1) ? buf1 : buf0;
     C* Y = (s & 1) ? buf0 : buf1;
     const bool fft_on = s < T && !(p.dbg & 1);
@@ -583,7 +610,7 @@ __global__ void __launch_bounds__(512) k_precond_xt_ws_2d(KP<float> p, const flo
       float ha[I1 - I0], hb[I1 - I0];
 #pragma unroll
       for (int i = I0; i < I1; ++i) hartley_padded<C, float>(Y + loff, N, kx_of(i), ha[i - I0], hb[i - I0]);
-      if (kr < T - 1) {
+      if (kr < T - 1 || !p.last_slab) {
 #pragma unroll
         for (int i = I0; i < I1; ++i) {
           const float s0 = c1[i].x + c2[i].x, s1 = c1[i].y + c2[i].y;
@@ -594,9 +621,11 @@ __global__ void __launch_bounds__(512) k_precond_xt_ws_2d(KP<float> p, const flo
         }
       } else {   // Neumann last row: u_{T-1} = ae (dd + h_{T-2})
 #pragma unroll
-        for (int i = I0; i < I1; ++i)
+        for (int i = I0; i < I1; ++i) {
           c3[i] = make_float2((ha[i - I0] * inv_ae + c3[i].x) / (c1[i].x + c2[i].x),
                               (hb[i - I0] * inv_ae + c3[i].y) / (c1[i].y + c2[i].y));
+          if (p.slab) dst[tt + i * NTT] = c3[i];   // re-read (after the carry fix-up) by the backward sweep
+        }
       }
     };
     using Z0 = std::integral_constant<int, 0>;
@@ -642,15 +671,20 @@ __global__ void __launch_bounds__(512) k_precond_xt_ws_2d(KP<float> p, const flo
 
   // ---------------- backward sweep ----------------
   // x_k = b'_k + g_k x_{k+1},  g_k = ae/u_k = e^-th E_{k+1}/E_{k+2},  E_m = expm1(-2 th m)
+  if (p.xt_phase == 1) return;   // forward sweep only (t-slab: the carry fix-up runs in between)
   if (!fftg) {
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       const float dl0 = 0.5f * c1[i].x, dl1 = 0.5f * c1[i].y;
       c1[i] = make_float2(fmaxf(log1pf(dl0 + sqrtf(dl0 * (dl0 + 2.f))), 1e-20f),
                           fmaxf(log1pf(dl1 + sqrtf(dl1 * (dl1 + 2.f))), 1e-20f));
-      c2[i] = make_float2(expm1f(-2.f * c1[i].x * (float)T), expm1f(-2.f * c1[i].y * (float)T));   // E_{(T-2)+2}
+      // E_{k+2} for the first substituted row: k = T-2 (single context) or T-1 (slab, from the right carry)
+      const float e0 = (float)(p.j0 + T + (p.slab ? 1 : 0));
+      c2[i] = make_float2(expm1f(-2.f * c1[i].x * e0), expm1f(-2.f * c1[i].y * e0));
+      if (p.slab)
+        c3[i] = p.carry_y ? reinterpret_cast<const C*>(p.carry_y + (size_t)b * M)[tt + i * NTT] : make_float2(0.f, 0.f);
     }
-    ldrow(max(T - 2, 0));
+    ldrow(p.slab ? T - 1 : max(T - 2, 0));
   }
   for (int s = 0; s <= T + 1; ++s) {
     C* X = (s & 1) ? buf1 : buf0;
@@ -659,7 +693,7 @@ __global__ void __launch_bounds__(512) k_precond_xt_ws_2d(KP<float> p, const flo
     const int ku = T + 1 - s;                    // row unpacked by the Thomas group (if s >= 2)
     const int kn = T - 1 - s;                    // x row computed by the Thomas group (if s <= T-1)
     C* wk = reinterpret_cast<C*>(wb + (size_t)max(min(ku, T - 1), 0) * kstride);
-    const float kk1 = (float)(kn + 1);
+    const float kk1 = (float)(p.j0 + kn + 1);   // global row index
     auto unpack = [&](int i) {
       float ha, hb;
       hartley_padded<C, float>(Y + loff, N, kx_of(i), ha, hb);
@@ -673,7 +707,7 @@ __global__ void __launch_bounds__(512) k_precond_xt_ws_2d(KP<float> p, const flo
       c3[i] = make_float2(pf[i].x + g0 * c3[i].x, pf[i].y + g1 * c3[i].y);
       c2[i] = E1;
     };
-    const bool do_unpack = s >= 2 && !(p.dbg & 4), do_subst = s >= 1 && s <= T - 1 && !(p.dbg & 4),
+    const bool do_unpack = s >= 2 && !(p.dbg & 4), do_subst = (s >= 1 || p.slab) && s <= T - 1 && !(p.dbg & 4),
                do_stage = s <= T - 1;
     // P1
     if (fftg) {

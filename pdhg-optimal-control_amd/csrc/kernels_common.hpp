@@ -138,3 +138,83 @@ __global__ void k_copy(R* __restrict__ dst, const R* __restrict__ src, size_t n)
 }
 
 }  // namespace pdhg
+
+// ---------------- t-slab decomposition (multi-GPU), see oracle/slab_oracle.py ----------------
+namespace pdhg {
+
+// Fold a partial-sum table into one row of kNumSums doubles (the vector the ranks all-reduce);
+// add0 is added to sums 1 and 2 (the fixed phi row 0 in the primal sums, first slab only).
+__global__ void __launch_bounds__(256) k_reduce_vec(const double* partials, int nrows, int ns, double add0,
+                                                    double* out) {
+  __shared__ double o[kNumSums];
+  reduce_partials(partials, nrows, ns, o);
+  if (threadIdx.x < kNumSums) out[threadIdx.x] = (threadIdx.x < ns ? o[threadIdx.x] : 0.0) +
+                                                 ((threadIdx.x == 1 || threadIdx.x == 2) ? add0 : 0.0);
+}
+
+// Per spectral mode m of the work-row layout (2-D: m = (b*nx + kx)*B + c, ky = b*B + c):
+//   c   = prefix scan of the upstream slabs' outgoing planes  (c = D_q + G_q c, q < rank)
+//   b_k += P_k c for the local rows (P_k = prod g_{j0..k}, g from the pivot recurrence), and
+//   X0  = sum_k P'_k b_k  (the zero-right-carry backward value at j0, P'_k = prod g_{j0..k-1}).
+// G mode (allD == null): only G = prod_k g_k is written to out (iteration-invariant, once per context).
+template <typename R>
+__global__ void __launch_bounds__(256) k_slab_fixup(KP<R> p, const R* __restrict__ allD, const R* __restrict__ allG,
+                                                    int rank, R* __restrict__ out) {
+  if (allD && p.ctrl->done) return;
+  const int nx = p.nx, B = p.B;
+  const size_t M = (size_t)p.nb * nx * B;
+  const size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  const int c = (int)(m % B);
+  const size_t bx = m / B;
+  const int kx = (int)(bx % nx), b = (int)(bx / nx);
+  const double inv_ae = 1.0 / (double)p.ae;
+  const double dd = ((double)p.C - (double)p.lamx[kx] - (double)p.lamy[b * B + c]) * inv_ae;
+  // pivot state entering row j0 (closed form, see h_entry)
+  double h = 1.0;
+  if (p.j0 > 0) {
+    const double dl = 0.5 * dd;
+    const double th = fmax(log1p(dl + sqrt(dl * (dl + 2.0))), 1e-300);
+    h = expm1(-th) * (1.0 + exp(-th * (2.0 * p.j0 + 1.0))) / expm1(-2.0 * th * (p.j0 + 1.0));
+  }
+  double cin = 0.0;
+  if (allD)
+    for (int q = 0; q < rank; ++q) cin = (double)allD[(size_t)q * M + m] + (double)allG[(size_t)q * M + m] * cin;
+  double P = 1.0, x0 = 0.0;
+  for (int k = 0; k < p.T; ++k) {
+    const bool last = p.last_slab && k == p.T - 1;
+    const double s = dd + h;
+    const double g = last ? 1.0 / s : 1.0 / (1.0 + s);
+    h = s * g;
+    const double Pn = P * g;
+    if (allD) {
+      R* w = p.work + (size_t)k * M + m;
+      const double bf = (double)*w + Pn * cin;
+      if (rank > 0) *w = (R)bf;
+      x0 += P * bf;
+    }
+    P = Pn;
+  }
+  out[m] = allD ? (R)x0 : (R)P;
+}
+
+// rho row 0 of the current buffer set (the set index lives on the device)
+template <typename R>
+__global__ void __launch_bounds__(256) k_copy_cur_rho(KP<R> p, R* __restrict__ dst, size_t n) {
+  const R* src = p.rho[p.ctrl->cur];
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+
+// Right carry y of slab `rank`: suffix scan y = X0_q + G_q y over the downstream slabs q > rank.
+template <typename R>
+__global__ void __launch_bounds__(256) k_slab_right_carry(const R* __restrict__ allX0, const R* __restrict__ allG,
+                                                          int rank, int nranks, size_t M, R* __restrict__ y) {
+  const size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  double v = 0.0;
+  for (int q = nranks - 1; q > rank; --q) v = (double)allX0[(size_t)q * M + m] + (double)allG[(size_t)q * M + m] * v;
+  y[m] = (R)v;
+}
+
+}  // namespace pdhg

@@ -34,6 +34,12 @@ struct KP {
   R* alp[2][4];            // live control components, each [T][nx][ny]
   double* partials;        // [blocks][kNumSums]
   Ctrl* ctrl;
+  // t-slab decomposition (multi-GPU): this context owns unknown rows [j0, j0+T) of Tg.
+  // slab == 0 -> j0 = 0, Tg = T, last_slab = 1 and no halos (single-context path).
+  int slab, j0, Tg, last_slab;
+  int xt_phase;            // x-transform/Thomas kernel: 0 both sweeps, 1 forward only, 2 backward only
+  const R* rho_halo;       // rho row j0+T (first row of the next slab) [nx][ny]; null on the last slab
+  const R* carry_y;        // backward right carry x_{j0+T} (spectral, work-row layout); null = zero
 };
 
 // neighbour index along an axis of length n with boundary condition bc

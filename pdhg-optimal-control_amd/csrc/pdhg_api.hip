@@ -116,6 +116,14 @@ struct Impl : ImplBase {
   bool prof = false;
   std::map<std::string, ProfEntry> prof_ev;
   int* h_done = nullptr;   // pinned
+  bool own_stream = true;
+  // t-slab decomposition (multi-GPU): this context owns unknown rows [slab_j0, slab_j0 + T) of slab_Tg
+  bool slab = false;
+  int slab_j0 = 0, slab_Tg = 0;
+  size_t Mspec = 0;          // spectral plane (work row) size
+  R* halo_rho = nullptr;     // rho row j0+T from the next slab
+  R* carry_y = nullptr;      // backward right carry (spectral plane)
+  R* x0buf = nullptr;        // X0 plane of this slab (zero-right-carry backward value at j0)
 
   ~Impl() override {
     if (stream) hipStreamSynchronize(stream);
@@ -126,7 +134,7 @@ struct Impl : ImplBase {
         hipEventDestroy(e.second);
       }
     if (h_done) hipHostFree(h_done);
-    if (stream) hipStreamDestroy(stream);
+    if (stream && own_stream) hipStreamDestroy(stream);
   }
 
   template <typename T>
@@ -265,6 +273,14 @@ struct Impl : ImplBase {
     g_outer = 2048;
     partial_rows = std::max<size_t>(
         {(size_t)gx4 * g4, (size_t)gx5 * g5, (size_t)g_outer, (size_t)g_fast_upd, (size_t)gxd * gyd * gzd, 1});
+    p.slab = slab ? 1 : 0;
+    p.j0 = slab ? slab_j0 : 0;
+    p.Tg = slab ? slab_Tg : T;
+    p.last_slab = (p.j0 + T == p.Tg) ? 1 : 0;
+    p.xt_phase = 0;
+    if (slab && !(is2d && fast_xt))
+      return fail(PDHG_ERR_UNSUPPORTED, "t-slab decomposition needs ndim 2, fp32 and a power-of-two nx in "
+                                        "[512, 4096] (fast x-transform kernels)");
 
     // ---- device buffers ----
     const size_t npl = plane();
@@ -285,6 +301,16 @@ struct Impl : ImplBase {
     for (int a = na; a < 4; ++a) p.alp[0][a] = p.alp[1][a] = nullptr;
     if ((rc = alloc(&p.partials, partial_rows * kNumSums))) return rc;
     if ((rc = alloc(&p.ctrl, 1))) return rc;
+    if (slab) {
+      Mspec = (size_t)p.nb * nx * p.B;
+      if ((rc = alloc(&halo_rho, npl))) return rc;
+      if ((rc = alloc(&carry_y, Mspec))) return rc;
+      if ((rc = alloc(&x0buf, Mspec))) return rc;
+      HIP_TRY(hipMemsetAsync(halo_rho, 0, npl * sizeof(R), stream));
+      HIP_TRY(hipMemsetAsync(carry_y, 0, Mspec * sizeof(R), stream));
+      p.rho_halo = p.last_slab ? nullptr : halo_rho;
+      p.carry_y = carry_y;
+    }
     HIP_TRY(hipMemsetAsync(p.ctrl, 0, sizeof(Ctrl), stream));
 
     // ---- coefficient / symbol tables (host fp64 -> R) ----
@@ -438,13 +464,18 @@ struct Impl : ImplBase {
   };
 
   // ---------------- launches ----------------
-  int launch_primal(R tau) {
+  // stages: 1 residual (+ forward y transform), 2 x transform + Thomas (sweeps per xt_phase: 0 both,
+  // 1 forward, 2 backward), 4 inverse transforms + phi/phi_bar update + primal sums.  sums_out != null
+  // (t-slab mode): the primal sums go to that vector (all-reduced by the caller) instead of ctrl.
+  int launch_primal(R tau, int stages = 7, int xt_phase = 0, double* sums_out = nullptr) {
     KP<R> p = kp;
     p.tau = tau;
+    p.xt_phase = xt_phase;
     const int T = pb.T;
     if (pb.ndim == 2) {
-      int rc;
-      if (fast_rows) {
+      int rc = PDHG_OK;
+      if (!(stages & 1)) {
+      } else if (fast_rows) {
         ProfScope ps(this, "residual");
         rc = with_fast_rows([&](auto Nc, auto RWc, auto NTc) {
           constexpr int N_ = decltype(Nc)::value, RW_ = decltype(RWc)::value, NT_ = decltype(NTc)::value;
@@ -493,7 +524,8 @@ struct Impl : ImplBase {
         });
         if (rc) return rc;
       }
-      if (fast_xt) {
+      if (!(stages & 2)) {
+      } else if (fast_xt) {
         ProfScope ps(this, "precond");
         rc = PDHG_OK;
         if constexpr (sizeof(R) == 4) {
@@ -524,6 +556,7 @@ struct Impl : ImplBase {
       } else {
         ProfScope ps(this, "precond");
         dim3 g(p.nb);
+        if (xt_phase != 0) return fail(PDHG_ERR_UNSUPPORTED, "t-slab sweeps need the fp32 power-of-two x kernels");
         rc = with_xt_fft([&](auto f) {
           using F = decltype(f);
           int r2;
@@ -532,6 +565,10 @@ struct Impl : ImplBase {
           return (int)PDHG_OK;
         });
         if (rc) return rc;
+      }
+      if (!(stages & 4)) {
+        HIP_TRY(hipGetLastError());
+        return PDHG_OK;
       }
       int upd_rows = gx4 * g4;
       if (fast_rows) {
@@ -559,7 +596,11 @@ struct Impl : ImplBase {
         });
         if (rc) return rc;
       }
-      hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(256), 0, stream, p.partials, upd_rows, row0_sq, p.ctrl);
+      if (sums_out)
+        hipLaunchKernelGGL(k_reduce_vec, dim3(1), dim3(256), 0, stream, p.partials, upd_rows, 3,
+                           kp.j0 == 0 ? row0_sq : 0.0, sums_out);
+      else
+        hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(256), 0, stream, p.partials, upd_rows, row0_sq, p.ctrl);
     } else {
       int rc;
       {
@@ -716,6 +757,128 @@ struct Impl : ImplBase {
       st->nan_seen = h.nan_seen;
     }
     primal_done = false;
+    return PDHG_OK;
+  }
+
+  // ---------------- t-slab phases (multi-GPU; the caller moves planes between slabs) ----------------
+  // One outer iteration of a slab = slab_forward -> [allgather D] -> slab_fixup -> [allgather X0] ->
+  // slab_backward -> [allreduce sums] -> slab_primal_finalize -> [phi_bar / rho halos] ->
+  // per dual sub-iteration: slab_dual -> [allreduce] -> slab_dual_finalize -> slab_outer ->
+  // [allreduce] -> slab_outer_finalize.  With one slab this is exactly iterate().
+  int need_slab() const { return slab ? PDHG_OK : fail(PDHG_ERR_STATE, "not a t-slab context"); }
+  int slab_G(R* out) {
+    hipLaunchKernelGGL((k_slab_fixup<R>), dim3((unsigned)((Mspec + 255) / 256)), dim3(256), 0, stream, kp,
+                       (const R*)nullptr, (const R*)nullptr, 0, out);
+    HIP_TRY(hipGetLastError());
+    return PDHG_OK;
+  }
+  int slab_forward(R tau) { return launch_primal(tau, 1 | 2, 1); }
+  int slab_fixup(const R* allD, const R* allG, int rank) {
+    hipLaunchKernelGGL((k_slab_fixup<R>), dim3((unsigned)((Mspec + 255) / 256)), dim3(256), 0, stream, kp, allD, allG,
+                       rank, x0buf);
+    HIP_TRY(hipGetLastError());
+    return PDHG_OK;
+  }
+  int slab_backward(R tau, const R* allX0, const R* allG, int rank, int nranks, double* sums) {
+    hipLaunchKernelGGL((k_slab_right_carry<R>), dim3((unsigned)((Mspec + 255) / 256)), dim3(256), 0, stream, allX0,
+                       allG, rank, nranks, Mspec, carry_y);
+    return launch_primal(tau, 2 | 4, 2, sums);
+  }
+  int slab_primal_finalize(const double* sums) {
+    hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(256), 0, stream, sums, 1, 0.0, kp.ctrl);
+    HIP_TRY(hipGetLastError());
+    return PDHG_OK;
+  }
+  int slab_dual(R sigma, int k, int sub, double* sums) {
+    KP<R> p = kp;
+    p.sigma = sigma;
+    p.inplace = (k <= 1) ? 1 : 0;
+    p.sub = sub;
+    if (!p.inplace && !two_sets)
+      return fail(PDHG_ERR_STATE, "rho_alp_iters=%d needs a context created with rho_alp_iters > 1", k);
+    {
+      ProfScope ps(this, "dual");
+      if (pb.ndim == 2 && fast_dual) {
+        launch_dual_fast(p);
+      } else {
+        dim3 g(gx5, g5);
+        switch (pb.egno) {
+          case 1: hipLaunchKernelGGL((k_dual_2d<R, 1>), g, dim3(256), 0, stream, p); break;
+          case 2: hipLaunchKernelGGL((k_dual_2d<R, 2>), g, dim3(256), 0, stream, p); break;
+          default: hipLaunchKernelGGL((k_dual_2d<R, 3>), g, dim3(256), 0, stream, p); break;
+        }
+      }
+    }
+    const int nrows_d = fast_dual ? gxd * gyd * gzd : gx5 * g5;
+    hipLaunchKernelGGL(k_reduce_vec, dim3(1), dim3(256), 0, stream, p.partials, nrows_d, 3 + 3 * na, 0.0, sums);
+    HIP_TRY(hipGetLastError());
+    return PDHG_OK;
+  }
+  int slab_dual_finalize(double eps, int sub, const double* sums) {
+    hipLaunchKernelGGL(k_finalize_dual, dim3(1), dim3(256), 0, stream, sums, 1, na, n_dead, eps, sub, kp.ctrl);
+    HIP_TRY(hipGetLastError());
+    return PDHG_OK;
+  }
+  int slab_outer(int k, double* sums) {
+    if (k > 1) {
+      hipLaunchKernelGGL((k_outer_sums<R>), dim3(g_outer), dim3(256), 0, stream, kp, (size_t)pb.T * plane());
+      hipLaunchKernelGGL(k_reduce_vec, dim3(1), dim3(256), 0, stream, kp.partials, g_outer, kNumSums, 0.0, sums);
+    }
+    HIP_TRY(hipGetLastError());
+    return PDHG_OK;
+  }
+  int slab_outer_finalize(double eps, int k, const double* sums) {
+    hipLaunchKernelGGL(k_finalize_outer, dim3(1), dim3(256), 0, stream, sums, k > 1 ? 1 : 0, na, eps, k > 1 ? 1 : 0,
+                       stop_conv, stop_nan, kp.ctrl);
+    HIP_TRY(hipGetLastError());
+    return PDHG_OK;
+  }
+  // planes out: 0 rho row 0 (current set), 1 phi_bar row T, 2 D = work row T-1, 3 X0
+  int slab_plane_out(int which, void* dst) {
+    const size_t npl = plane();
+    switch (which) {
+      case 0:
+        hipLaunchKernelGGL((k_copy_cur_rho<R>), dim3(1024), dim3(256), 0, stream, kp, (R*)dst, npl);
+        break;
+      case 1: HIP_TRY(hipMemcpyAsync(dst, kp.phibar + (size_t)pb.T * npl, npl * sizeof(R), hipMemcpyDeviceToDevice, stream)); break;
+      case 2: HIP_TRY(hipMemcpyAsync(dst, kp.work + (size_t)(pb.T - 1) * Mspec, Mspec * sizeof(R), hipMemcpyDeviceToDevice, stream)); break;
+      case 3: HIP_TRY(hipMemcpyAsync(dst, x0buf, Mspec * sizeof(R), hipMemcpyDeviceToDevice, stream)); break;
+      default: return fail(PDHG_ERR_ARG, "unknown plane %d", which);
+    }
+    HIP_TRY(hipGetLastError());
+    return PDHG_OK;
+  }
+  // planes in: 0 rho halo (next slab's rho row 0), 1 phi_bar row 0 (previous slab's phi_bar row T)
+  int slab_plane_in(int which, const void* src) {
+    const size_t npl = plane();
+    switch (which) {
+      case 0: HIP_TRY(hipMemcpyAsync(halo_rho, src, npl * sizeof(R), hipMemcpyDeviceToDevice, stream)); break;
+      case 1: HIP_TRY(hipMemcpyAsync(kp.phibar, src, npl * sizeof(R), hipMemcpyDeviceToDevice, stream)); break;
+      default: return fail(PDHG_ERR_ARG, "unknown plane %d", which);
+    }
+    return PDHG_OK;
+  }
+  int set_stream(hipStream_t s) {
+    HIP_TRY(hipStreamSynchronize(stream));
+    if (own_stream) HIP_TRY(hipStreamDestroy(stream));
+    stream = s;
+    own_stream = false;
+    return PDHG_OK;
+  }
+  int slab_status(pdhg_stats* st) {
+    Ctrl h;
+    int rc;
+    if ((rc = read_ctrl(h))) return rc;
+    st->iters_run = h.iters;
+    st->status = h.done;
+    st->inner_last = h.inner_count;
+    st->inner_total = h.inner_total;
+    st->err1 = h.err1;
+    st->err2 = h.err2;
+    st->err_inner = h.err_inner;
+    st->rho_min = NAN;
+    st->rho_max = NAN;
+    st->nan_seen = h.nan_seen;
     return PDHG_OK;
   }
 
@@ -918,6 +1081,16 @@ int dispatch(pdhg_ctx* ctx, F&& f) {
   return f(*static_cast<Impl<float>*>(b->impl.get()));
 }
 
+template <typename F>
+int slab_dispatch(pdhg_ctx* ctx, F&& f) {
+  if (!ctx) return fail(PDHG_ERR_ARG, "null context");
+  CtxBox* b = reinterpret_cast<CtxBox*>(ctx);
+  if (b->precision != 4) return fail(PDHG_ERR_STATE, "not a t-slab context");
+  auto& im = *static_cast<Impl<float>*>(b->impl.get());
+  int rc = im.need_slab();
+  return rc ? rc : f(im);
+}
+
 }  // namespace
 
 extern "C" {
@@ -1077,6 +1250,105 @@ int pdhg_algorithmic_bytes(pdhg_ctx* ctx, int k, const char* cls, double* bytes)
   return dispatch(ctx, [&](auto& im) {
     *bytes = im.algorithmic_bytes(k, cls);
     return *bytes < 0 ? fail(PDHG_ERR_ARG, "unknown kernel class %s", cls) : (int)PDHG_OK;
+  });
+}
+
+/* ---------------- t-slab decomposition ---------------- */
+int pdhg_create_slab(const pdhg_problem* prob, int j0, int T_total, int device, pdhg_ctx** out) {
+  if (!prob || !out) return fail(PDHG_ERR_ARG, "null argument");
+  *out = nullptr;
+  if (j0 < 0 || prob->T < 1 || j0 + prob->T > T_total)
+    return fail(PDHG_ERR_ARG, "slab rows [%d, %d) outside the window of %d rows", j0, j0 + prob->T, T_total);
+  if (prob->precision != 4) return fail(PDHG_ERR_UNSUPPORTED, "t-slab decomposition is fp32 only");
+  if (prob->ndim != 2) return fail(PDHG_ERR_UNSUPPORTED, "t-slab decomposition is 2-D only");
+  // validate the rest exactly like pdhg_create, then rebuild as a slab
+  pdhg_ctx* probe = nullptr;
+  pdhg_problem q = *prob;
+  q.T = 1;
+  int rc = pdhg_create(&q, device, &probe);
+  if (rc) return rc;
+  pdhg_destroy(probe);
+  auto box = std::make_unique<CtxBox>();
+  box->precision = 4;
+  auto im = std::make_unique<Impl<float>>();
+  im->pb = *prob;
+  im->device = device;
+  im->slab = true;
+  im->slab_j0 = j0;
+  im->slab_Tg = T_total;
+  rc = im->setup();
+  box->impl = std::move(im);
+  if (rc) return rc;
+  *out = reinterpret_cast<pdhg_ctx*>(box.release());
+  return PDHG_OK;
+}
+
+int pdhg_set_stream(pdhg_ctx* ctx, void* hip_stream) {   // null = the device's default stream
+  return dispatch(ctx, [&](auto& im) { return im.set_stream(static_cast<hipStream_t>(hip_stream)); });
+}
+int pdhg_slab_begin(pdhg_ctx* ctx) {
+  return slab_dispatch(ctx, [&](auto& im) { return im.reset_ctrl(); });
+}
+int pdhg_slab_carry_gain(pdhg_ctx* ctx, void* G_out) {
+  if (!G_out) return fail(PDHG_ERR_ARG, "null G plane");
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_G(static_cast<float*>(G_out)); });
+}
+int pdhg_slab_forward(pdhg_ctx* ctx, double tau) {
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_forward((float)tau); });
+}
+int pdhg_slab_fixup(pdhg_ctx* ctx, const void* all_D, const void* all_G, int rank) {
+  if (!all_D || !all_G) return fail(PDHG_ERR_ARG, "null carry planes");
+  return slab_dispatch(ctx, [&](auto& im) {
+    return im.slab_fixup(static_cast<const float*>(all_D), static_cast<const float*>(all_G), rank);
+  });
+}
+int pdhg_slab_backward(pdhg_ctx* ctx, double tau, const void* all_X0, const void* all_G, int rank, int nranks,
+                       double* sums) {
+  if (!all_X0 || !all_G || !sums) return fail(PDHG_ERR_ARG, "null argument");
+  if (rank < 0 || rank >= nranks) return fail(PDHG_ERR_ARG, "rank %d of %d", rank, nranks);
+  return slab_dispatch(ctx, [&](auto& im) {
+    return im.slab_backward((float)tau, static_cast<const float*>(all_X0), static_cast<const float*>(all_G), rank,
+                            nranks, sums);
+  });
+}
+int pdhg_slab_primal_finalize(pdhg_ctx* ctx, const double* sums) {
+  if (!sums) return fail(PDHG_ERR_ARG, "null sums");
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_primal_finalize(sums); });
+}
+int pdhg_slab_dual(pdhg_ctx* ctx, double sigma, int rho_alp_iters, int sub, double* sums) {
+  if (!sums) return fail(PDHG_ERR_ARG, "null sums");
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_dual((float)sigma, rho_alp_iters, sub, sums); });
+}
+int pdhg_slab_dual_finalize(pdhg_ctx* ctx, double eps, int sub, const double* sums) {
+  if (!sums) return fail(PDHG_ERR_ARG, "null sums");
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_dual_finalize(eps, sub, sums); });
+}
+int pdhg_slab_outer(pdhg_ctx* ctx, int rho_alp_iters, double* sums) {
+  if (!sums) return fail(PDHG_ERR_ARG, "null sums");
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_outer(rho_alp_iters, sums); });
+}
+int pdhg_slab_outer_finalize(pdhg_ctx* ctx, double eps, int rho_alp_iters, const double* sums) {
+  if (!sums) return fail(PDHG_ERR_ARG, "null sums");
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_outer_finalize(eps, rho_alp_iters, sums); });
+}
+int pdhg_slab_plane_out(pdhg_ctx* ctx, int which, void* dst) {
+  if (!dst) return fail(PDHG_ERR_ARG, "null plane");
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_plane_out(which, dst); });
+}
+int pdhg_slab_plane_in(pdhg_ctx* ctx, int which, const void* src) {
+  if (!src) return fail(PDHG_ERR_ARG, "null plane");
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_plane_in(which, src); });
+}
+int pdhg_slab_status(pdhg_ctx* ctx, pdhg_stats* st) {
+  if (!st) return fail(PDHG_ERR_ARG, "null stats");
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_status(st); });
+}
+int pdhg_slab_plane_size(pdhg_ctx* ctx, unsigned long long* spatial, unsigned long long* spectral) {
+  if (!spatial || !spectral) return fail(PDHG_ERR_ARG, "null argument");
+  return slab_dispatch(ctx, [&](auto& im) {
+    *spatial = im.plane();
+    *spectral = im.Mspec;
+    return (int)PDHG_OK;
   });
 }
 

@@ -25,6 +25,11 @@ EXPORTS = (
     "pdhg_set_state", "pdhg_get_state", "pdhg_get_phi_bar", "pdhg_set_phi_bar", "pdhg_init_state",
     "pdhg_update_primal", "pdhg_update_dual", "pdhg_errors", "pdhg_inner_error", "pdhg_iterate", "pdhg_set_stop_rules", "pdhg_synchronize",
     "pdhg_device_bytes", "pdhg_profile_enable", "pdhg_profile_query", "pdhg_algorithmic_bytes",
+    # t-slab decomposition (multi-GPU)
+    "pdhg_create_slab", "pdhg_set_stream", "pdhg_slab_plane_size", "pdhg_slab_begin", "pdhg_slab_carry_gain",
+    "pdhg_slab_forward", "pdhg_slab_fixup", "pdhg_slab_backward", "pdhg_slab_primal_finalize", "pdhg_slab_dual",
+    "pdhg_slab_dual_finalize", "pdhg_slab_outer", "pdhg_slab_outer_finalize", "pdhg_slab_plane_out",
+    "pdhg_slab_plane_in", "pdhg_slab_status",
 )
 
 
@@ -69,6 +74,13 @@ def load():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError("libpdhg.so not built at {} — run __graft_entry__.build()".format(LIB_PATH))
+    # PyTorch-ROCm ships its own HIP runtime; if libpdhg.so (built against /opt/rocm) initialises HIP
+    # first, torch later reports "No HIP GPUs are available".  Load torch's runtime first whenever
+    # torch is installed (the multi-GPU driver and the bench use it for RCCL and streams).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(LIB_PATH)
     P = ctypes.c_void_p
     dp = ctypes.POINTER(ctypes.c_double)
@@ -96,6 +108,24 @@ def load():
         "pdhg_profile_enable": ([P, ctypes.c_int], ctypes.c_int),
         "pdhg_profile_query": ([P, ctypes.c_char_p, dp, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
         "pdhg_algorithmic_bytes": ([P, ctypes.c_int, ctypes.c_char_p, dp], ctypes.c_int),
+        "pdhg_create_slab": ([ctypes.POINTER(pdhg_problem), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                              ctypes.POINTER(P)], ctypes.c_int),
+        "pdhg_set_stream": ([P, P], ctypes.c_int),
+        "pdhg_slab_plane_size": ([P, ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_ulonglong)],
+                                 ctypes.c_int),
+        "pdhg_slab_begin": ([P], ctypes.c_int),
+        "pdhg_slab_carry_gain": ([P, P], ctypes.c_int),
+        "pdhg_slab_forward": ([P, ctypes.c_double], ctypes.c_int),
+        "pdhg_slab_fixup": ([P, P, P, ctypes.c_int], ctypes.c_int),
+        "pdhg_slab_backward": ([P, ctypes.c_double, P, P, ctypes.c_int, ctypes.c_int, P], ctypes.c_int),
+        "pdhg_slab_primal_finalize": ([P, P], ctypes.c_int),
+        "pdhg_slab_dual": ([P, ctypes.c_double, ctypes.c_int, ctypes.c_int, P], ctypes.c_int),
+        "pdhg_slab_dual_finalize": ([P, ctypes.c_double, ctypes.c_int, P], ctypes.c_int),
+        "pdhg_slab_outer": ([P, ctypes.c_int, P], ctypes.c_int),
+        "pdhg_slab_outer_finalize": ([P, ctypes.c_double, ctypes.c_int, P], ctypes.c_int),
+        "pdhg_slab_plane_out": ([P, ctypes.c_int, P], ctypes.c_int),
+        "pdhg_slab_plane_in": ([P, ctypes.c_int, P], ctypes.c_int),
+        "pdhg_slab_status": ([P, ctypes.POINTER(pdhg_stats)], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

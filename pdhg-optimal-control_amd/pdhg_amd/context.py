@@ -41,9 +41,12 @@ class PDHGContext:
         prob.ys = N.dptr(self._ys) if self._ys is not None else None
         self.rho_alp_iters = int(rho_alp_iters)
         self._prob = prob
+        self._h = self._create(prob, int(device))
+
+    def _create(self, prob, device):
         h = ctypes.c_void_p()
-        N.check(self._lib.pdhg_create(ctypes.byref(prob), int(device), ctypes.byref(h)))
-        self._h = h
+        N.check(self._lib.pdhg_create(ctypes.byref(prob), device, ctypes.byref(h)))
+        return h
 
     # ---- shapes ----
     @property

@@ -1,0 +1,294 @@
+"""t-slab decomposition of one PDHG window over P GPUs.
+
+The reference runs one window on one device (README.md:6; utils_pdhg_solver.py:51-88).  Here the T
+unknown time rows of a window are split into P contiguous slabs, one SlabContext (one GPU, one
+process) each; whole x-y planes stay local, so every FFT stays local.  Per outer iteration a slab
+exchanges, over RCCL on xGMI:
+
+* halos, point to point: rho row j1 from the next slab (the continuity residual's rho_{j+1},
+  update_fns_in_pdhg.py:83-96) and phi_bar row j0 from the previous slab (the dual's phi_bar_j,
+  :150-165), one plane each;
+* the distributed t-solve of the H1 preconditioner (utils_precond.py:142-178): two allgathers of one
+  spectral plane per slab (the zero-carry forward outputs D, then the X0 values), each slab folding
+  the upstream / downstream carries itself (oracle/slab_oracle.py restates the algebra);
+* allreduces of the 16-double sum vectors behind every stop test (the err of
+  update_dual_alternative, err1/err2 of utils_pdhg_solver.py:58-68), so every slab takes the same
+  control decisions on its device.
+
+Communicators: DistComm (torch.distributed, one slab per rank: "nccl" = RCCL on the GPUs, "gloo" on
+CPU tensors) and LocalComm (P slabs in one process on one device -- the single-GPU rehearsal and the
+parity tests; its collectives are copies).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+from .context import PDHGContext
+
+RHO_ROW0, PHIBAR_LAST, CARRY_D, CARRY_X0 = 0, 1, 2, 3    # pdhg_slab_plane_out
+RHO_HALO, PHIBAR_ROW0 = 0, 1                             # pdhg_slab_plane_in
+
+
+def slab_bounds(T, P):
+    """Contiguous near-equal row ranges [(j0, j1)] of T rows over P slabs (the first T % P get one more)."""
+    if P < 1 or P > T:
+        raise ValueError("need 1 <= P <= T (P={}, T={})".format(P, T))
+    base, extra = divmod(T, P)
+    out, j = [], 0
+    for q in range(P):
+        n = base + (1 if q < extra else 0)
+        out.append((j, j + n))
+        j += n
+    return out
+
+
+class SlabContext(PDHGContext):
+    """The slab [j0, j1) of a window of T_total rows (fp32, 2-D).  Arrays at this boundary are the
+    slab's rows: phi [T+1, nx, ny] (row 0 = global phi row j0), rho / alp [T, nx, ny(, n_ctrl)]."""
+
+    def __init__(self, rank, nranks, T_total, egno, nx, ny, dx, dy, dt, xs, ys, device=0, **kw):
+        self.rank, self.nranks, self.T_total = int(rank), int(nranks), int(T_total)
+        self.j0, self.j1 = slab_bounds(self.T_total, self.nranks)[self.rank]
+        kw.setdefault("precision", "fp32")
+        super().__init__(egno, 2, nx, ny, self.j1 - self.j0, dx, dy, dt, xs, ys, device=device, **kw)
+
+    def _create(self, prob, device):
+        h = ctypes.c_void_p()
+        N.check(self._lib.pdhg_create_slab(ctypes.byref(prob), self.j0, self.T_total, device, ctypes.byref(h)))
+        return h
+
+    @property
+    def last(self):
+        return self.rank == self.nranks - 1
+
+    def plane_sizes(self):
+        sp, spec = ctypes.c_ulonglong(), ctypes.c_ulonglong()
+        N.check(self._lib.pdhg_slab_plane_size(self._h, ctypes.byref(sp), ctypes.byref(spec)))
+        return sp.value, spec.value
+
+    # thin wrappers; tensor arguments are device tensors (float32 planes, float64[16] sums)
+    def set_stream(self, stream_handle):
+        N.check(self._lib.pdhg_set_stream(self._h, ctypes.c_void_p(stream_handle)))
+
+    def begin(self):
+        N.check(self._lib.pdhg_slab_begin(self._h))
+
+    def carry_gain(self, G):
+        N.check(self._lib.pdhg_slab_carry_gain(self._h, _ptr(G)))
+
+    def forward(self, tau):
+        N.check(self._lib.pdhg_slab_forward(self._h, float(tau)))
+
+    def fixup(self, allD, allG):
+        N.check(self._lib.pdhg_slab_fixup(self._h, _ptr(allD), _ptr(allG), self.rank))
+
+    def backward(self, tau, allX0, allG, sums):
+        N.check(self._lib.pdhg_slab_backward(self._h, float(tau), _ptr(allX0), _ptr(allG), self.rank, self.nranks,
+                                             _ptr(sums)))
+
+    def primal_finalize(self, sums):
+        N.check(self._lib.pdhg_slab_primal_finalize(self._h, _ptr(sums)))
+
+    def dual(self, sigma, k, sub, sums):
+        N.check(self._lib.pdhg_slab_dual(self._h, float(sigma), int(k), int(sub), _ptr(sums)))
+
+    def dual_finalize(self, eps, sub, sums):
+        N.check(self._lib.pdhg_slab_dual_finalize(self._h, float(eps), int(sub), _ptr(sums)))
+
+    def outer(self, k, sums):
+        N.check(self._lib.pdhg_slab_outer(self._h, int(k), _ptr(sums)))
+
+    def outer_finalize(self, eps, k, sums):
+        N.check(self._lib.pdhg_slab_outer_finalize(self._h, float(eps), int(k), _ptr(sums)))
+
+    def plane_out(self, which, dst):
+        N.check(self._lib.pdhg_slab_plane_out(self._h, int(which), _ptr(dst)))
+
+    def plane_in(self, which, src):
+        N.check(self._lib.pdhg_slab_plane_in(self._h, int(which), _ptr(src)))
+
+    def status(self):
+        st = N.pdhg_stats()
+        N.check(self._lib.pdhg_slab_status(self._h, ctypes.byref(st)))
+        return {"iters": st.iters_run, "status": st.status, "err1": st.err1, "err2": st.err2,
+                "inner_last": st.inner_last, "inner_total": st.inner_total, "nan_seen": st.nan_seen}
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+# ---------------------------------------------------------------------------------------------
+# communicators: lists hold one entry per slab living in this process
+# ---------------------------------------------------------------------------------------------
+class LocalComm:
+    """P slabs in one process on one device: every collective is a device copy."""
+
+    def __init__(self, nranks):
+        self.nranks = nranks
+        self.ranks = list(range(nranks))
+
+    def allgather(self, planes):
+        import torch
+        out = torch.stack(planes)
+        return [out] * len(planes)
+
+    def allreduce(self, vecs):
+        tot = vecs[0].clone()
+        for v in vecs[1:]:
+            tot += v
+        for v in vecs:
+            v.copy_(tot)
+
+    def shift_down(self, send, recv):     # slab r -> slab r+1
+        for r in range(1, self.nranks):
+            recv[r].copy_(send[r - 1])
+
+    def shift_up(self, send, recv):       # slab r -> slab r-1
+        for r in range(self.nranks - 1):
+            recv[r].copy_(send[r + 1])
+
+
+class DistComm:
+    """One slab per rank over torch.distributed (backend "nccl" = RCCL on ROCm, or "gloo")."""
+
+    def __init__(self):
+        import torch.distributed as dist
+        self.dist = dist
+        self.rank = dist.get_rank()
+        self.nranks = dist.get_world_size()
+        self.ranks = [self.rank]
+        self.gloo = dist.get_backend() == "gloo"
+
+    def allgather(self, planes):
+        import torch
+        (x,) = planes
+        if self.gloo:
+            parts = [torch.empty_like(x) for _ in range(self.nranks)]
+            self.dist.all_gather(parts, x)
+            return [torch.stack(parts)]
+        out = torch.empty((self.nranks,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+        self.dist.all_gather_into_tensor(out, x)
+        return [out]
+
+    def allreduce(self, vecs):
+        self.dist.all_reduce(vecs[0])
+
+    def _shift(self, send, recv, step):
+        dst, src = self.rank + step, self.rank - step
+        ops = []
+        if 0 <= dst < self.nranks:
+            ops.append(self.dist.P2POp(self.dist.isend, send[0], dst))
+        if 0 <= src < self.nranks:
+            ops.append(self.dist.P2POp(self.dist.irecv, recv[0], src))
+        if ops:
+            for w in self.dist.batch_isend_irecv(ops):
+                w.wait()
+
+    def shift_down(self, send, recv):
+        self._shift(send, recv, 1)
+
+    def shift_up(self, send, recv):
+        self._shift(send, recv, -1)
+
+
+# ---------------------------------------------------------------------------------------------
+# the iteration
+# ---------------------------------------------------------------------------------------------
+class SlabRunner:
+    """Drives the slabs of this process through outer iterations (pdhg_iterate's loop, split at
+    every point where slabs exchange data)."""
+
+    def __init__(self, slabs, comm):
+        import torch
+        self.torch = torch
+        self.slabs, self.comm = list(slabs), comm
+        dev = torch.device("cuda", torch.cuda.current_device())
+        sp, spec = self.slabs[0].plane_sizes()
+        f32, f64 = torch.float32, torch.float64
+        self.b = []
+        handle = torch.cuda.current_stream().cuda_stream
+        for s in self.slabs:
+            s.set_stream(handle)
+            self.b.append({k: torch.zeros(n, dtype=f32, device=dev) for k, n in
+                           (("rho_send", sp), ("rho_recv", sp), ("pb_send", sp), ("pb_recv", sp),
+                            ("D", spec), ("X0", spec), ("G", spec))})
+            self.b[-1]["sums"] = torch.zeros(16, dtype=f64, device=dev)
+        for s, b in zip(self.slabs, self.b):
+            s.carry_gain(b["G"])
+        self.allG = comm.allgather([b["G"] for b in self.b])   # iteration-invariant
+
+    def _each(self, name, *args):
+        for s in self.slabs:
+            getattr(s, name)(*args)
+
+    def step(self, tau, sigma, eps, k):
+        S, B, C = self.slabs, self.b, self.comm
+        # halo: rho row 0 of slab r+1 -> slab r (the residual's rho_{j+1} on its last row)
+        for s, b in zip(S, B):
+            s.plane_out(RHO_ROW0, b["rho_send"])
+        C.shift_up([b["rho_send"] for b in B], [b["rho_recv"] for b in B])
+        for s, b in zip(S, B):
+            if not s.last:
+                s.plane_in(RHO_HALO, b["rho_recv"])
+        # primal: forward sweeps, carry scans, backward sweeps + update
+        self._each("forward", tau)
+        for s, b in zip(S, B):
+            s.plane_out(CARRY_D, b["D"])
+        allD = C.allgather([b["D"] for b in B])
+        for i, s in enumerate(S):
+            s.fixup(allD[i], self.allG[i])
+            s.plane_out(CARRY_X0, B[i]["X0"])
+        allX0 = C.allgather([b["X0"] for b in B])
+        for i, s in enumerate(S):
+            s.backward(tau, allX0[i], self.allG[i], B[i]["sums"])
+        C.allreduce([b["sums"] for b in B])
+        for s, b in zip(S, B):
+            s.primal_finalize(b["sums"])
+        # halo: phi_bar row T of slab r -> phi_bar row 0 of slab r+1 (the dual's phi_bar_j)
+        for s, b in zip(S, B):
+            s.plane_out(PHIBAR_LAST, b["pb_send"])
+        C.shift_down([b["pb_send"] for b in B], [b["pb_recv"] for b in B])
+        for s, b in zip(S, B):
+            if s.rank > 0:
+                s.plane_in(PHIBAR_ROW0, b["pb_recv"])
+        # dual sub-iterations (device-side early exit once the global inner error is below eps)
+        for sub in range(k):
+            for s, b in zip(S, B):
+                s.dual(sigma, k, sub, b["sums"])
+            C.allreduce([b["sums"] for b in B])
+            for s, b in zip(S, B):
+                s.dual_finalize(eps, sub, b["sums"])
+        for s, b in zip(S, B):
+            s.outer(k, b["sums"])
+        if k > 1:
+            C.allreduce([b["sums"] for b in B])
+        for s, b in zip(S, B):
+            s.outer_finalize(eps, k, b["sums"])
+
+    def iterate(self, n, tau, sigma, eps, k, check_every=8):
+        """Up to n outer iterations; stops when the device control block says done (checked every
+        check_every iterations, like pdhg_iterate).  Returns the first slab's status dict."""
+        self._each("begin")
+        for it in range(n):
+            self.step(tau, sigma, eps, k)
+            if (it + 1) % check_every == 0 and it + 1 < n and self.slabs[0].status()["status"]:
+                break
+        return self.slabs[0].status()
+
+
+def split_state(phi, rho, alp, bounds):
+    """Slice a window's state (reference layouts) into per-slab states."""
+    out = []
+    for (j0, j1) in bounds:
+        out.append((phi[j0:j1 + 1], rho[j0:j1], tuple(a[j0:j1] for a in alp)))
+    return out
+
+
+def join_state(parts):
+    """Inverse of split_state: phi rows j0..j1 of every slab (row 0 of slab r > 0 is the halo)."""
+    phi = np.concatenate([parts[0][0]] + [p[0][1:] for p in parts[1:]], axis=0)
+    rho = np.concatenate([p[1] for p in parts], axis=0)
+    alp = tuple(np.concatenate([p[2][a] for p in parts], axis=0) for a in range(len(parts[0][2])))
+    return phi, rho, alp

@@ -1,0 +1,65 @@
+"""t-slab decomposition on the GPU: P slab contexts on one device, exchanging planes
+through LocalComm, must reproduce the single-context iteration (pdhg_iterate) of the same window --
+same state after n outer iterations within fp32 rounding, same error history and stop decisions.
+The single-context path is itself pinned to the oracle by test_gpu_parity.py."""
+import numpy as np
+import pytest
+
+from _problems import make_problem, rel
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # (egno, nx, ny, T, P, k)   nx = 512: k_precond_xt_fast_2d;  nx = 4096: k_precond_xt_ws_2d
+    (1, 512, 256, 6, 2, 1),
+    (2, 512, 256, 7, 3, 1),
+    (1, 512, 256, 5, 5, 3),
+    (2, 4096, 256, 6, 2, 1),
+    (1, 4096, 256, 4, 3, 2),
+]
+
+
+def _slabs(P, nranks, k):
+    from pdhg_amd.slab import SlabContext
+    return [SlabContext(r, nranks, P["T"], P["egno"], P["nx"], P["ny"], P["dx"], P["dy"], P["dt"], P["xs"], P["ys"],
+                        epsl=P["epsl"], rho_alp_iters=k) for r in range(nranks)]
+
+
+@pytest.mark.parametrize("egno,nx,ny,T,nr,k", CASES, ids=[f"e{c[0]}_{c[1]}x{c[2]}_T{c[3]}_P{c[4]}_k{c[5]}"
+                                                         for c in CASES])
+def test_slabs_match_single_context(native, egno, nx, ny, T, nr, k):
+    import torch
+    from pdhg_amd.context import PDHGContext
+    from pdhg_amd.slab import LocalComm, SlabRunner, join_state, slab_bounds, split_state
+    P = make_problem(egno, 2, nx, ny, T, 0.0)
+    tau, sigma, n = 0.1 / 1.5, 0.1 * 1.5, 6
+    ref = PDHGContext(egno, 2, nx, ny, T, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"], epsl=0.0,
+                      precision="fp32", rho_alp_iters=k)
+    ref.set_state(P["phi"], P["rho"], P["alp"])
+    st_ref = ref.iterate(n, tau, sigma, -1.0, k)
+    phi_r, rho_r, alp_r = ref.get_state()
+
+    slabs = _slabs(P, nr, k)
+    for s, part in zip(slabs, split_state(P["phi"], P["rho"], P["alp"], slab_bounds(T, nr))):
+        s.set_state(*part)
+    runner = SlabRunner(slabs, LocalComm(nr))
+    st = runner.iterate(n, tau, sigma, -1.0, k)
+    torch.cuda.synchronize()
+    phi_s, rho_s, alp_s = join_state([s.get_state() for s in slabs])
+    assert st["iters"] == st_ref["iters_run"] == n
+    assert rel(phi_s, phi_r) < 2e-5
+    assert rel(rho_s, rho_r) < 2e-4
+    assert rel(np.stack(alp_s), np.stack(alp_r)) < 2e-4
+    assert abs(st["err1"] - st_ref["err1"]) <= 1e-3 * st_ref["err1"]
+    assert abs(st["err2"] - st_ref["err2"]) <= 1e-3 * st_ref["err2"]
+    for s in slabs:
+        s.close()
+    ref.close()
+
+
+def test_slab_rejects_unsupported(native):
+    from pdhg_amd import _native as N
+    from pdhg_amd.slab import SlabContext
+    P = make_problem(1, 2, 48, 40, 4, 0.0)
+    with pytest.raises(N.PDHGError):      # nx = 48: no fast x-transform kernel
+        SlabContext(0, 2, 4, 1, 48, 40, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"])
