@@ -1,0 +1,73 @@
+"""The N > 1 path on CPU: two processes over torch.distributed "gloo" (world size 2).
+
+DistComm (pdhg_amd/slab.py) is the communicator the multi-GPU run uses over RCCL; here it moves CPU
+tensors.  Checked: the halo shifts, allgather and allreduce semantics, and the distributed t-solve
+(oracle/slab_oracle.py algebra) driven through those collectives reproduces the monolithic solve."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, paths):
+    import sys
+    sys.path[:0] = paths
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{}".format(port), rank=rank, world_size=world)
+    try:
+        from pdhg_amd.slab import DistComm, slab_bounds
+        import slab_oracle as S
+        comm = DistComm()
+        assert comm.rank == rank and comm.nranks == world
+        # --- halo shifts: rank r sends r+1 (down) / r-1 (up)
+        send = [torch.full((5,), float(rank + 1))]
+        recv = [torch.zeros(5)]
+        comm.shift_down(send, recv)
+        assert float(recv[0][0]) == (rank if rank > 0 else 0.0)
+        recv = [torch.zeros(5)]
+        comm.shift_up(send, recv)
+        assert float(recv[0][0]) == (rank + 2 if rank < world - 1 else 0.0)
+        # --- allgather / allreduce
+        (g,) = comm.allgather([torch.arange(3, dtype=torch.float32) + 10 * rank])
+        assert g.shape == (world, 3) and all(float(g[q, 0]) == 10 * q for q in range(world))
+        v = [torch.full((16,), float(rank + 1), dtype=torch.float64)]
+        comm.allreduce(v)
+        assert float(v[0][3]) == sum(range(1, world + 1))
+        # --- distributed Thomas over the real collectives
+        rng = np.random.default_rng(3)           # same data on every rank
+        T, M = 11, 9
+        ae = 1.0 / 0.04 ** 2
+        diag = np.tile(1.0 + rng.uniform(0, 3e3, M) + 2 * ae, (T, 1))
+        diag[-1] -= ae
+        r = rng.standard_normal((T, M))
+        ref = S.monolithic_tridiag(diag, r, ae)
+        j0, j1 = slab_bounds(T, world)[rank]
+        gp = S.pivots(diag, ae)
+        b0, D, G = S.local_forward(r, gp, ae, j0, j1)
+        (allD,) = comm.allgather([torch.from_numpy(D)])
+        (allG,) = comm.allgather([torch.from_numpy(G)])
+        c = S.carry_in(list(allD.numpy()), list(allG.numpy()), rank)
+        b, X0 = S.fixup(b0, gp, j0, c)
+        (allX0,) = comm.allgather([torch.from_numpy(X0)])
+        y = S.right_carry(list(allX0.numpy()), list(allG.numpy()), rank)
+        x = S.local_backward(b, gp, j0, y)
+        assert np.allclose(x, ref[j0:j1], rtol=1e-11, atol=1e-12 * np.abs(ref).max())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_slab_exchanges():
+    paths = [os.path.join(HERE, "..", "pdhg-optimal-control_amd"), os.path.join(HERE, "..", "oracle")]
+    mp.spawn(_worker, args=(2, _free_port(), [os.path.abspath(p) for p in paths]), nprocs=2, join=True)
