@@ -8,9 +8,10 @@ utils_pdhg_solver.py:123-137).  One "step" = one outer PDHG iteration
 (utils_pdhg_solver.py:51-88): primal (residual + H1 preconditioner + update), extrapolation,
 dual (alpha/rho prox), err1/err2 and the device-side stop tests.
 
-N > 1 (launched by torch.distributed.run): one process per GPU.  The t-slab sharding of one
-window is not built yet, so every rank runs an independent replica of the same window
-("replicas", weak scaling); value = sum of the ranks' iterations / max-over-ranks time.
+N > 1 (launched by torch.distributed.run): one process per GPU, the SAME window split into N t-slabs
+of T/N rows (pdhg_amd/slab.py): rho / phi_bar halos point to point, the distributed
+t-solve's two plane allgathers and the stop-test allreduces over RCCL.  Total work is fixed, so the
+scaling is "strong"; value = iterations of the window / max-over-ranks time.
 """
 import argparse
 import json
@@ -156,8 +157,11 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as tdist
-        torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl")
+        # device = local rank (modulo the visible GPUs: PDHG_DIST_BACKEND=gloo rehearses the multi-rank
+        # path with several ranks on one GPU; the driver's runs use one GPU per rank over RCCL)
+        dev = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+        tdist.init_process_group(os.environ.get("PDHG_DIST_BACKEND", "nccl"))
         dist = tdist
 
     pmc, pmc_err = None, "disabled"
@@ -171,8 +175,14 @@ def main():
     k = args.rho_alp_iters
     xs, ys = grid(ndim, nx, ny)
     dt = 1.0 / (nt - 1)
-    ctx = PDHGContext(egno, ndim, nx, ny, T, 2.0 / nx, 2.0 / ny if ndim == 2 else 0.0, dt, xs, ys, epsl=epsl,
-                      precision="fp32", rho_alp_iters=k, device=local_rank if world > 1 else 0)
+    runner = None
+    if world > 1:
+        from pdhg_amd.slab import DistComm, SlabContext, SlabRunner
+        ctx = SlabContext(rank, world, T, egno, nx, ny, 2.0 / nx, 2.0 / ny, dt, xs, ys, epsl=epsl,
+                          rho_alp_iters=k, device=torch.cuda.current_device())
+    else:
+        ctx = PDHGContext(egno, ndim, nx, ny, T, 2.0 / nx, 2.0 / ny if ndim == 2 else 0.0, dt, xs, ys, epsl=epsl,
+                          precision="fp32", rho_alp_iters=k, device=0)
     if ndim == 1:
         g = np.sin(np.pi * xs)
     else:
@@ -185,9 +195,26 @@ def main():
     tau, sigma = 0.1 / 1.5, 0.1 * 1.5
     eps = 1e-6
 
+    if world > 1:
+        import torch
+        runner = SlabRunner([ctx], DistComm())
+
+        def run(n):
+            s = runner.iterate(n, tau, sigma, eps, k)
+            return {"iters_run": s["iters"], "status": s["status"], "nan_seen": s["nan_seen"]}
+
+        def sync():
+            torch.cuda.synchronize()
+    else:
+        def run(n):
+            return ctx.iterate(n, tau, sigma, eps, k)
+
+        def sync():
+            ctx.synchronize()
+
     if args.warmup > 0:
-        ctx.iterate(args.warmup, tau, sigma, eps, k)
-    ctx.synchronize()
+        run(args.warmup)
+    sync()
 
     def barrier():
         if dist is not None:
@@ -195,10 +222,10 @@ def main():
 
     ctx.profile_enable(True)
     barrier()
-    ctx.synchronize()
+    sync()
     t0 = time.perf_counter()
-    st = ctx.iterate(args.steps, tau, sigma, eps, k)
-    ctx.synchronize()
+    st = run(args.steps)
+    sync()
     barrier()
     el = time.perf_counter() - t0
     iters = st["iters_run"]
@@ -207,8 +234,7 @@ def main():
         t = torch.tensor([el, float(iters)], dtype=torch.float64, device="cuda")
         tmax = t.clone()
         dist.all_reduce(tmax[0:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:2], op=dist.ReduceOp.SUM)
-        el_max, iters_total = float(tmax[0]), int(t[1])
+        el_max, iters_total = float(tmax[0]), iters          # one window: every rank ran the same iterations
     else:
         el_max, iters_total = el, iters
 
@@ -218,11 +244,14 @@ def main():
         ms, n = ctx.profile_query(cls)
         if n:
             kern[cls] = {"avg_ms": ms / n, "launches": n, "bytes_per_launch": ctx.algorithmic_bytes(k, cls)}
+    if world > 1 and "precond" in kern:   # t-slab: forward and backward sweeps are separate launches
+        kern["precond"]["launches"] //= 2
+        kern["precond"]["avg_ms"] *= 2
     ctx.profile_enable(False)
     dom = max(kern, key=lambda c: kern[c]["avg_ms"] * kern[c]["launches"])
     d = kern[dom]
     achieved = d["bytes_per_launch"] / (d["avg_ms"] * 1e-3) / 1e9
-    it_bytes = ctx.algorithmic_bytes(k, "iteration")
+    it_bytes = ctx.algorithmic_bytes(k, "iteration") * world   # whole window (slabs are equal-ish)
     ms_per_step = el_max / max(iters, 1) * 1e3
 
     if rank != 0:
@@ -238,13 +267,14 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if world > 1 else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (reference initial state phi=g, rho=70, alp=0)",
         "config": {"workload": "egno{} ndim{} epsl{} nx={} ny={} nt={}: one PDHG window of T={} rows, "
                                "rho_alp_iters={}".format(egno, ndim, epsl, nx, ny, nt, T, k),
-                   "parallelism": "replicas" if world > 1 else "single GPU",
+                   "parallelism": "t-slab x{} (RCCL halos + carry allgathers)".format(world) if world > 1
+                   else "single GPU",
                    "iters_executed": iters, "stop_status": st["status"], "state_nonfinite": bool(st["nan_seen"])},
         "hbm_gbps_iteration": it_bytes / (ms_per_step * 1e-3) / 1e9,
         "iteration_bytes": it_bytes,

@@ -161,30 +161,43 @@ class DistComm:
         self.ranks = [self.rank]
         self.gloo = dist.get_backend() == "gloo"
 
+    # gloo moves host memory: device tensors are staged through the host (functional rehearsal of the
+    # multi-rank path; the GPU runs use RCCL on device buffers directly)
     def allgather(self, planes):
         import torch
         (x,) = planes
         if self.gloo:
-            parts = [torch.empty_like(x) for _ in range(self.nranks)]
-            self.dist.all_gather(parts, x)
-            return [torch.stack(parts)]
+            h = x.cpu()
+            parts = [torch.empty_like(h) for _ in range(self.nranks)]
+            self.dist.all_gather(parts, h)
+            return [torch.stack(parts).to(x.device)]
         out = torch.empty((self.nranks,) + tuple(x.shape), dtype=x.dtype, device=x.device)
         self.dist.all_gather_into_tensor(out, x)
         return [out]
 
     def allreduce(self, vecs):
-        self.dist.all_reduce(vecs[0])
+        if self.gloo and vecs[0].is_cuda:
+            h = vecs[0].cpu()
+            self.dist.all_reduce(h)
+            vecs[0].copy_(h)
+        else:
+            self.dist.all_reduce(vecs[0])
 
     def _shift(self, send, recv, step):
         dst, src = self.rank + step, self.rank - step
+        stage = self.gloo and send[0].is_cuda
+        s_buf = send[0].cpu() if stage else send[0]
+        r_buf = recv[0].cpu() if stage else recv[0]
         ops = []
         if 0 <= dst < self.nranks:
-            ops.append(self.dist.P2POp(self.dist.isend, send[0], dst))
+            ops.append(self.dist.P2POp(self.dist.isend, s_buf, dst))
         if 0 <= src < self.nranks:
-            ops.append(self.dist.P2POp(self.dist.irecv, recv[0], src))
+            ops.append(self.dist.P2POp(self.dist.irecv, r_buf, src))
         if ops:
             for w in self.dist.batch_isend_irecv(ops):
                 w.wait()
+        if stage and 0 <= src < self.nranks:
+            recv[0].copy_(r_buf)
 
     def shift_down(self, send, recv):
         self._shift(send, recv, 1)
