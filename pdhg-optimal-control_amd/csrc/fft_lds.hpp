@@ -182,7 +182,10 @@ __device__ void stockham_pass_generic(const C* __restrict__ src, C* __restrict__
 // a; b is scratch of the same size.  All threads of the block take part; the
 // call starts and ends with a barrier-complete state.  Returns the buffer that
 // holds the result (natural order).
-template <typename C>
+// GLB: a and b are global-memory scratch of this workgroup (lines longer than LDS holds); the
+// passes are then separated by full barriers (stores drained), which orders them within the
+// workgroup because all its waves share one CU's vector L1.
+template <typename C, bool GLB = false>
 __device__ C* lds_fft(C* a, C* b, int nl, const FFTPlan& pl, const C* __restrict__ tw) {
   int lnl = 0;
   while ((1 << lnl) < nl) ++lnl;
@@ -199,7 +202,10 @@ __device__ C* lds_fft(C* a, C* b, int nl, const FFTPlan& pl, const C* __restrict
       case 3: stockham_pass<C, 3>(src, dst, pl.n, nl, lnl, Ls, pl.pow2, tw); break;
       default: stockham_pass_generic<C>(src, dst, pl.n, nl, lnl, Ls, R, tw); break;
     }
-    lds_sync();
+    if constexpr (GLB)
+      __syncthreads();
+    else
+      lds_sync();
     C* t = src;
     src = dst;
     dst = t;
@@ -503,11 +509,28 @@ struct FFTRt {              // any n (mixed radix, runtime plan), nl interleaved
   int nl;
   template <typename C>
   __device__ __forceinline__ C* run(C* a, C* b, const C* __restrict__ tw) const { return lds_fft<C>(a, b, nl, pl, tw); }
+  template <typename C>
+  __device__ __forceinline__ C* buffer(C* lds, C*, int) const { return lds; }
   __device__ __forceinline__ int n() const { return pl.n; }
   __device__ __forceinline__ int lines() const { return nl; }
 };
+struct FFTGlb {             // any n, line buffers in global scratch (slot per workgroup): lines beyond LDS
+  FFTPlan pl;
+  int nl;
+  template <typename C>
+  __device__ __forceinline__ C* run(C* a, C* b, const C* __restrict__ tw) const {
+    return lds_fft<C, true>(a, b, nl, pl, tw);
+  }
+  template <typename C>
+  __device__ __forceinline__ C* buffer(C*, C* g, int slot) const { return g + (size_t)slot * 2 * pl.n * nl; }
+  __device__ __forceinline__ int n() const { return pl.n; }
+  __device__ __forceinline__ int lines() const { return nl; }
+};
+
 template <int N, int NL>
 struct FFTFx {              // compile-time power-of-two n, NL lines
+  template <typename C>
+  __device__ __forceinline__ C* buffer(C* lds, C*, int) const { return lds; }
   template <typename C>
   __device__ __forceinline__ C* run(C* a, C* b, const C* __restrict__ tw) const {
     return lds_fft_fixed<C, N, NL>(a, b, tw);

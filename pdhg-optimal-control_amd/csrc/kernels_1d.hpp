@@ -39,11 +39,11 @@ __device__ __forceinline__ R cont_residual_1d(const KP<R>& p, const R* __restric
 
 // grid: ceil(T/2) row pairs; block 256; LDS 2 * nx complex
 template <typename R, int EGNO, class F>
-__global__ void __launch_bounds__(256) k_res_fwdx_1d(KP<R> p, F plx, const cplx<R>* __restrict__ twx) {
+__global__ void __launch_bounds__(1024) k_res_fwdx_1d(KP<R> p, F plx, const cplx<R>* __restrict__ twx) {
   using C = cplx<R>;
   if (p.ctrl->done) return;
   extern __shared__ __align__(16) unsigned char smem_raw[];
-  C* A = reinterpret_cast<C*>(smem_raw);
+  C* A = plx.template buffer<C>(reinterpret_cast<C*>(smem_raw), reinterpret_cast<C*>(p.gscr), blockIdx.x);
   C* Bf = A + plx.n();
   const int cur = p.ctrl->cur;
   const R* rho = p.rho[cur];
@@ -121,11 +121,11 @@ __global__ void __launch_bounds__(256) k_thomas_1d(KP<R> p) {
 
 // grid: G workgroups striding over the ceil(T/2) row pairs; block 256; LDS 2 * nx complex
 template <typename R, class F>
-__global__ void __launch_bounds__(256) k_invx_update_1d(KP<R> p, F plx, const cplx<R>* __restrict__ twx) {
+__global__ void __launch_bounds__(1024) k_invx_update_1d(KP<R> p, F plx, const cplx<R>* __restrict__ twx) {
   using C = cplx<R>;
   if (p.ctrl->done) return;
   extern __shared__ __align__(16) unsigned char smem_raw[];
-  C* A = reinterpret_cast<C*>(smem_raw);
+  C* A = plx.template buffer<C>(reinterpret_cast<C*>(smem_raw), reinterpret_cast<C*>(p.gscr), blockIdx.x);
   C* Bf = A + plx.n();
   const int nx = p.nx;
   const R scale = p.tau * p.inv_n;

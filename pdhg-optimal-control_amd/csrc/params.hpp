@@ -40,6 +40,7 @@ struct KP {
   int xt_phase;            // x-transform/Thomas kernel: 0 both sweeps, 1 forward only, 2 backward only
   const R* rho_halo;       // rho row j0+T (first row of the next slab) [nx][ny]; null on the last slab
   const R* carry_y;        // backward right carry x_{j0+T} (spectral, work-row layout); null = zero
+  void* gscr;              // per-workgroup global FFT scratch (1-D lines beyond LDS), 2 lines per slot
 };
 
 // neighbour index along an axis of length n with boundary condition bc

@@ -104,6 +104,8 @@ struct Impl : ImplBase {
   size_t lds_res = 0, lds_xt = 0;
   // fast row kernels (fp32, power-of-two ny): RW rows per workgroup, NTf threads
   bool fast_rows = false;
+  bool glb_line = false;          // 1-D line FFTs over global scratch (nx beyond LDS)
+  int nt1d = 256;                 // 1-D residual / update block size (1024 on the global-scratch path)
   bool fast_xt = false;
   bool ws_xt = false;             // warp-specialised variant (k_precond_xt_ws_2d)            // fp32 power-of-two nx: k_precond_xt_fast_2d
   size_t lds_fast_xt = 0;
@@ -263,9 +265,13 @@ struct Impl : ImplBase {
       p.nb = 1;
       p.rows_per_wg = 2;
       lds_res = 2 * (size_t)nx * csz;
-      if (lds_res > kLdsBytes) return fail(PDHG_ERR_UNSUPPORTED, "nx=%d exceeds the LDS line transform (1-D)", nx);
       gx1 = (T + 1) / 2;
       gx4 = std::min(gx1, 2048);
+      if (lds_res > kLdsBytes) {   // lines beyond LDS (C1: nx = 65536): Stockham passes over global scratch
+        glb_line = true;
+        lds_res = 0;
+        nt1d = 1024;
+      }
       g4 = 1;
       gx5 = (nx + 255) / 256;
       g5 = std::max(1, std::min(T, 8192 / std::max(1, gx5)));
@@ -301,6 +307,11 @@ struct Impl : ImplBase {
     for (int a = na; a < 4; ++a) p.alp[0][a] = p.alp[1][a] = nullptr;
     if ((rc = alloc(&p.partials, partial_rows * kNumSums))) return rc;
     if ((rc = alloc(&p.ctrl, 1))) return rc;
+    if (glb_line) {   // 2 lines of nx complex per concurrent workgroup (gx1 >= gx4)
+      C* g = nullptr;
+      if ((rc = alloc(&g, (size_t)gx1 * 2 * nx))) return rc;
+      p.gscr = g;
+    }
     if (slab) {
       Mspec = (size_t)p.nb * nx * p.B;
       if ((rc = alloc(&halo_rho, npl))) return rc;
@@ -379,6 +390,7 @@ struct Impl : ImplBase {
   // runtime mixed-radix plan otherwise.
   template <typename Fn>
   int with_line_fft(const FFTPlan& pl, Fn&& fn) {
+    if (glb_line) return fn(FFTGlb{pl, 1});   // 1-D lines beyond LDS
     if constexpr (sizeof(R) == 4) {
       if (pl.pow2) {
         switch (pl.n) {
@@ -610,10 +622,10 @@ struct Impl : ImplBase {
           int r2;
           if (pb.egno == 1) {
             if ((r2 = ensure_lds(k_res_fwdx_1d<R, 1, F>, lds_res))) return r2;
-            hipLaunchKernelGGL((k_res_fwdx_1d<R, 1, F>), dim3(gx1), dim3(256), lds_res, stream, p, f, twx);
+            hipLaunchKernelGGL((k_res_fwdx_1d<R, 1, F>), dim3(gx1), dim3(nt1d), lds_res, stream, p, f, twx);
           } else {
             if ((r2 = ensure_lds(k_res_fwdx_1d<R, 2, F>, lds_res))) return r2;
-            hipLaunchKernelGGL((k_res_fwdx_1d<R, 2, F>), dim3(gx1), dim3(256), lds_res, stream, p, f, twx);
+            hipLaunchKernelGGL((k_res_fwdx_1d<R, 2, F>), dim3(gx1), dim3(nt1d), lds_res, stream, p, f, twx);
           }
           return (int)PDHG_OK;
         });
@@ -629,7 +641,7 @@ struct Impl : ImplBase {
           using F = decltype(f);
           int r2;
           if ((r2 = ensure_lds(k_invx_update_1d<R, F>, lds_res))) return r2;
-          hipLaunchKernelGGL((k_invx_update_1d<R, F>), dim3(gx4), dim3(256), lds_res, stream, p, f, twx);
+          hipLaunchKernelGGL((k_invx_update_1d<R, F>), dim3(gx4), dim3(nt1d), lds_res, stream, p, f, twx);
           return (int)PDHG_OK;
         });
         if (rc) return rc;

@@ -2,7 +2,8 @@
 
 Tolerances (stated per SURVEY.md Appendix B.8):
   * fp64 device path: relative L2 <= 1e-10 on every state array after 1 and 10 iterations
-    (same algorithm up to FFT/Hartley/closed-form-pivot roundoff);
+    (same algorithm up to FFT/Hartley/closed-form-pivot roundoff); x10 for lines of >= 16384 points
+    (C1's 65536: FFT roundoff grows with log n and the stencil's 1/dx^2 reaches 1e9);
   * fp32 device path from the reference's own initial state (phi = g, rho = c, alp = 0;
     utils_pdhg_solver.py:123-137): relative L2 of the primal update U = (phi' - phi)/tau <= 2e-6,
     of phi after 10 iterations <= 1e-5 (the north-star "phi within 1e-5 rel-L2"), rho <= 1e-5;
@@ -35,8 +36,15 @@ CASES = [
     (2, 2, 64, 48, 8, 0.1),
     (1, 2, 256, 256, 3, 0.0),   # fixed-size FFT paths (rows 256, x-slab 256 x 8 lines) in fp32
     (2, 2, 512, 256, 2, 0.0),   # fp32 fast row kernels (8-row groups, in-place 4-line FFT)
+    (1, 1, 16384, 1, 5, 0.0),   # 1-D lines beyond LDS: Stockham passes over global scratch
+    (2, 1, 65536, 1, 3, 0.0),   # C1's line length (BASELINE configs[1])
 ]
 IDS = ["e{}d{}_{}x{}_T{}_eps{}".format(*c) for c in CASES]
+
+
+def _big(P):
+    """fp64 tolerance factor for long lines (see the module docstring)."""
+    return 10.0 if max(P["nx"], P["ny"]) >= 16384 else 1.0
 
 
 def _oracle_primal(P, phi, rho, alp):
@@ -63,8 +71,8 @@ def test_primal(native, case, prec):
     U_o = (phi_o - P["phi"]) / TAU
     U_d = (phi_d - P["phi"]) / TAU
     if prec == "fp64":
-        assert rel(U_d, U_o) < 1e-10
-        assert rel(pbar_d, 2 * phi_o - P["phi"]) < 1e-12
+        assert rel(U_d, U_o) < 1e-10 * _big(P)
+        assert rel(pbar_d, 2 * phi_o - P["phi"]) < 1e-12 * _big(P)
     else:
         # U recovered from fp32 phi' carries phi's rounding / tau; phi' itself is the checked quantity
         assert rel(U_d, U_o) < 5e-4
@@ -139,7 +147,7 @@ def test_iterate_10(native, case, prec):
     assert st["iters_run"] == 10 and st["status"] == 0
     phi_d, rho_d, alp_d = ctx.get_state()
     if prec == "fp64":
-        assert rel(phi_d, phi_o) < 1e-11 and rel(rho_d, rho_o) < 1e-10
+        assert rel(phi_d, phi_o) < 1e-11 * _big(P) and rel(rho_d, rho_o) < 1e-10 * _big(P)
         assert abs(st["err1"] - e1_o) <= 1e-8 * e1_o and abs(st["err2"] - e2_o) <= 1e-8 * e2_o
     else:
         assert rel(phi_d, phi_o) < 1e-5

@@ -43,3 +43,19 @@ def test_h1_precond_2d_slabs_equals_oracle(P):
     ref = O.H1_precond_2d(src, fv, dt, (0, 0), C=1.0)
     out = S.h1_precond_2d_slabs(src, fv, dt, 1.0, P)
     assert np.allclose(out, ref, rtol=1e-10, atol=1e-12)
+
+
+def test_split_join_state_roundtrip():
+    import sys, os
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "pdhg-optimal-control_amd"))
+    from pdhg_amd.slab import join_state, slab_bounds, split_state
+    T = 7
+    phi = rng.standard_normal((T + 1, 4, 3))
+    rho = rng.standard_normal((T, 4, 3))
+    alp = tuple(rng.standard_normal((T, 4, 3, 2)) for _ in range(4))
+    for P in (1, 2, 3, 7):
+        parts = split_state(phi, rho, alp, slab_bounds(T, P))
+        assert [p[1].shape[0] for p in parts] == [j1 - j0 for j0, j1 in slab_bounds(T, P)]
+        phi2, rho2, alp2 = join_state(parts)
+        assert np.array_equal(phi2, phi) and np.array_equal(rho2, rho)
+        assert all(np.array_equal(a, b) for a, b in zip(alp2, alp))
