@@ -30,6 +30,7 @@ HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CONFIGS = {
     # name: (egno, ndim, epsl, nx, ny, nt)
     "c3": (2, 2, 0.1, 4096, 4096, 201),
+    "c4": (2, 2, 0.1, 8192, 8192, 401),   # 8-GPU point (t-slabs; >= 4 GPUs for memory)
     "c2": (1, 2, 0.0, 2048, 2048, 101),
     "c1": (1, 1, 0.0, 65536, 1, 401),
     "c0": (1, 1, 0.0, 160, 1, 41),

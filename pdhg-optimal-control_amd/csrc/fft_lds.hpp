@@ -401,7 +401,7 @@ __device__ __forceinline__ void lds_fft_inplace_tl(C* a, const C* twl) {
 
 // Fill the TwLds<N> table from the global twiddle table (W_N^m at tw[m]); caller syncs before use.
 template <typename C, int N>
-__device__ __forceinline__ void fill_twlds(C* twl, const C* __restrict__ tw) {
+__device__ __forceinline__ void fill_twlds(C* twl, const C* __restrict__ tw, int tw_stride = 1) {
   for (int i = threadIdx.x; i < TwLds<N>::SIZE; i += blockDim.x) {
     const int LS = i >= 816 ? 4096 : i >= 48 ? 256 : 16;
     const int e = i - twlds_off(LS);
@@ -409,7 +409,7 @@ __device__ __forceinline__ void fill_twlds(C* twl, const C* __restrict__ tw) {
     const int R = (N / LS >= 16) ? 16 : N / LS;
     const int tws = N / (LS * R);
     const int mult = (m == 0) ? 1 : (m == 1) ? 4 : 8;
-    twl[i] = tw[(mult * k * tws) & (N - 1)];
+    twl[i] = tw[(size_t)tw_stride * ((mult * k * tws) & (N - 1))];   // tw holds W_{N*tw_stride}
   }
 }
 
@@ -491,6 +491,21 @@ __device__ __forceinline__ void split_write(C* __restrict__ a, C (&v)[NV],
       for (int r = 0; r < R; ++r) d[(LS == 1) ? r : r * (LS + LS / 16)] = u[r];
     }
   }
+}
+
+// DHT of ONE real line of length 2M from the M-point complex FFT Z of z[m] = x[2m] + i x[2m+1]:
+// E = (Z_k + conj Z_{M-k})/2, O = (Z_k - conj Z_{M-k})/(2i), X_k = E + W^k O, X_{k+M} = E - W^k O
+// (W = e^{-2 pi i/(2M)}), H = Re X - Im X.  Returns H_k and H_{k+M}.  Z padded (pix).
+template <typename C, typename T>
+__device__ __forceinline__ void realsplit_padded(const C* Z, int M, int k, C w, T& h0, T& h1) {
+  const int km = (k == 0) ? 0 : M - k;
+  const C z = Z[pix(k)];
+  const C c = Z[pix(km)];
+  const T ex = (T)0.5 * (z.x + c.x), ey = (T)0.5 * (z.y - c.y);    // E
+  const T ox = (T)0.5 * (z.y + c.y), oy = (T)-0.5 * (z.x - c.x);   // O = (Z - conj C) / 2i
+  const T wox = w.x * ox - w.y * oy, woy = w.x * oy + w.y * ox;    // W O
+  h0 = (ex + wox) - (ey + woy);
+  h1 = (ex - wox) - (ey - woy);
 }
 
 // Hartley unpack from a padded line (see hartley_pair).

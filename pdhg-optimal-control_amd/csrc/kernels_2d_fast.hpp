@@ -530,7 +530,10 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
 // Thomas carries (registers, per item of 2 modes): forward dd = 2 delta, h = 1 - g, b';
 // backward theta, E, x (same arithmetic as k_precond_xt_fast_2d).
 // LDS: 2 padded FFT buffers NL*(N + N/16) complex + twiddle seeds (~76 KiB).  grid: nb; block 512.
-template <int N, int NL>
+// HR ("half real", nx = 2N): column blocks of ONE real column of 2N points, packed z[m] = x[2m] + i x[2m+1]
+// into the N-point FFT and split with realsplit_padded; item k carries modes kx = k and k + N.
+// + N-complex split-twiddle table (W_{2N}^k) in LDS.
+template <int N, int NL, bool HR = false>
 __global__ void __launch_bounds__(512) k_precond_xt_ws_2d(KP<float> p, const float2* __restrict__ twx) {
   using C = float2;
   constexpr int NTF = 256, NTT = 256;
@@ -549,7 +552,12 @@ __global__ void __launch_bounds__(512) k_precond_xt_ws_2d(KP<float> p, const flo
   C* buf0 = reinterpret_cast<C*>(smem_raw);
   C* buf1 = buf0 + NL * LINE;
   C* twl = buf1 + NL * LINE;
-  fill_twlds<C, N>(twl, twx);
+  C* rsw = twl + TwLds<N>::SIZE;                 // HR split twiddles W_{2N}^k, k < N
+  fill_twlds<C, N>(twl, twx, HR ? 2 : 1);        // HR: twx holds W_{2N}
+  if constexpr (HR) {
+    static_assert(NL == 1, "one real column per block");
+    for (int i = threadIdx.x; i < N; i += blockDim.x) rsw[i] = twx[i];
+  }
   const int T = p.T, tid = threadIdx.x;
   const bool fftg = tid < NTF;                 // wave-uniform role
   const int tt = fftg ? 0 : tid - NTF;         // Thomas-group thread
@@ -574,14 +582,22 @@ __global__ void __launch_bounds__(512) k_precond_xt_ws_2d(KP<float> p, const flo
 #pragma unroll
     for (int i = 0; i < IT; ++i) Y[loff + pix(kx_of(i))] = pf[i];
   };
+  // DHT pair of item i from a transformed buffer: two packed columns (Hartley) or one real column (HR)
+  auto unpack2 = [&](const C* Y, int i, float& h0, float& h1) {
+    if constexpr (HR)
+      realsplit_padded<C, float>(Y, N, kx_of(i), rsw[kx_of(i)], h0, h1);
+    else
+      hartley_padded<C, float>(Y + loff, N, kx_of(i), h0, h1);
+  };
   int bs0[P0::PER], bs1[P1::PER], bs2[P2::PER];
 
   if (!fftg) {
-    const float cm0 = p.C - p.lamy[b * B + 2 * l], cm1 = p.C - p.lamy[b * B + 2 * l + 1];
+    const float cm0 = p.C - p.lamy[HR ? b : b * B + 2 * l];
+    const float cm1 = HR ? cm0 : p.C - p.lamy[b * B + 2 * l + 1];
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
-      const float lx = p.lamx[kx_of(i)];
-      c1[i] = make_float2((cm0 - lx) * inv_ae, (cm1 - lx) * inv_ae);
+      const float lx0 = p.lamx[kx_of(i)], lx1 = HR ? p.lamx[kx_of(i) + N] : lx0;
+      c1[i] = make_float2((cm0 - lx0) * inv_ae, (cm1 - lx1) * inv_ae);
     }
     if (p.xt_phase != 2) {
 #pragma unroll
@@ -609,7 +625,7 @@ __global__ void __launch_bounds__(512) k_precond_xt_ws_2d(KP<float> p, const flo
       constexpr int I0 = decltype(I0c)::value, I1 = decltype(I1c)::value;
       float ha[I1 - I0], hb[I1 - I0];
 #pragma unroll
-      for (int i = I0; i < I1; ++i) hartley_padded<C, float>(Y + loff, N, kx_of(i), ha[i - I0], hb[i - I0]);
+      for (int i = I0; i < I1; ++i) unpack2(Y, i, ha[i - I0], hb[i - I0]);
       if (kr < T - 1 || !p.last_slab) {
 #pragma unroll
         for (int i = I0; i < I1; ++i) {
@@ -696,8 +712,14 @@ __global__ void __launch_bounds__(512) k_precond_xt_ws_2d(KP<float> p, const flo
     const float kk1 = (float)(p.j0 + kn + 1);   // global row index
     auto unpack = [&](int i) {
       float ha, hb;
-      hartley_padded<C, float>(Y + loff, N, kx_of(i), ha, hb);
-      wk[tt + i * NTT] = make_float2(ha, hb);
+      unpack2(Y, i, ha, hb);
+      if constexpr (HR) {   // spatial x = k and k + N of the real column
+        float* wf = reinterpret_cast<float*>(wk);
+        wf[kx_of(i)] = ha;
+        wf[kx_of(i) + N] = hb;
+      } else {
+        wk[tt + i * NTT] = make_float2(ha, hb);
+      }
     };
     auto subst = [&](int i) {
       // theta >= 1e-20 (clamped at the sweep start): the closed form tends to (k+1)/(k+2) as theta -> 0
@@ -755,8 +777,18 @@ __global__ void __launch_bounds__(512) k_precond_xt_ws_2d(KP<float> p, const flo
     if (fftg) {
       if (fft_on) split_write<C, N, NL, NTF, 1>(X, vf, bs1);
     } else if (do_stage) {
+      if constexpr (HR) {   // modes k and k + N -> packed positions (float f at element f/2, part f%2)
+        float* Yf = reinterpret_cast<float*>(Y);
 #pragma unroll
-      for (int i = 0; i < IT; ++i) Y[loff + pix(kx_of(i))] = c3[i];
+        for (int i = 0; i < IT; ++i) {
+          const int f0 = kx_of(i), f1 = kx_of(i) + N;
+          Yf[2 * pix(f0 >> 1) + (f0 & 1)] = c3[i].x;
+          Yf[2 * pix(f1 >> 1) + (f1 & 1)] = c3[i].y;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < IT; ++i) Y[loff + pix(kx_of(i))] = c3[i];
+      }
       ldrow(max(kn - 1, 0));
     }
     lds_sync();

@@ -165,11 +165,19 @@ __global__ void __launch_bounds__(256) k_slab_fixup(KP<R> p, const R* __restrict
   const size_t M = (size_t)p.nb * nx * B;
   const size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= M) return;
-  const int c = (int)(m % B);
-  const size_t bx = m / B;
-  const int kx = (int)(bx % nx), b = (int)(bx / nx);
+  int kx, ky;
+  if (p.half_real) {   // one real column per block; item k of the block holds modes k and k + nx/2
+    const int w = (int)(m % nx);
+    ky = (int)(m / nx);
+    kx = (w >> 1) + (w & 1) * (nx >> 1);
+  } else {
+    const int c = (int)(m % B);
+    const size_t bx = m / B;
+    kx = (int)(bx % nx);
+    ky = (int)(bx / nx) * B + c;
+  }
   const double inv_ae = 1.0 / (double)p.ae;
-  const double dd = ((double)p.C - (double)p.lamx[kx] - (double)p.lamy[b * B + c]) * inv_ae;
+  const double dd = ((double)p.C - (double)p.lamx[kx] - (double)p.lamy[ky]) * inv_ae;
   // pivot state entering row j0 (closed form, see h_entry)
   double h = 1.0;
   if (p.j0 > 0) {

@@ -41,6 +41,7 @@ struct KP {
   const R* rho_halo;       // rho row j0+T (first row of the next slab) [nx][ny]; null on the last slab
   const R* carry_y;        // backward right carry x_{j0+T} (spectral, work-row layout); null = zero
   void* gscr;              // per-workgroup global FFT scratch (1-D lines beyond LDS), 2 lines per slot
+  int half_real;           // 2-D x-transform on one real column per block (nx = 8192, B = 1)
 };
 
 // neighbour index along an axis of length n with boundary condition bc

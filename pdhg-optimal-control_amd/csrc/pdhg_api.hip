@@ -105,6 +105,7 @@ struct Impl : ImplBase {
   // fast row kernels (fp32, power-of-two ny): RW rows per workgroup, NTf threads
   bool fast_rows = false;
   bool glb_line = false;          // 1-D line FFTs over global scratch (nx beyond LDS)
+  bool half_real = false;         // 2-D nx = 8192: one real column per x-transform block
   int nt1d = 256;                 // 1-D residual / update block size (1024 on the global-scratch path)
   bool fast_xt = false;
   bool ws_xt = false;             // warp-specialised variant (k_precond_xt_ws_2d)            // fp32 power-of-two nx: k_precond_xt_fast_2d
@@ -198,9 +199,13 @@ struct Impl : ImplBase {
       int nyp = 2;
       while (nyp < ny) nyp <<= 1;
       if (B > nyp) B = nyp;
-      if ((size_t)nx * B > cap)
+      // fp32 nx = 8192 (C4): one real column per block, packed into a 4096-point FFT (half_real)
+      half_real = sizeof(R) == 4 && nx == 8192;
+      if (half_real) B = 1;
+      if (!half_real && (size_t)nx * B > cap)
         return fail(PDHG_ERR_UNSUPPORTED, "nx=%d too large for the x-transform slab (max %zu in this precision)", nx,
                     cap / 2);
+      p.half_real = half_real ? 1 : 0;
       p.B = B;
       p.lB = 0;
       while ((1 << p.lB) < B) ++p.lB;
@@ -217,7 +222,11 @@ struct Impl : ImplBase {
       gx5 = (ny + 255) / 256;
       g5 = std::max(1, std::min(T * nx, 8192 / std::max(1, gx5)));
       if (const char* e = getenv("PDHG_DBG")) p.dbg = atoi(e);   // timing experiments only
-      if (sizeof(R) == 4 && plx.pow2 && nx * (B / 2) == 4096 && nx >= 512) {
+      if (half_real) {
+        fast_xt = true;
+        ws_xt = true;
+        lds_fast_xt = (size_t)(2 * (4096 + 4096 / 16) + 816 + 4096) * sizeof(C);   // + split twiddles
+      } else if (sizeof(R) == 4 && plx.pow2 && nx * (B / 2) == 4096 && nx >= 512) {
         fast_xt = true;
         ws_xt = (nx == 4096);   // the other widths spill registers in the warp-specialised form
         if (const char* e = getenv("PDHG_XT_WS")) ws_xt = atoi(e) != 0;   // tuning override
@@ -550,6 +559,7 @@ struct Impl : ImplBase {
           };
           if (ws_xt) {
             switch (pb.nx) {
+              case 8192: rc = go(k_precond_xt_ws_2d<4096, 1, true>); break;
               case 4096: rc = go(k_precond_xt_ws_2d<4096, 1>); break;
               case 2048: rc = go(k_precond_xt_ws_2d<2048, 2>); break;
               case 1024: rc = go(k_precond_xt_ws_2d<1024, 4>); break;

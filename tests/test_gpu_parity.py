@@ -304,3 +304,26 @@ def test_dropin_update_functions(native):
     finally:
         U.set_precision("fp32")
         U.clear_cache()
+
+
+HALF_REAL = [(1, 2, 8192, 256, 3, 0.0), (2, 2, 8192, 256, 4, 0.0)]   # C4's nx: one real column per x block
+
+
+@pytest.mark.parametrize("case", HALF_REAL, ids=["e{}d{}_{}x{}_T{}_eps{}".format(*c) for c in HALF_REAL])
+def test_half_real_x_transform_fp32(native, case):
+    """nx = 8192 (BASELINE configs[4]) in fp32: the x-DHT of one real 8192-point column per block via a
+    packed 4096-point FFT and the real split; same bounds as the other fp32 cases."""
+    P = make_problem(*case)
+    ctx = device_ctx(P, "fp32")
+    ctx.set_state(P["phi"], P["rho"], P["alp"])
+    ctx.update_primal(TAU)
+    phi_o = _oracle_primal(P, P["phi"], P["rho"], P["alp"])
+    assert rel(ctx.get_state()[0], phi_o) < 1e-6
+    ctx.set_state(P["phi"], P["rho"], P["alp"])
+    phi_o, rho_o, alp_o, e1_o, e2_o = _oracle_iterate(P, 5)
+    st = ctx.iterate(5, TAU, SIGMA, -1.0, 1)
+    phi_d, rho_d, _ = ctx.get_state()
+    assert st["iters_run"] == 5
+    assert rel(phi_d, phi_o) < 1e-5
+    assert rel(rho_d, rho_o) < 2e-4
+    ctx.close()

@@ -16,6 +16,7 @@ CASES = [
     (1, 512, 256, 5, 5, 3),
     (2, 4096, 256, 6, 2, 1),
     (1, 4096, 256, 4, 3, 2),
+    (2, 8192, 256, 5, 2, 1),    # half-real x blocks (C4's nx)
 ]
 
 
