@@ -555,6 +555,22 @@ struct FFTFx {              // compile-time power-of-two n, NL lines
 };
 
 // Hartley unpack of line l at frequency k from the FFT Z of z = a + i b.
+// DCT-II (scipy norm=None: y_k = 2 sum x_n cos(pi k (2n+1) / 2n)) of two real columns a, b that were
+// packed as z = v_a + i v_b in Makhoul order (v[m] = x[2m], v[n-1-m] = x[2m+1]) and FFT'd into Z:
+// V_a = (Z_k + conj Z_{n-k})/2, V_b = (Z_k - conj Z_{n-k})/(2i), y = 2 Re(w_k V), w_k = e^{-i pi k/(2n)}.
+template <typename C, typename T>
+__device__ __forceinline__ void dct_pair(const C* Z, int n, int nl, int k, int l, C w, T& ya, T& yb) {
+  const int km = (k == 0) ? 0 : n - k;
+  const C z = Z[(size_t)k * nl + l];
+  const C c = Z[(size_t)km * nl + l];
+  const T ax = (T)0.5 * (z.x + c.x), ay = (T)0.5 * (z.y - c.y);     // V_a
+  const T bx = (T)0.5 * (z.y + c.y), by = (T)-0.5 * (z.x - c.x);    // V_b
+  ya = (T)2 * (w.x * ax - w.y * ay);
+  yb = (T)2 * (w.x * bx - w.y * by);
+}
+// Makhoul position of sample x in the packed DCT sequence (and its inverse map)
+__device__ __forceinline__ int dct_perm(int x, int n) { return (x & 1) ? n - 1 - (x >> 1) : (x >> 1); }
+
 template <typename C, typename T>
 __device__ __forceinline__ void hartley_pair(const C* Z, int n, int nl, int k, int l, T& ha, T& hb) {
   const int km = (k == 0) ? 0 : n - k;

@@ -151,9 +151,10 @@ __global__ void __launch_bounds__(512) k_precond_xt_2d(KP<R> p, F plx, const cpl
   const R ae = p.ae;
   const R inv_ae = (R)1 / ae;
 
+  const bool dct = p.dctw != nullptr;   // bc_x = 1: DCT-II along x (egno 3)
   for (int pos = tid; pos < M; pos += NT) {
     const int kx = pos >> p.lB, c = pos & (B - 1);
-    const R d0 = p.C - p.lamx[kx] - p.lamy[b * B + c];
+    const R d0 = p.C - p.lamx[kx] - p.cx[kx] * p.lamy[b * B + c];
     const R delta = d0 / ((R)2 * ae);
     const R th = log1p(delta + sqrt(delta * (delta + (R)2)));   // cosh(th) = 1 + d0/(2 ae)
     sth[pos] = th;
@@ -174,7 +175,14 @@ __global__ void __launch_bounds__(512) k_precond_xt_2d(KP<R> p, F plx, const cpl
 #pragma unroll
     for (int i = 0; i < PF; ++i) {
       const int e = tid + i * NT;
-      if (e < NC) A[e] = pf[i];
+      if (e < NC) {
+        if (dct) {   // sample x of line l -> Makhoul position
+          const int xs = e / nl, l = e - xs * nl;
+          A[(size_t)dct_perm(xs, nx) * nl + l] = pf[i];
+        } else {
+          A[e] = pf[i];
+        }
+      }
     }
     __syncthreads();
     if (k + 1 < T) {
@@ -191,7 +199,10 @@ __global__ void __launch_bounds__(512) k_precond_xt_2d(KP<R> p, F plx, const cpl
     for (int pos = tid; pos < M; pos += NT) {
       const int kx = pos >> p.lB, c = pos & (B - 1);
       R ha, hb;
-      hartley_pair<C, R>(Z, nx, nl, kx, c >> 1, ha, hb);
+      if (dct)
+        dct_pair<C, R>(Z, nx, nl, kx, c >> 1, p.dctw[kx], ha, hb);
+      else
+        hartley_pair<C, R>(Z, nx, nl, kx, c >> 1, ha, hb);
       const R h = (c & 1) ? hb : ha;
       const R th = sth[pos];
       const R prev = sbp[pos];
@@ -205,7 +216,7 @@ __global__ void __launch_bounds__(512) k_precond_xt_2d(KP<R> p, F plx, const cpl
         dst[pos] = v;
       } else {
         // Neumann last row: u_{T-1} = d0 + ae expm1(-th)(1 + e^{-th(2T-1)}) / E_T
-        const R d0 = p.C - p.lamx[kx] - p.lamy[b * B + c];
+        const R d0 = p.C - p.lamx[kx] - p.cx[kx] * p.lamy[b * B + c];
         R u;
         if (th > (R)0) {
           const R ET = expm1((R)-2 * th * (R)T);
@@ -258,11 +269,35 @@ __global__ void __launch_bounds__(512) k_precond_xt_2d(KP<R> p, F plx, const cpl
       }
     }
     __syncthreads();
-    const C* Z = plx.template run<C>(A, Bf, twx);
+    const C* Z;
+    if (dct) {
+      // inverse DCT-II (scipy idct) via one forward FFT: V_k = 1/2 e^{i pi k/2n} (y_k - i y_{n-k}) per
+      // column (y_n = 0), z = V_a + i V_b, v = IFFT(z) = conj(FFT(conj z)) (the 1/n sits in the update's
+      // 1/(nx ny)); x[2m] = v[m], x[2m+1] = v[n-1-m]
+      for (int e = tid; e < NC; e += NT) {
+        const int kk = e / nl, l = e - kk * nl;
+        const C ck = A[(size_t)kk * nl + l];                                    // (y_a[k], y_b[k])
+        const C cr = (kk == 0) ? cmk<C>((R)0, (R)0) : A[(size_t)(nx - kk) * nl + l];
+        const C w = p.dctw[kk];                                                 // conj -> e^{+i pi k/2n}
+        const R vax = (R)0.5 * (w.x * ck.x - w.y * cr.x), vay = (R)0.5 * (-w.x * cr.x - w.y * ck.x);
+        const R vbx = (R)0.5 * (w.x * ck.y - w.y * cr.y), vby = (R)0.5 * (-w.x * cr.y - w.y * ck.y);
+        Bf[e] = cmk<C>(vax - vby, -(vay + vbx));                                // conj(V_a + i V_b)
+      }
+      __syncthreads();
+      Z = plx.template run<C>(Bf, A, twx);
+    } else {
+      Z = plx.template run<C>(A, Bf, twx);
+    }
     for (int e = tid; e < M; e += NT) {
       const int xx = e >> p.lB, c = e & (B - 1);
       R ha, hb;
-      hartley_pair<C, R>(Z, nx, nl, xx, c >> 1, ha, hb);
+      if (dct) {
+        const C v = Z[(size_t)dct_perm(xx, nx) * nl + (c >> 1)];   // conj of the FFT output
+        ha = v.x;
+        hb = -v.y;
+      } else {
+        hartley_pair<C, R>(Z, nx, nl, xx, c >> 1, ha, hb);
+      }
       wk[e] = (c & 1) ? hb : ha;
     }
     __syncthreads();

@@ -42,6 +42,9 @@ struct KP {
   const R* carry_y;        // backward right carry x_{j0+T} (spectral, work-row layout); null = zero
   void* gscr;              // per-workgroup global FFT scratch (1-D lines beyond LDS), 2 lines per slot
   int half_real;           // 2-D x-transform on one real column per block (nx = 8192, B = 1)
+  // bc_x = 1 (egno 3, utils_precond.py:159-174): DCT-II along x instead of the DHT
+  const R* cx;             // y-symbol factor per x mode: 2 cos(pi kx / 2nx) (DCT) or 1 [nx]
+  const cplx<R>* dctw;     // e^{-i pi k / 2nx}, k < nx (DCT only)
 };
 
 // neighbour index along an axis of length n with boundary condition bc

@@ -200,7 +200,7 @@ struct Impl : ImplBase {
       while (nyp < ny) nyp <<= 1;
       if (B > nyp) B = nyp;
       // fp32 nx = 8192 (C4): one real column per block, packed into a 4096-point FFT (half_real)
-      half_real = sizeof(R) == 4 && nx == 8192;
+      half_real = sizeof(R) == 4 && nx == 8192 && pb.bc_x == 0;
       if (half_real) B = 1;
       if (!half_real && (size_t)nx * B > cap)
         return fail(PDHG_ERR_UNSUPPORTED, "nx=%d too large for the x-transform slab (max %zu in this precision)", nx,
@@ -226,7 +226,7 @@ struct Impl : ImplBase {
         fast_xt = true;
         ws_xt = true;
         lds_fast_xt = (size_t)(2 * (4096 + 4096 / 16) + 816 + 4096) * sizeof(C);   // + split twiddles
-      } else if (sizeof(R) == 4 && plx.pow2 && nx * (B / 2) == 4096 && nx >= 512) {
+      } else if (sizeof(R) == 4 && plx.pow2 && nx * (B / 2) == 4096 && nx >= 512 && pb.bc_x == 0) {
         fast_xt = true;
         ws_xt = (nx == 4096);   // the other widths spill registers in the warp-specialised form
         if (const char* e = getenv("PDHG_XT_WS")) ws_xt = atoi(e) != 0;   // tuning override
@@ -344,11 +344,28 @@ struct Impl : ImplBase {
         const double y = pb.ys[i];
         ay[i] = (R)((y - 1.0) * (y - 1.0) + 0.1);
       }
-    // Laplacian symbol = FFT of the periodic stencil (utils_precond.py:42-71), real part
+    // Laplacian symbol = FFT of the periodic stencil (utils_precond.py:42-71), real part.
+    // bc (1,0) (egno 3): fv = fft_y(dct_x(lap)) = DCT-II(x stencil)[kx] + 2 cos(pi kx/2nx) * lam_y[ky]
+    // -- the reference transforms the periodic stencil array with the DCT, and DCT-II(e_0) = 2 cos(.)
+    const bool dct_x = is2d && pb.bc_x == 1;
+    std::vector<R> cx(nx, (R)1);
+    std::vector<C> dctw;
     for (int k = 0; k < nx; ++k) {
-      const double l = -2.0 * (1.0 - std::cos(2.0 * M_PI * k / nx)) / (pb.dx * pb.dx);
+      double l = -2.0 * (1.0 - std::cos(2.0 * M_PI * k / nx)) / (pb.dx * pb.dx);
+      if (dct_x) {
+        auto c2 = [&](int n) { return 2.0 * std::cos(M_PI * k * (2.0 * n + 1.0) / (2.0 * nx)); };
+        l = (-2.0 * c2(0) + c2(1) + c2(nx - 1)) / (pb.dx * pb.dx);
+        cx[k] = (R)c2(0);
+      }
       lamx[k] = (R)l;
       d0[k] = (R)std::pow(pb.C - l, pb.pow_);   // 1-D thomas_b = (C - fv)^pow, :125-126
+    }
+    if (dct_x) {
+      dctw.resize(nx);
+      for (int k = 0; k < nx; ++k) {
+        dctw[k].x = (R)std::cos(-M_PI * k / (2.0 * nx));
+        dctw[k].y = (R)std::sin(-M_PI * k / (2.0 * nx));
+      }
     }
     R *d_ax, *d_ay, *d_lamx, *d_lamy, *d_d0;
     if ((rc = alloc(&d_ax, nx))) return rc;
@@ -365,6 +382,19 @@ struct Impl : ImplBase {
       for (int k = 0; k < ny; ++k) lamy[k] = (R)(-2.0 * (1.0 - std::cos(2.0 * M_PI * k / ny)) / (pb.dy * pb.dy));
     if ((rc = alloc(&d_lamy, nyp))) return rc;
     HIP_TRY(hipMemcpy(d_lamy, lamy.data(), nyp * sizeof(R), hipMemcpyHostToDevice));
+    {
+      R* d_cx;
+      if ((rc = alloc(&d_cx, nx))) return rc;
+      HIP_TRY(hipMemcpy(d_cx, cx.data(), nx * sizeof(R), hipMemcpyHostToDevice));
+      p.cx = d_cx;
+      p.dctw = nullptr;
+      if (dct_x) {
+        C* d_w;
+        if ((rc = alloc(&d_w, nx))) return rc;
+        HIP_TRY(hipMemcpy(d_w, dctw.data(), nx * sizeof(C), hipMemcpyHostToDevice));
+        p.dctw = d_w;
+      }
+    }
     p.ax = d_ax;
     p.ay = d_ay;
     p.lamx = d_lamx;
@@ -1144,9 +1174,9 @@ int pdhg_create(const pdhg_problem* prob, int device, pdhg_ctx** out) {
   if (p.rho_alp_iters < 1) return fail(PDHG_ERR_ARG, "rho_alp_iters must be >= 1");
   // preconditioner boundary conditions (utils_precond.py:121-124, :157-163)
   if (p.ndim == 1 && p.bc_x != 0) return fail(PDHG_ERR_UNSUPPORTED, "H1_precond_1d supports bc=0 only");
-  if (p.ndim == 2 && !(p.bc_x == 0 && p.bc_y == 0))
-    return fail(PDHG_ERR_UNSUPPORTED, "bc (%d,%d): only periodic (0,0) is implemented on the device (egno 3's "
-                                      "(1,0) DCT path is not built yet)", p.bc_x, p.bc_y);
+  if (p.ndim == 2 && !((p.bc_x == 0 || p.bc_x == 1) && p.bc_y == 0))
+    return fail(PDHG_ERR_UNSUPPORTED, "bc (%d,%d): H1_precond_2d supports (0,0) and (1,0) only "
+                                      "(utils_precond.py:157-163)", p.bc_x, p.bc_y);
   if (p.ndim == 1 && p.Ct < 0) return fail(PDHG_ERR_ARG, "Ct must be >= 0");
   if (p.C < 0) return fail(PDHG_ERR_ARG, "C must be >= 0");
   int ndev = 0;
