@@ -731,72 +731,80 @@ __global__ void __launch_bounds__(512) k_precond_xt_ws_2d(KP<float> p, const flo
     };
     const bool do_unpack = s >= 2 && !(p.dbg & 4), do_subst = (s >= 1 || p.slab) && s <= T - 1 && !(p.dbg & 4),
                do_stage = s <= T - 1;
-    // P1
-    if (fftg) {
-      if (fft_on) split_read<C, N, NL, NTF, 0>(X, twl, tid, vf, bs0);
-    } else {
-      if (do_unpack) {
-#pragma unroll
-        for (int i = 0; i < CH0; ++i) unpack(i);
-      }
-      if (do_subst) {
-#pragma unroll
-        for (int i = 0; i < CH0; ++i) subst(i);
-      }
-    }
-    lds_sync();
-    // P2
-    if (fftg) {
-      if (fft_on) split_write<C, N, NL, NTF, 0>(X, vf, bs0);
-    } else {
-      if (do_unpack) {
-#pragma unroll
-        for (int i = CH0; i < CH1; ++i) unpack(i);
-      }
-      if (do_subst) {
-#pragma unroll
-        for (int i = CH0; i < CH1; ++i) subst(i);
-      }
-    }
-    lds_sync();
-    // P3
-    if (fftg) {
-      if (fft_on) split_read<C, N, NL, NTF, 1>(X, twl, tid, vf, bs1);
-    } else {
-      if (do_unpack) {
-#pragma unroll
-        for (int i = CH1; i < IT; ++i) unpack(i);
-      }
-      if (do_subst) {
-#pragma unroll
-        for (int i = CH1; i < IT; ++i) subst(i);
-      }
-    }
-    lds_sync();
-    // P4: Y is no longer read -> stage x_{kn} into it, prefetch b'_{kn-1}
-    if (fftg) {
-      if (fft_on) split_write<C, N, NL, NTF, 1>(X, vf, bs1);
-    } else if (do_stage) {
+    // stage x_{kn} of items [I0, I1) into Y (after every unpack read of Y: phases P4-P6)
+    auto stage_x = [&](auto I0c, auto I1c) {
+      constexpr int I0 = decltype(I0c)::value, I1 = decltype(I1c)::value;
       if constexpr (HR) {   // modes k and k + N -> packed positions (float f at element f/2, part f%2)
         float* Yf = reinterpret_cast<float*>(Y);
 #pragma unroll
-        for (int i = 0; i < IT; ++i) {
+        for (int i = I0; i < I1; ++i) {
           const int f0 = kx_of(i), f1 = kx_of(i) + N;
           Yf[2 * pix(f0 >> 1) + (f0 & 1)] = c3[i].x;
           Yf[2 * pix(f1 >> 1) + (f1 & 1)] = c3[i].y;
         }
       } else {
 #pragma unroll
-        for (int i = 0; i < IT; ++i) Y[loff + pix(kx_of(i))] = c3[i];
+        for (int i = I0; i < I1; ++i) Y[loff + pix(kx_of(i))] = c3[i];
       }
-      ldrow(max(kn - 1, 0));
+    };
+    using Z0 = std::integral_constant<int, 0>;
+    using ZA = std::integral_constant<int, CH0>;
+    using ZB = std::integral_constant<int, CH1>;
+    using ZC = std::integral_constant<int, IT>;
+    // P1-P3: FFT passes 0-1 | unpack of Y (the previous x row's transform) in three chunks
+    if (fftg) {
+      if (fft_on) split_read<C, N, NL, NTF, 0>(X, twl, tid, vf, bs0);
+    } else if (do_unpack) {
+#pragma unroll
+      for (int i = 0; i < CH0; ++i) unpack(i);
     }
     lds_sync();
-    // P5
-    if (fftg && fft_on) split_read<C, N, NL, NTF, 2>(X, twl, tid, vf, bs2);
+    if (fftg) {
+      if (fft_on) split_write<C, N, NL, NTF, 0>(X, vf, bs0);
+    } else if (do_unpack) {
+#pragma unroll
+      for (int i = CH0; i < CH1; ++i) unpack(i);
+    }
     lds_sync();
-    // P6
-    if (fftg && fft_on) split_write<C, N, NL, NTF, 2>(X, vf, bs2);
+    if (fftg) {
+      if (fft_on) split_read<C, N, NL, NTF, 1>(X, twl, tid, vf, bs1);
+    } else if (do_unpack) {
+#pragma unroll
+      for (int i = CH1; i < IT; ++i) unpack(i);
+    }
+    lds_sync();
+    // P4-P6: FFT passes 1-2 | substitution x_{kn} = b'_{kn} + g x_{kn+1} in three chunks, staged into Y;
+    // the next b' row is prefetched once the last chunk has consumed pf
+    if (fftg) {
+      if (fft_on) split_write<C, N, NL, NTF, 1>(X, vf, bs1);
+    } else if (do_stage) {
+      if (do_subst) {
+#pragma unroll
+        for (int i = 0; i < CH0; ++i) subst(i);
+      }
+      stage_x(Z0{}, ZA{});
+    }
+    lds_sync();
+    if (fftg) {
+      if (fft_on) split_read<C, N, NL, NTF, 2>(X, twl, tid, vf, bs2);
+    } else if (do_stage) {
+      if (do_subst) {
+#pragma unroll
+        for (int i = CH0; i < CH1; ++i) subst(i);
+      }
+      stage_x(ZA{}, ZB{});
+    }
+    lds_sync();
+    if (fftg) {
+      if (fft_on) split_write<C, N, NL, NTF, 2>(X, vf, bs2);
+    } else if (do_stage) {
+      if (do_subst) {
+#pragma unroll
+        for (int i = CH1; i < IT; ++i) subst(i);
+      }
+      stage_x(ZB{}, ZC{});
+      ldrow(max(kn - 1, 0));
+    }
     lds_sync();
   }
 }
