@@ -154,31 +154,33 @@ int pdhg_algorithmic_bytes(pdhg_ctx* ctx, int k, const char* kernel_class, doubl
  * New capability: the reference (JAX, single device, README.md:6) has no distributed path.  A window's
  * T_total unknown time rows are split into contiguous slabs, one context (one GPU) each; a slab context
  * owns rows [j0, j0 + p->T) (its phi arrays hold p->T + 1 rows: row 0 is global phi row j0).  The
- * caller moves planes between slabs (RCCL halos / allgathers / allreduces; pdhg_amd/slab.py) and runs
- * one outer iteration of utils_pdhg_solver.py:51-88 as:
- *   plane_in(0, rho halo) -> forward(tau) -> plane_out(2, D) -> [allgather D] -> fixup(allD, allG, rank)
- *   -> plane_out(3, X0) -> [allgather X0] -> backward(tau, allX0, allG, rank, n, sums) -> [allreduce sums]
- *   -> primal_finalize(sums) -> plane_out(1, phi_bar row T) -> [to the next slab: plane_in(1, ...)]
+ * caller moves planes between slabs (RCCL; pdhg_amd/slab.py) and runs one outer iteration of
+ * utils_pdhg_solver.py:51-88 as:
+ *   plane_in(0, next slab's rho row 0) -> forward(tau) -> plane_out(2, [D, S1]) -> [allgather]
+ *   -> fixup(allDS, allGS, rank, n) -> backward(tau, sums) -> [allreduce sums] -> primal_finalize(sums)
+ *   -> plane_out(1, phi_bar row T) -> [to the next slab: plane_in(1, ...)]
  *   -> per dual sub-iteration s: dual(sigma, k, s, sums) -> [allreduce] -> dual_finalize(eps, s, sums)
- *   -> outer(k, sums) -> [allreduce] -> outer_finalize(eps, k, sums).
- * allG: every slab's pdhg_slab_carry_gain plane (iteration-invariant; gather once).  Plane pointers are
- * device pointers (float); sums are device vectors of 16 doubles.  All calls enqueue on the context's
- * stream (pdhg_set_stream to share the caller's).  fp32, ndim 2, power-of-two nx in [512, 4096]. */
+ *   -> outer(k, sums) -> [allreduce when k > 1] -> outer_finalize(eps, k, sums).
+ * The Thomas recurrences are affine in the carries entering a slab (oracle/slab_oracle.py): D = the
+ * zero-carry forward sweep's last row, S1 = sum P'_k b0_k; allGS: every slab's [G, S2]
+ * (pdhg_slab_carry_gain, iteration-invariant, gather once).  Planes are device pointers (float; D/S1 and
+ * G/S2 are pairs of spectral planes, see pdhg_slab_plane_size); sums are device vectors of 16 doubles.
+ * All calls enqueue on the context's stream (pdhg_set_stream to share the caller's).
+ * fp32, ndim 2, power-of-two nx in [512, 8192], bc (0,0). */
 int pdhg_create_slab(const pdhg_problem* p, int j0, int T_total, int device, pdhg_ctx** out);
 int pdhg_set_stream(pdhg_ctx* ctx, void* hip_stream);
 int pdhg_slab_plane_size(pdhg_ctx* ctx, unsigned long long* spatial, unsigned long long* spectral);
 int pdhg_slab_begin(pdhg_ctx* ctx);                                       /* reset the device loop control */
-int pdhg_slab_carry_gain(pdhg_ctx* ctx, void* G_out);                      /* G = prod of the slab's pivots */
+int pdhg_slab_carry_gain(pdhg_ctx* ctx, void* GS_out);                    /* [G, S2], 2 spectral planes */
 int pdhg_slab_forward(pdhg_ctx* ctx, double tau);                          /* residual + x-DHT + forward sweep */
-int pdhg_slab_fixup(pdhg_ctx* ctx, const void* all_D, const void* all_G, int rank);
-int pdhg_slab_backward(pdhg_ctx* ctx, double tau, const void* all_X0, const void* all_G, int rank, int nranks,
-                       double* sums);                                      /* backward + inverse + update */
+int pdhg_slab_fixup(pdhg_ctx* ctx, const void* all_DS, const void* all_GS, int rank, int nranks);
+int pdhg_slab_backward(pdhg_ctx* ctx, double tau, double* sums);           /* backward + inverse + update */
 int pdhg_slab_primal_finalize(pdhg_ctx* ctx, const double* sums);
 int pdhg_slab_dual(pdhg_ctx* ctx, double sigma, int rho_alp_iters, int sub, double* sums);
 int pdhg_slab_dual_finalize(pdhg_ctx* ctx, double eps, int sub, const double* sums);
 int pdhg_slab_outer(pdhg_ctx* ctx, int rho_alp_iters, double* sums);
 int pdhg_slab_outer_finalize(pdhg_ctx* ctx, double eps, int rho_alp_iters, const double* sums);
-int pdhg_slab_plane_out(pdhg_ctx* ctx, int which, void* dst); /* 0 rho row 0, 1 phi_bar row T, 2 D, 3 X0 */
+int pdhg_slab_plane_out(pdhg_ctx* ctx, int which, void* dst); /* 0 rho row 0, 1 phi_bar row T, 2 [D, S1] */
 int pdhg_slab_plane_in(pdhg_ctx* ctx, int which, const void* src); /* 0 rho halo, 1 phi_bar row 0 */
 int pdhg_slab_status(pdhg_ctx* ctx, pdhg_stats* st);
 

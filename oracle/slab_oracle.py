@@ -128,3 +128,47 @@ def monolithic_tridiag(diag, r, ae):
     du = np.full(T, -ae)
     du[-1] = 0.0
     return O.tridiagonal_solve(dl, diag, du, r)
+
+
+# ---- single-exchange variant: X0_q is affine in the slab's incoming carry -------------------------
+#   X0_q = S1_q + c_{q-1} S2_q,   S1 = sum_k P'_k b0_k (data),  S2 = sum_k P'_k P_k (iteration-invariant)
+# so ONE allgather of (D, S1) per iteration lets every slab fold both scans locally.
+
+def s_sums(b0, g, j0):
+    """S1 = sum P'_k b0_k and S2 = sum P'_k P_k over the slab's rows (P'_k = prod g_{j0..k-1})."""
+    Pk = np.ones_like(g[0])
+    s1 = np.zeros_like(b0[0])
+    s2 = np.zeros_like(g[0])
+    for i in range(b0.shape[0]):
+        s1 = s1 + Pk * b0[i]
+        s2 = s2 + Pk * Pk * g[j0 + i]
+        Pk = Pk * g[j0 + i]
+    return s1, s2
+
+
+def carries_single(D, S1, G, S2, q):
+    """(c_{q-1}, y_q) of slab q from everybody's (D, S1, G, S2)."""
+    P = len(D)
+    cin = [np.zeros_like(D[0])]
+    for p in range(P - 1):
+        cin.append(D[p] + G[p] * cin[p])          # cin[p] = carry INTO slab p
+    y = np.zeros_like(D[0])
+    for p in range(P - 1, q, -1):
+        y = (S1[p] + cin[p] * S2[p]) + G[p] * y   # X0_p + G_p y
+    return cin[q], y
+
+
+def thomas_slabs_single(diag, r, ae, P):
+    T = diag.shape[0]
+    bounds = slab_bounds(T, P)
+    g = pivots(diag, ae)
+    fw = [local_forward(r, g, ae, j0, j1) for (j0, j1) in bounds]
+    ss = [s_sums(fw[q][0], g, bounds[q][0]) for q in range(P)]
+    D, G = [f[1] for f in fw], [f[2] for f in fw]
+    S1, S2 = [s[0] for s in ss], [s[1] for s in ss]
+    out = []
+    for q, (j0, j1) in enumerate(bounds):
+        c, y = carries_single(D, S1, G, S2, q)
+        b, _ = fixup(fw[q][0], g, j0, c)
+        out.append(local_backward(b, g, j0, y))
+    return np.concatenate(out, axis=0)

@@ -152,21 +152,13 @@ __global__ void __launch_bounds__(256) k_reduce_vec(const double* partials, int 
                                                  ((threadIdx.x == 1 || threadIdx.x == 2) ? add0 : 0.0);
 }
 
-// Per spectral mode m of the work-row layout (2-D: m = (b*nx + kx)*B + c, ky = b*B + c):
-//   c   = prefix scan of the upstream slabs' outgoing planes  (c = D_q + G_q c, q < rank)
-//   b_k += P_k c for the local rows (P_k = prod g_{j0..k}, g from the pivot recurrence), and
-//   X0  = sum_k P'_k b_k  (the zero-right-carry backward value at j0, P'_k = prod g_{j0..k-1}).
-// G mode (allD == null): only G = prod_k g_k is written to out (iteration-invariant, once per context).
+// Per spectral mode m of the work-row layout (2-D: m = (b*nx + kx)*B + c, ky = b*B + c; half_real:
+// item k of block b holds kx = k, k + nx/2): dd = d0/ae and the pivot state entering row j0.
 template <typename R>
-__global__ void __launch_bounds__(256) k_slab_fixup(KP<R> p, const R* __restrict__ allD, const R* __restrict__ allG,
-                                                    int rank, R* __restrict__ out) {
-  if (allD && p.ctrl->done) return;
+__device__ __forceinline__ void slab_mode(const KP<R>& p, size_t m, double& dd, double& h) {
   const int nx = p.nx, B = p.B;
-  const size_t M = (size_t)p.nb * nx * B;
-  const size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= M) return;
   int kx, ky;
-  if (p.half_real) {   // one real column per block; item k of the block holds modes k and k + nx/2
+  if (p.half_real) {
     const int w = (int)(m % nx);
     ky = (int)(m / nx);
     kx = (w >> 1) + (w & 1) * (nx >> 1);
@@ -176,34 +168,83 @@ __global__ void __launch_bounds__(256) k_slab_fixup(KP<R> p, const R* __restrict
     kx = (int)(bx % nx);
     ky = (int)(bx / nx) * B + c;
   }
-  const double inv_ae = 1.0 / (double)p.ae;
-  const double dd = ((double)p.C - (double)p.lamx[kx] - (double)p.lamy[ky]) * inv_ae;
-  // pivot state entering row j0 (closed form, see h_entry)
-  double h = 1.0;
-  if (p.j0 > 0) {
+  dd = ((double)p.C - (double)p.lamx[kx] - (double)p.cx[kx] * (double)p.lamy[ky]) / (double)p.ae;
+  h = 1.0;
+  if (p.j0 > 0) {   // closed form h_{j0-1} (see h_entry)
     const double dl = 0.5 * dd;
     const double th = fmax(log1p(dl + sqrt(dl * (dl + 2.0))), 1e-300);
     h = expm1(-th) * (1.0 + exp(-th * (2.0 * p.j0 + 1.0))) / expm1(-2.0 * th * (p.j0 + 1.0));
   }
-  double cin = 0.0;
-  if (allD)
-    for (int q = 0; q < rank; ++q) cin = (double)allD[(size_t)q * M + m] + (double)allG[(size_t)q * M + m] * cin;
-  double P = 1.0, x0 = 0.0;
+}
+// pivot g_k of local row k (recurrence s = dd + h, g = 1/(1+s), h = s g; Neumann window end: g = 1/s)
+template <typename R>
+__device__ __forceinline__ double slab_pivot(const KP<R>& p, int k, double dd, double& h) {
+  const double s = dd + h;
+  const double g = (p.last_slab && k == p.T - 1) ? 1.0 / s : 1.0 / (1.0 + s);
+  h = s * g;
+  return g;
+}
+
+// Exchange planes of a slab (oracle/slab_oracle.py, single-exchange variant), 2 planes of M each:
+//   data = 0 (once per context):  out = [G, S2],  G = prod_k g_k,  S2 = sum_k P'_k P_k
+//   data = 1 (every iteration):   out = [D, S1],  D = b0 of the last local row,  S1 = sum_k P'_k b0_k
+// (P'_k = prod g_{j0..k-1}, P_k = P'_k g_k; b0 = the zero-carry forward sweep stored in work).
+template <typename R>
+__global__ void __launch_bounds__(256) k_slab_sums(KP<R> p, int data, R* __restrict__ out) {
+  if (data && p.ctrl->done) return;
+  const size_t M = (size_t)p.nb * p.nx * p.B;
+  const size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  double dd, h;
+  slab_mode(p, m, dd, h);
+  double P = 1.0, s = 0.0, b0 = 0.0;
   for (int k = 0; k < p.T; ++k) {
-    const bool last = p.last_slab && k == p.T - 1;
-    const double s = dd + h;
-    const double g = last ? 1.0 / s : 1.0 / (1.0 + s);
-    h = s * g;
-    const double Pn = P * g;
-    if (allD) {
-      R* w = p.work + (size_t)k * M + m;
-      const double bf = (double)*w + Pn * cin;
-      if (rank > 0) *w = (R)bf;
-      x0 += P * bf;
+    const double g = slab_pivot(p, k, dd, h);
+    if (data) {
+      b0 = (double)p.work[(size_t)k * M + m];
+      s += P * b0;
+    } else {
+      s += P * P * g;
     }
-    P = Pn;
+    P *= g;
   }
-  out[m] = allD ? (R)x0 : (R)P;
+  out[m] = data ? (R)b0 : (R)P;
+  out[M + m] = (R)s;
+}
+
+// Carries of slab `rank` from everybody's planes (allDS[q] = [D_q, S1_q], allGS[q] = [G_q, S2_q]):
+//   c_in(q) = D_{q-1} + G_{q-1} c_in(q-1)              (carry INTO slab q; c_in(0) = 0)
+//   X0_q    = S1_q + c_in(q) S2_q                       (slab q's zero-right-carry backward value)
+//   y       = sum_{q > rank} (prod_{rank < s < q} G_s) X0_q   (= x at this slab's j1; written to carry_y)
+// then the own rows' forward fix-up b_k += P_k c_in(rank).
+template <typename R>
+__global__ void __launch_bounds__(256) k_slab_fix(KP<R> p, const R* __restrict__ allDS, const R* __restrict__ allGS,
+                                                  int rank, int nranks, R* __restrict__ carry_y) {
+  if (p.ctrl->done) return;
+  const size_t M = (size_t)p.nb * p.nx * p.B;
+  const size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  double c = 0.0, c_own = 0.0, y = 0.0, W = 1.0;
+  for (int q = 0; q < nranks; ++q) {
+    const size_t o = (size_t)q * 2 * M + m;
+    if (q == rank) c_own = c;
+    if (q > rank) {
+      y += W * ((double)allDS[o + M] + c * (double)allGS[o + M]);
+      W *= (double)allGS[o];
+    }
+    c = (double)allDS[o] + (double)allGS[o] * c;
+  }
+  carry_y[m] = (R)y;
+  if (rank > 0) {
+    double dd, h;
+    slab_mode(p, m, dd, h);
+    double P = 1.0;
+    for (int k = 0; k < p.T; ++k) {
+      P *= slab_pivot(p, k, dd, h);
+      R* w = p.work + (size_t)k * M + m;
+      *w = (R)((double)*w + P * c_own);
+    }
+  }
 }
 
 // rho row 0 of the current buffer set (the set index lives on the device)
@@ -212,17 +253,6 @@ __global__ void __launch_bounds__(256) k_copy_cur_rho(KP<R> p, R* __restrict__ d
   const R* src = p.rho[p.ctrl->cur];
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
     dst[i] = src[i];
-}
-
-// Right carry y of slab `rank`: suffix scan y = X0_q + G_q y over the downstream slabs q > rank.
-template <typename R>
-__global__ void __launch_bounds__(256) k_slab_right_carry(const R* __restrict__ allX0, const R* __restrict__ allG,
-                                                          int rank, int nranks, size_t M, R* __restrict__ y) {
-  const size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= M) return;
-  double v = 0.0;
-  for (int q = nranks - 1; q > rank; --q) v = (double)allX0[(size_t)q * M + m] + (double)allG[(size_t)q * M + m] * v;
-  y[m] = (R)v;
 }
 
 }  // namespace pdhg

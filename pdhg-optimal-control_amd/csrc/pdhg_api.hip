@@ -126,7 +126,7 @@ struct Impl : ImplBase {
   size_t Mspec = 0;          // spectral plane (work row) size
   R* halo_rho = nullptr;     // rho row j0+T from the next slab
   R* carry_y = nullptr;      // backward right carry (spectral plane)
-  R* x0buf = nullptr;        // X0 plane of this slab (zero-right-carry backward value at j0)
+  R* dsbuf = nullptr;        // [D, S1] exchange planes of this slab (2 x Mspec)
 
   ~Impl() override {
     if (stream) hipStreamSynchronize(stream);
@@ -325,7 +325,7 @@ struct Impl : ImplBase {
       Mspec = (size_t)p.nb * nx * p.B;
       if ((rc = alloc(&halo_rho, npl))) return rc;
       if ((rc = alloc(&carry_y, Mspec))) return rc;
-      if ((rc = alloc(&x0buf, Mspec))) return rc;
+      if ((rc = alloc(&dsbuf, 2 * Mspec))) return rc;
       HIP_TRY(hipMemsetAsync(halo_rho, 0, npl * sizeof(R), stream));
       HIP_TRY(hipMemsetAsync(carry_y, 0, Mspec * sizeof(R), stream));
       p.rho_halo = p.last_slab ? nullptr : halo_rho;
@@ -818,24 +818,25 @@ struct Impl : ImplBase {
   // per dual sub-iteration: slab_dual -> [allreduce] -> slab_dual_finalize -> slab_outer ->
   // [allreduce] -> slab_outer_finalize.  With one slab this is exactly iterate().
   int need_slab() const { return slab ? PDHG_OK : fail(PDHG_ERR_STATE, "not a t-slab context"); }
-  int slab_G(R* out) {
-    hipLaunchKernelGGL((k_slab_fixup<R>), dim3((unsigned)((Mspec + 255) / 256)), dim3(256), 0, stream, kp,
-                       (const R*)nullptr, (const R*)nullptr, 0, out);
+  int slab_G(R* out) {   // [G, S2] (iteration-invariant)
+    hipLaunchKernelGGL((k_slab_sums<R>), dim3((unsigned)((Mspec + 255) / 256)), dim3(256), 0, stream, kp, 0, out);
     HIP_TRY(hipGetLastError());
     return PDHG_OK;
   }
-  int slab_forward(R tau) { return launch_primal(tau, 1 | 2, 1); }
-  int slab_fixup(const R* allD, const R* allG, int rank) {
-    hipLaunchKernelGGL((k_slab_fixup<R>), dim3((unsigned)((Mspec + 255) / 256)), dim3(256), 0, stream, kp, allD, allG,
-                       rank, x0buf);
+  int slab_forward(R tau) {   // residual + zero-carry forward sweep + this slab's [D, S1]
+    int rc = launch_primal(tau, 1 | 2, 1);
+    if (rc) return rc;
+    hipLaunchKernelGGL((k_slab_sums<R>), dim3((unsigned)((Mspec + 255) / 256)), dim3(256), 0, stream, kp, 1, dsbuf);
     HIP_TRY(hipGetLastError());
     return PDHG_OK;
   }
-  int slab_backward(R tau, const R* allX0, const R* allG, int rank, int nranks, double* sums) {
-    hipLaunchKernelGGL((k_slab_right_carry<R>), dim3((unsigned)((Mspec + 255) / 256)), dim3(256), 0, stream, allX0,
-                       allG, rank, nranks, Mspec, carry_y);
-    return launch_primal(tau, 2 | 4, 2, sums);
+  int slab_fixup(const R* allDS, const R* allGS, int rank, int nranks) {
+    hipLaunchKernelGGL((k_slab_fix<R>), dim3((unsigned)((Mspec + 255) / 256)), dim3(256), 0, stream, kp, allDS,
+                       allGS, rank, nranks, carry_y);
+    HIP_TRY(hipGetLastError());
+    return PDHG_OK;
   }
+  int slab_backward(R tau, double* sums) { return launch_primal(tau, 2 | 4, 2, sums); }
   int slab_primal_finalize(const double* sums) {
     hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(256), 0, stream, sums, 1, 0.0, kp.ctrl);
     HIP_TRY(hipGetLastError());
@@ -885,7 +886,7 @@ struct Impl : ImplBase {
     HIP_TRY(hipGetLastError());
     return PDHG_OK;
   }
-  // planes out: 0 rho row 0 (current set), 1 phi_bar row T, 2 D = work row T-1, 3 X0
+  // planes out: 0 rho row 0 (current set), 1 phi_bar row T, 2 [D, S1] (2 spectral planes)
   int slab_plane_out(int which, void* dst) {
     const size_t npl = plane();
     switch (which) {
@@ -893,8 +894,7 @@ struct Impl : ImplBase {
         hipLaunchKernelGGL((k_copy_cur_rho<R>), dim3(1024), dim3(256), 0, stream, kp, (R*)dst, npl);
         break;
       case 1: HIP_TRY(hipMemcpyAsync(dst, kp.phibar + (size_t)pb.T * npl, npl * sizeof(R), hipMemcpyDeviceToDevice, stream)); break;
-      case 2: HIP_TRY(hipMemcpyAsync(dst, kp.work + (size_t)(pb.T - 1) * Mspec, Mspec * sizeof(R), hipMemcpyDeviceToDevice, stream)); break;
-      case 3: HIP_TRY(hipMemcpyAsync(dst, x0buf, Mspec * sizeof(R), hipMemcpyDeviceToDevice, stream)); break;
+      case 2: HIP_TRY(hipMemcpyAsync(dst, dsbuf, 2 * Mspec * sizeof(R), hipMemcpyDeviceToDevice, stream)); break;
       default: return fail(PDHG_ERR_ARG, "unknown plane %d", which);
     }
     HIP_TRY(hipGetLastError());
@@ -1341,27 +1341,23 @@ int pdhg_set_stream(pdhg_ctx* ctx, void* hip_stream) {   // null = the device's 
 int pdhg_slab_begin(pdhg_ctx* ctx) {
   return slab_dispatch(ctx, [&](auto& im) { return im.reset_ctrl(); });
 }
-int pdhg_slab_carry_gain(pdhg_ctx* ctx, void* G_out) {
-  if (!G_out) return fail(PDHG_ERR_ARG, "null G plane");
-  return slab_dispatch(ctx, [&](auto& im) { return im.slab_G(static_cast<float*>(G_out)); });
+int pdhg_slab_carry_gain(pdhg_ctx* ctx, void* GS_out) {
+  if (!GS_out) return fail(PDHG_ERR_ARG, "null plane");
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_G(static_cast<float*>(GS_out)); });
 }
 int pdhg_slab_forward(pdhg_ctx* ctx, double tau) {
   return slab_dispatch(ctx, [&](auto& im) { return im.slab_forward((float)tau); });
 }
-int pdhg_slab_fixup(pdhg_ctx* ctx, const void* all_D, const void* all_G, int rank) {
-  if (!all_D || !all_G) return fail(PDHG_ERR_ARG, "null carry planes");
-  return slab_dispatch(ctx, [&](auto& im) {
-    return im.slab_fixup(static_cast<const float*>(all_D), static_cast<const float*>(all_G), rank);
-  });
-}
-int pdhg_slab_backward(pdhg_ctx* ctx, double tau, const void* all_X0, const void* all_G, int rank, int nranks,
-                       double* sums) {
-  if (!all_X0 || !all_G || !sums) return fail(PDHG_ERR_ARG, "null argument");
+int pdhg_slab_fixup(pdhg_ctx* ctx, const void* all_DS, const void* all_GS, int rank, int nranks) {
+  if (!all_DS || !all_GS) return fail(PDHG_ERR_ARG, "null carry planes");
   if (rank < 0 || rank >= nranks) return fail(PDHG_ERR_ARG, "rank %d of %d", rank, nranks);
   return slab_dispatch(ctx, [&](auto& im) {
-    return im.slab_backward((float)tau, static_cast<const float*>(all_X0), static_cast<const float*>(all_G), rank,
-                            nranks, sums);
+    return im.slab_fixup(static_cast<const float*>(all_DS), static_cast<const float*>(all_GS), rank, nranks);
   });
+}
+int pdhg_slab_backward(pdhg_ctx* ctx, double tau, double* sums) {
+  if (!sums) return fail(PDHG_ERR_ARG, "null sums");
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_backward((float)tau, sums); });
 }
 int pdhg_slab_primal_finalize(pdhg_ctx* ctx, const double* sums) {
   if (!sums) return fail(PDHG_ERR_ARG, "null sums");

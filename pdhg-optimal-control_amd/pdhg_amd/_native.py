@@ -116,8 +116,8 @@ def load():
         "pdhg_slab_begin": ([P], ctypes.c_int),
         "pdhg_slab_carry_gain": ([P, P], ctypes.c_int),
         "pdhg_slab_forward": ([P, ctypes.c_double], ctypes.c_int),
-        "pdhg_slab_fixup": ([P, P, P, ctypes.c_int], ctypes.c_int),
-        "pdhg_slab_backward": ([P, ctypes.c_double, P, P, ctypes.c_int, ctypes.c_int, P], ctypes.c_int),
+        "pdhg_slab_fixup": ([P, P, P, ctypes.c_int, ctypes.c_int], ctypes.c_int),
+        "pdhg_slab_backward": ([P, ctypes.c_double, P], ctypes.c_int),
         "pdhg_slab_primal_finalize": ([P, P], ctypes.c_int),
         "pdhg_slab_dual": ([P, ctypes.c_double, ctypes.c_int, ctypes.c_int, P], ctypes.c_int),
         "pdhg_slab_dual_finalize": ([P, ctypes.c_double, ctypes.c_int, P], ctypes.c_int),

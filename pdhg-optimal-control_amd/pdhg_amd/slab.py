@@ -8,9 +8,10 @@ exchanges, over RCCL on xGMI:
 * halos, point to point: rho row j1 from the next slab (the continuity residual's rho_{j+1},
   update_fns_in_pdhg.py:83-96) and phi_bar row j0 from the previous slab (the dual's phi_bar_j,
   :150-165), one plane each;
-* the distributed t-solve of the H1 preconditioner (utils_precond.py:142-178): two allgathers of one
-  spectral plane per slab (the zero-carry forward outputs D, then the X0 values), each slab folding
-  the upstream / downstream carries itself (oracle/slab_oracle.py restates the algebra);
+* the distributed t-solve of the H1 preconditioner (utils_precond.py:142-178): ONE allgather per
+  iteration of two spectral planes per slab (D = the zero-carry forward sweep's last row, S1 =
+  sum P'_k b0_k); every slab folds the upstream carry and the downstream X0 values itself
+  (oracle/slab_oracle.py restates the algebra and pins it against the monolithic solve);
 * allreduces of the 16-double sum vectors behind every stop test (the err of
   update_dual_alternative, err1/err2 of utils_pdhg_solver.py:58-68), so every slab takes the same
   control decisions on its device.
@@ -26,7 +27,7 @@ import numpy as np
 from . import _native as N
 from .context import PDHGContext
 
-RHO_ROW0, PHIBAR_LAST, CARRY_D, CARRY_X0 = 0, 1, 2, 3    # pdhg_slab_plane_out
+RHO_ROW0, PHIBAR_LAST, CARRY_DS = 0, 1, 2               # pdhg_slab_plane_out
 RHO_HALO, PHIBAR_ROW0 = 0, 1                             # pdhg_slab_plane_in
 
 
@@ -74,18 +75,17 @@ class SlabContext(PDHGContext):
     def begin(self):
         N.check(self._lib.pdhg_slab_begin(self._h))
 
-    def carry_gain(self, G):
-        N.check(self._lib.pdhg_slab_carry_gain(self._h, _ptr(G)))
+    def carry_gain(self, GS):
+        N.check(self._lib.pdhg_slab_carry_gain(self._h, _ptr(GS)))
 
     def forward(self, tau):
         N.check(self._lib.pdhg_slab_forward(self._h, float(tau)))
 
-    def fixup(self, allD, allG):
-        N.check(self._lib.pdhg_slab_fixup(self._h, _ptr(allD), _ptr(allG), self.rank))
+    def fixup(self, allDS, allGS):
+        N.check(self._lib.pdhg_slab_fixup(self._h, _ptr(allDS), _ptr(allGS), self.rank, self.nranks))
 
-    def backward(self, tau, allX0, allG, sums):
-        N.check(self._lib.pdhg_slab_backward(self._h, float(tau), _ptr(allX0), _ptr(allG), self.rank, self.nranks,
-                                             _ptr(sums)))
+    def backward(self, tau, sums):
+        N.check(self._lib.pdhg_slab_backward(self._h, float(tau), _ptr(sums)))
 
     def primal_finalize(self, sums):
         N.check(self._lib.pdhg_slab_primal_finalize(self._h, _ptr(sums)))
@@ -226,11 +226,11 @@ class SlabRunner:
             s.set_stream(handle)
             self.b.append({k: torch.zeros(n, dtype=f32, device=dev) for k, n in
                            (("rho_send", sp), ("rho_recv", sp), ("pb_send", sp), ("pb_recv", sp),
-                            ("D", spec), ("X0", spec), ("G", spec))})
+                            ("DS", 2 * spec), ("GS", 2 * spec))})
             self.b[-1]["sums"] = torch.zeros(16, dtype=f64, device=dev)
         for s, b in zip(self.slabs, self.b):
-            s.carry_gain(b["G"])
-        self.allG = comm.allgather([b["G"] for b in self.b])   # iteration-invariant
+            s.carry_gain(b["GS"])
+        self.allGS = comm.allgather([b["GS"] for b in self.b])   # iteration-invariant
 
     def _each(self, name, *args):
         for s in self.slabs:
@@ -245,17 +245,14 @@ class SlabRunner:
         for s, b in zip(S, B):
             if not s.last:
                 s.plane_in(RHO_HALO, b["rho_recv"])
-        # primal: forward sweeps, carry scans, backward sweeps + update
+        # primal: zero-carry forward sweeps, ONE allgather of [D, S1], carry folds, backward sweeps + update
         self._each("forward", tau)
         for s, b in zip(S, B):
-            s.plane_out(CARRY_D, b["D"])
-        allD = C.allgather([b["D"] for b in B])
+            s.plane_out(CARRY_DS, b["DS"])
+        allDS = C.allgather([b["DS"] for b in B])
         for i, s in enumerate(S):
-            s.fixup(allD[i], self.allG[i])
-            s.plane_out(CARRY_X0, B[i]["X0"])
-        allX0 = C.allgather([b["X0"] for b in B])
-        for i, s in enumerate(S):
-            s.backward(tau, allX0[i], self.allG[i], B[i]["sums"])
+            s.fixup(allDS[i], self.allGS[i])
+            s.backward(tau, B[i]["sums"])
         C.allreduce([b["sums"] for b in B])
         for s, b in zip(S, B):
             s.primal_finalize(b["sums"])

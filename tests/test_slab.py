@@ -24,6 +24,17 @@ def test_thomas_slabs_equals_monolithic(T, P):
     assert np.allclose(out, ref, rtol=1e-11, atol=1e-12 * np.abs(ref).max())
 
 
+@pytest.mark.parametrize("T,P", [(5, 2), (7, 3), (8, 8), (40, 8)])
+def test_single_exchange_variant_equals_monolithic(T, P):
+    M = 11
+    ae = 1.0 / (0.05 ** 2)
+    diag = np.tile(1.0 + rng.uniform(0, 5e3, M) + 2 * ae, (T, 1))
+    diag[-1] -= ae
+    r = rng.standard_normal((T, M))
+    ref = S.monolithic_tridiag(diag, r, ae)
+    assert np.allclose(S.thomas_slabs_single(diag, r, ae, P), ref, rtol=1e-11, atol=1e-12 * np.abs(ref).max())
+
+
 def test_slab_bounds_cover_rows():
     for T in (1, 7, 200):
         for P in (1, 2, 3, 8):
