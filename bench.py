@@ -245,9 +245,11 @@ def main():
         ms, n = ctx.profile_query(cls)
         if n:
             kern[cls] = {"avg_ms": ms / n, "launches": n, "bytes_per_launch": ctx.algorithmic_bytes(k, cls)}
-    if world > 1 and "precond" in kern:   # t-slab: forward and backward sweeps are separate launches
-        kern["precond"]["launches"] //= 2
-        kern["precond"]["avg_ms"] *= 2
+    if world > 1:   # t-slab: sweeps and halo/interior row parts are separate launches -> per iteration
+        for cls, d in kern.items():
+            per = max(iters, 1) * (k if cls == "dual" else 1)
+            d["avg_ms"] = d["avg_ms"] * d["launches"] / per
+            d["launches"] = per
     ctx.profile_enable(False)
     dom = max(kern, key=lambda c: kern[c]["avg_ms"] * kern[c]["launches"])
     d = kern[dom]

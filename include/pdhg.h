@@ -156,11 +156,16 @@ int pdhg_algorithmic_bytes(pdhg_ctx* ctx, int k, const char* kernel_class, doubl
  * owns rows [j0, j0 + p->T) (its phi arrays hold p->T + 1 rows: row 0 is global phi row j0).  The
  * caller moves planes between slabs (RCCL; pdhg_amd/slab.py) and runs one outer iteration of
  * utils_pdhg_solver.py:51-88 as:
- *   plane_in(0, next slab's rho row 0) -> forward(tau) -> plane_out(2, [D, S1]) -> [allgather]
- *   -> fixup(allDS, allGS, rank, n) -> backward(tau, sums) -> [allreduce sums] -> primal_finalize(sums)
- *   -> plane_out(1, phi_bar row T) -> [to the next slab: plane_in(1, ...)]
- *   -> per dual sub-iteration s: dual(sigma, k, s, sums) -> [allreduce] -> dual_finalize(eps, s, sums)
- *   -> outer(k, sums) -> [allreduce when k > 1] -> outer_finalize(eps, k, sums).
+ *   plane_out(0, rho row 0) -> [to the previous slab] || residual(1)     (halo overlapped with interior rows)
+ *   -> plane_in(0, next slab's rho row 0) -> residual(2) -> forward(tau) -> plane_out(2, [D, S1])
+ *   -> [allgather] -> fixup(allDS, allGS, rank, n) -> backward(tau, sums) -> [allreduce sums]
+ *   -> primal_finalize(sums) -> plane_out(1, phi_bar row T) -> [to the next slab]
+ *      || dual(sigma, k, 0, sums, 1)                                        (halo overlapped with interior rows)
+ *   -> plane_in(1, previous slab's phi_bar row T) -> dual(sigma, k, 0, sums, 2) -> [allreduce]
+ *   -> dual_finalize(eps, 0, sums) -> per further sub-iteration s: dual(sigma, k, s, sums, 3) -> [allreduce]
+ *   -> dual_finalize(eps, s, sums) -> outer(k, sums) -> [allreduce when k > 1] -> outer_finalize(eps, k, sums).
+ * `parts` bit 0 = the rows that do not read a halo plane, bit 1 = the row that does (residual: the last
+ * row unless this is the window's last slab; dual: row 0 unless it is the first slab, then the sums).
  * The Thomas recurrences are affine in the carries entering a slab (oracle/slab_oracle.py): D = the
  * zero-carry forward sweep's last row, S1 = sum P'_k b0_k; allGS: every slab's [G, S2]
  * (pdhg_slab_carry_gain, iteration-invariant, gather once).  Planes are device pointers (float; D/S1 and
@@ -172,11 +177,12 @@ int pdhg_set_stream(pdhg_ctx* ctx, void* hip_stream);
 int pdhg_slab_plane_size(pdhg_ctx* ctx, unsigned long long* spatial, unsigned long long* spectral);
 int pdhg_slab_begin(pdhg_ctx* ctx);                                       /* reset the device loop control */
 int pdhg_slab_carry_gain(pdhg_ctx* ctx, void* GS_out);                    /* [G, S2], 2 spectral planes */
-int pdhg_slab_forward(pdhg_ctx* ctx, double tau);                          /* residual + x-DHT + forward sweep */
+int pdhg_slab_residual(pdhg_ctx* ctx, int parts);                          /* residual + y-DHT of rows */
+int pdhg_slab_forward(pdhg_ctx* ctx, double tau);                          /* x-DHT + forward sweep, [D, S1] */
 int pdhg_slab_fixup(pdhg_ctx* ctx, const void* all_DS, const void* all_GS, int rank, int nranks);
 int pdhg_slab_backward(pdhg_ctx* ctx, double tau, double* sums);           /* backward + inverse + update */
 int pdhg_slab_primal_finalize(pdhg_ctx* ctx, const double* sums);
-int pdhg_slab_dual(pdhg_ctx* ctx, double sigma, int rho_alp_iters, int sub, double* sums);
+int pdhg_slab_dual(pdhg_ctx* ctx, double sigma, int rho_alp_iters, int sub, double* sums, int parts);
 int pdhg_slab_dual_finalize(pdhg_ctx* ctx, double eps, int sub, const double* sums);
 int pdhg_slab_outer(pdhg_ctx* ctx, int rho_alp_iters, double* sums);
 int pdhg_slab_outer_finalize(pdhg_ctx* ctx, double eps, int rho_alp_iters, const double* sums);

@@ -45,19 +45,26 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const floa
   const int nx = p.nx, T = p.T;
   const int ngx = nx / RW;
   const int task = xcd_remap(blockIdx.x, gridDim.x);
+  // this launch covers time rows [row_base, row_base + row_cnt) (the t-slab path launches the rows
+  // that need the next slab's rho separately, so the halo exchange overlaps the others)
   int j, gx;
-  if (p.tile_j > 1) {
+  const int TJ = p.tile_j, ntiled = (p.row_cnt / TJ) * TJ * ngx;
+  if (TJ > 1 && task < ntiled) {
     // tiles of 4 row groups x TJ time rows: the ~32 tasks an XCD runs together share rho row j+1
-    // and the x-halo rows in that XCD's L2 (needs ngx % 4 == 0, T % TJ == 0; checked on the host)
-    const int TJ = p.tile_j, tsz = 4 * TJ, ngt = ngx >> 2;
+    // and the x-halo rows in that XCD's L2 (needs ngx % 4 == 0, checked on the host); the rows
+    // after the last whole tile fall back to the row-major order below
+    const int tsz = 4 * TJ, ngt = ngx >> 2;
     const int tile = task / tsz, w = task - tile * tsz;
     const int tjx = tile / ngt, tg = tile - tjx * ngt;
     j = tjx * TJ + (w >> 2);
     gx = tg * 4 + (w & 3);
   } else {
-    j = task / ngx;
-    gx = task - j * ngx;
+    const int t2 = task - (TJ > 1 ? ntiled : 0);
+    j = t2 / ngx;
+    gx = t2 - j * ngx;
+    if (TJ > 1) j += (p.row_cnt / TJ) * TJ;
   }
+  j += p.row_base;
   const int x0 = gx * RW;
   const size_t plane = (size_t)nx * N;
   const float* rj = p.rho[cur] + (size_t)j * plane;
@@ -819,7 +826,7 @@ __global__ void __launch_bounds__(512) k_precond_xt_ws_2d(KP<float> p, const flo
 // zeroed by a select), so nothing drains the load queue.  y neighbours come from the adjacent
 // lanes (DPP), the wave-edge ones from uniform loads.  Sums as in k_dual_2d (double per point).
 template <int EGNO>
-__global__ void __launch_bounds__(256) k_dual_fast_2d(KP<float> p, int jchunk) {
+__global__ void __launch_bounds__(256) k_dual_fast_2d(KP<float> p, int jchunk, int jbase, int jend, int zbase) {
   if (p.ctrl->done || p.ctrl->inner_done) return;
   constexpr int NA = (EGNO == 3) ? 2 : 4;
   constexpr int NS = 3 + 3 * NA;
@@ -830,8 +837,9 @@ __global__ void __launch_bounds__(256) k_dual_fast_2d(KP<float> p, int jchunk) {
   const size_t plane = (size_t)nx * ny;
   const int x = xcd_remap(blockIdx.x, gridDim.x);
   const int y = 4 * (blockIdx.y * blockDim.x + threadIdx.x);
-  const int j0 = blockIdx.z * jchunk;
-  const int j1 = min(p.T, j0 + jchunk);
+  // rows [jbase, jend) in chunks of jchunk (blockIdx.z); partials of this launch start at block row zbase
+  const int j0 = jbase + blockIdx.z * jchunk;
+  const int j1 = min(jend, j0 + jchunk);
   double s[NS];
 #pragma unroll
   for (int i = 0; i < NS; ++i) s[i] = 0.0;
@@ -914,7 +922,7 @@ __global__ void __launch_bounds__(256) k_dual_fast_2d(KP<float> p, int jchunk) {
       f0 = pc;
     }
   }
-  block_reduce_store<NS>(s, p.partials, ((int)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x);
+  block_reduce_store<NS>(s, p.partials, ((zbase + (int)blockIdx.z) * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x);
 }
 
 }  // namespace pdhg

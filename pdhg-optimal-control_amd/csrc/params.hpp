@@ -16,6 +16,7 @@ struct KP {
   int sub;                 // dual sub-iteration index of this launch
   int dbg;                 // timing experiments only (env PDHG_DBG); 0 in production
   int tile_j;              // residual task tiling: TJ time rows x 4 row groups per tile (1 = off)
+  int row_base, row_cnt;   // fast residual launch: time rows [row_base, row_base + row_cnt)
   R inv_dx, inv_dy, inv_dt, inv_dx2, inv_dy2;
   R epsl, c_over_dt;
   R ae;                    // Ct/dt^2 (1-D) or 1/dt^2 (2-D): off-diagonal magnitude of the t-Laplacian

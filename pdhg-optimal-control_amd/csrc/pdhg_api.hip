@@ -253,16 +253,11 @@ struct Impl : ImplBase {
         }
         if (nx % RWf == 0 && (RWf * B) % 4 == 0) {
           fast_rows = true;
-          p.tile_j = 1;
-          if ((nx / RWf) % 4 == 0)
-            for (int tj : {8, 4, 2})
-              if (T % tj == 0) {
-                p.tile_j = tj;
-                break;
-              }
-          if (const char* e = getenv("PDHG_TILE_J")) {   // tuning override (must divide T)
+          // residual task tiles of 8 time rows x 4 row groups (rows past the last whole tile run untiled)
+          p.tile_j = ((nx / RWf) % 4 == 0) ? 8 : 1;
+          if (const char* e = getenv("PDHG_TILE_J")) {   // tuning override
             const int v = atoi(e);
-            if (v >= 1 && T % v == 0 && (v == 1 || (nx / RWf) % 4 == 0)) p.tile_j = v;
+            if (v >= 1 && (v == 1 || (nx / RWf) % 4 == 0)) p.tile_j = v;
           }
           lds_fast = (size_t)(RWf / 2) * (ny + ny / 16) * sizeof(C);
           g_fast_upd = std::min((nx / RWf) * T, 2048);
@@ -287,12 +282,14 @@ struct Impl : ImplBase {
     }
     g_outer = 2048;
     partial_rows = std::max<size_t>(
-        {(size_t)gx4 * g4, (size_t)gx5 * g5, (size_t)g_outer, (size_t)g_fast_upd, (size_t)gxd * gyd * gzd, 1});
+        {(size_t)gx4 * g4, (size_t)gx5 * g5, (size_t)g_outer, (size_t)g_fast_upd, (size_t)gxd * gyd * (gzd + 1), 1});
     p.slab = slab ? 1 : 0;
     p.j0 = slab ? slab_j0 : 0;
     p.Tg = slab ? slab_Tg : T;
     p.last_slab = (p.j0 + T == p.Tg) ? 1 : 0;
     p.xt_phase = 0;
+    p.row_base = 0;
+    p.row_cnt = T;
     if (slab && !(is2d && fast_xt))
       return fail(PDHG_ERR_UNSUPPORTED, "t-slab decomposition needs ndim 2, fp32 and a power-of-two nx in "
                                         "[512, 4096] (fast x-transform kernels)");
@@ -514,6 +511,66 @@ struct Impl : ImplBase {
     }
   };
 
+  // residual + forward y transform over time rows [lo, hi) (2-D).  The generic kernels only run the
+  // whole window (lo = 0, hi = T).
+  int launch_residual(KP<R> p, int lo, int hi) {
+    if (hi <= lo) return PDHG_OK;
+    int rc = PDHG_OK;
+    if (fast_rows) {
+      ProfScope ps(this, "residual");
+      p.row_base = lo;
+      p.row_cnt = hi - lo;
+      rc = with_fast_rows([&](auto Nc, auto RWc, auto NTc) {
+        constexpr int N_ = decltype(Nc)::value, RW_ = decltype(RWc)::value, NT_ = decltype(NTc)::value;
+        const dim3 g((pb.nx / RW_) * (hi - lo));
+        int r2;
+        if constexpr (sizeof(R) == 4) {
+          switch (pb.egno) {
+            case 1:
+              if ((r2 = ensure_lds(k_res_fwdy_fast_2d<1, N_, RW_, NT_>, lds_fast))) return r2;
+              hipLaunchKernelGGL((k_res_fwdy_fast_2d<1, N_, RW_, NT_>), g, dim3(NT_), lds_fast, stream, p, twy);
+              break;
+            case 2:
+              if ((r2 = ensure_lds(k_res_fwdy_fast_2d<2, N_, RW_, NT_>, lds_fast))) return r2;
+              hipLaunchKernelGGL((k_res_fwdy_fast_2d<2, N_, RW_, NT_>), g, dim3(NT_), lds_fast, stream, p, twy);
+              break;
+            default:
+              if ((r2 = ensure_lds(k_res_fwdy_fast_2d<3, N_, RW_, NT_>, lds_fast))) return r2;
+              hipLaunchKernelGGL((k_res_fwdy_fast_2d<3, N_, RW_, NT_>), g, dim3(NT_), lds_fast, stream, p, twy);
+              break;
+          }
+        }
+        return (int)PDHG_OK;
+      });
+    } else {
+      if (lo != 0 || hi != pb.T) return fail(PDHG_ERR_UNSUPPORTED, "row-range residual needs the fast row kernels");
+      ProfScope ps(this, "residual");
+      dim3 g(gx1);
+      rc = with_line_fft(ply, [&](auto f) {
+        using F = decltype(f);
+        int r2;
+        switch (pb.egno) {
+          case 1:
+            if ((r2 = ensure_lds(k_res_fwdy_2d<R, 1, F>, lds_res))) return r2;
+            hipLaunchKernelGGL((k_res_fwdy_2d<R, 1, F>), g, dim3(256), lds_res, stream, p, f, twy);
+            break;
+          case 2:
+            if ((r2 = ensure_lds(k_res_fwdy_2d<R, 2, F>, lds_res))) return r2;
+            hipLaunchKernelGGL((k_res_fwdy_2d<R, 2, F>), g, dim3(256), lds_res, stream, p, f, twy);
+            break;
+          default:
+            if ((r2 = ensure_lds(k_res_fwdy_2d<R, 3, F>, lds_res))) return r2;
+            hipLaunchKernelGGL((k_res_fwdy_2d<R, 3, F>), g, dim3(256), lds_res, stream, p, f, twy);
+            break;
+        }
+        return (int)PDHG_OK;
+      });
+    }
+    if (rc) return rc;
+    HIP_TRY(hipGetLastError());
+    return PDHG_OK;
+  }
+
   // ---------------- launches ----------------
   // stages: 1 residual (+ forward y transform), 2 x transform + Thomas (sweeps per xt_phase: 0 both,
   // 1 forward, 2 backward), 4 inverse transforms + phi/phi_bar update + primal sums.  sums_out != null
@@ -525,56 +582,8 @@ struct Impl : ImplBase {
     const int T = pb.T;
     if (pb.ndim == 2) {
       int rc = PDHG_OK;
-      if (!(stages & 1)) {
-      } else if (fast_rows) {
-        ProfScope ps(this, "residual");
-        rc = with_fast_rows([&](auto Nc, auto RWc, auto NTc) {
-          constexpr int N_ = decltype(Nc)::value, RW_ = decltype(RWc)::value, NT_ = decltype(NTc)::value;
-          const dim3 g((pb.nx / RW_) * T);
-          int r2;
-          if constexpr (sizeof(R) == 4) {
-            switch (pb.egno) {
-              case 1:
-                if ((r2 = ensure_lds(k_res_fwdy_fast_2d<1, N_, RW_, NT_>, lds_fast))) return r2;
-                hipLaunchKernelGGL((k_res_fwdy_fast_2d<1, N_, RW_, NT_>), g, dim3(NT_), lds_fast, stream, p, twy);
-                break;
-              case 2:
-                if ((r2 = ensure_lds(k_res_fwdy_fast_2d<2, N_, RW_, NT_>, lds_fast))) return r2;
-                hipLaunchKernelGGL((k_res_fwdy_fast_2d<2, N_, RW_, NT_>), g, dim3(NT_), lds_fast, stream, p, twy);
-                break;
-              default:
-                if ((r2 = ensure_lds(k_res_fwdy_fast_2d<3, N_, RW_, NT_>, lds_fast))) return r2;
-                hipLaunchKernelGGL((k_res_fwdy_fast_2d<3, N_, RW_, NT_>), g, dim3(NT_), lds_fast, stream, p, twy);
-                break;
-            }
-          }
-          return (int)PDHG_OK;
-        });
-        if (rc) return rc;
-      } else {
-        ProfScope ps(this, "residual");
-        dim3 g(gx1);
-        rc = with_line_fft(ply, [&](auto f) {
-          using F = decltype(f);
-          int r2;
-          switch (pb.egno) {
-            case 1:
-              if ((r2 = ensure_lds(k_res_fwdy_2d<R, 1, F>, lds_res))) return r2;
-              hipLaunchKernelGGL((k_res_fwdy_2d<R, 1, F>), g, dim3(256), lds_res, stream, p, f, twy);
-              break;
-            case 2:
-              if ((r2 = ensure_lds(k_res_fwdy_2d<R, 2, F>, lds_res))) return r2;
-              hipLaunchKernelGGL((k_res_fwdy_2d<R, 2, F>), g, dim3(256), lds_res, stream, p, f, twy);
-              break;
-            default:
-              if ((r2 = ensure_lds(k_res_fwdy_2d<R, 3, F>, lds_res))) return r2;
-              hipLaunchKernelGGL((k_res_fwdy_2d<R, 3, F>), g, dim3(256), lds_res, stream, p, f, twy);
-              break;
-          }
-          return (int)PDHG_OK;
-        });
-        if (rc) return rc;
-      }
+      if (stages & 1)
+        if ((rc = launch_residual(p, 0, T))) return rc;
       if (!(stages & 2)) {
       } else if (fast_xt) {
         ProfScope ps(this, "precond");
@@ -692,15 +701,20 @@ struct Impl : ImplBase {
     return PDHG_OK;
   }
 
+  // fast dual over time rows [lo, hi); its partials start at block row zbase.  Returns the z extent.
   template <int EGNO>
-  void launch_dual_fast_e(const KP<R>& p) {
+  void launch_dual_fast_e(const KP<R>& p, int lo, int hi, int gz, int zbase) {
     if constexpr (std::is_same<R, float>::value)
-      hipLaunchKernelGGL((k_dual_fast_2d<EGNO>), dim3(gxd, gyd, gzd), dim3(NTd), 0, stream, p, jchunk_d);
+      hipLaunchKernelGGL((k_dual_fast_2d<EGNO>), dim3(gxd, gyd, gz), dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase);
   }
-  void launch_dual_fast(const KP<R>& p) {
-    if (pb.egno == 1) launch_dual_fast_e<1>(p);
-    else if (pb.egno == 2) launch_dual_fast_e<2>(p);
-    else launch_dual_fast_e<3>(p);
+  int launch_dual_fast(const KP<R>& p, int lo = 0, int hi = -1, int zbase = 0) {
+    if (hi < 0) hi = pb.T;
+    if (hi <= lo) return 0;
+    const int gz = (hi - lo + jchunk_d - 1) / jchunk_d;
+    if (pb.egno == 1) launch_dual_fast_e<1>(p, lo, hi, gz, zbase);
+    else if (pb.egno == 2) launch_dual_fast_e<2>(p, lo, hi, gz, zbase);
+    else launch_dual_fast_e<3>(p, lo, hi, gz, zbase);
+    return gz;
   }
 
   int launch_dual(R sigma, double eps, int k) {
@@ -813,18 +827,28 @@ struct Impl : ImplBase {
   }
 
   // ---------------- t-slab phases (multi-GPU; the caller moves planes between slabs) ----------------
-  // One outer iteration of a slab = slab_forward -> [allgather D] -> slab_fixup -> [allgather X0] ->
-  // slab_backward -> [allreduce sums] -> slab_primal_finalize -> [phi_bar / rho halos] ->
-  // per dual sub-iteration: slab_dual -> [allreduce] -> slab_dual_finalize -> slab_outer ->
-  // [allreduce] -> slab_outer_finalize.  With one slab this is exactly iterate().
+  // One outer iteration of a slab (include/pdhg.h): slab_residual(rows without the rho halo) ||
+  // [rho halo] -> slab_residual(the halo row) -> slab_forward -> [allgather D, S1] -> slab_fixup ->
+  // slab_backward -> [allreduce sums] -> slab_primal_finalize -> slab_dual(rows without the phi_bar
+  // halo) || [phi_bar halo] -> slab_dual(the halo row + sums) -> [allreduce] -> slab_dual_finalize ->
+  // ... -> slab_outer -> [allreduce] -> slab_outer_finalize.  With one slab this is iterate().
   int need_slab() const { return slab ? PDHG_OK : fail(PDHG_ERR_STATE, "not a t-slab context"); }
   int slab_G(R* out) {   // [G, S2] (iteration-invariant)
     hipLaunchKernelGGL((k_slab_sums<R>), dim3((unsigned)((Mspec + 255) / 256)), dim3(256), 0, stream, kp, 0, out);
     HIP_TRY(hipGetLastError());
     return PDHG_OK;
   }
-  int slab_forward(R tau) {   // residual + zero-carry forward sweep + this slab's [D, S1]
-    int rc = launch_primal(tau, 1 | 2, 1);
+  // residual rows: parts bit 0 = the rows that do not read the rho halo, bit 1 = the row that does
+  // (the last row, unless this is the window's last slab)
+  int slab_residual(int parts) {
+    const int T = pb.T, split = (fast_rows && !kp.last_slab) ? T - 1 : (fast_rows ? T : 0);
+    int rc;
+    if ((parts & 1) && (rc = launch_residual(kp, 0, split))) return rc;
+    if ((parts & 2) && (rc = launch_residual(kp, split, T))) return rc;
+    return PDHG_OK;
+  }
+  int slab_forward(R tau) {   // zero-carry forward sweep + this slab's [D, S1] (after both residual parts)
+    int rc = launch_primal(tau, 2, 1);
     if (rc) return rc;
     hipLaunchKernelGGL((k_slab_sums<R>), dim3((unsigned)((Mspec + 255) / 256)), dim3(256), 0, stream, kp, 1, dsbuf);
     HIP_TRY(hipGetLastError());
@@ -842,27 +866,42 @@ struct Impl : ImplBase {
     HIP_TRY(hipGetLastError());
     return PDHG_OK;
   }
-  int slab_dual(R sigma, int k, int sub, double* sums) {
+  // dual rows: parts bit 0 = the rows that do not read the phi_bar halo, bit 1 = the row that does
+  // (row 0, unless this is the window's first slab) followed by the sum reduction into `sums`
+  int slab_dual(R sigma, int k, int sub, double* sums, int parts) {
     KP<R> p = kp;
     p.sigma = sigma;
     p.inplace = (k <= 1) ? 1 : 0;
     p.sub = sub;
     if (!p.inplace && !two_sets)
       return fail(PDHG_ERR_STATE, "rho_alp_iters=%d needs a context created with rho_alp_iters > 1", k);
-    {
+    const int T = pb.T, split = fast_dual ? (kp.j0 > 0 ? 1 : 0) : T;   // halo rows [0, split)
+    const int gz_in = fast_dual ? (T - split + jchunk_d - 1) / jchunk_d : 0;
+    if ((parts & 1) && fast_dual) {
       ProfScope ps(this, "dual");
-      if (pb.ndim == 2 && fast_dual) {
-        launch_dual_fast(p);
-      } else {
-        dim3 g(gx5, g5);
-        switch (pb.egno) {
-          case 1: hipLaunchKernelGGL((k_dual_2d<R, 1>), g, dim3(256), 0, stream, p); break;
-          case 2: hipLaunchKernelGGL((k_dual_2d<R, 2>), g, dim3(256), 0, stream, p); break;
-          default: hipLaunchKernelGGL((k_dual_2d<R, 3>), g, dim3(256), 0, stream, p); break;
-        }
-      }
+      launch_dual_fast(p, split, T, 0);
     }
-    const int nrows_d = fast_dual ? gxd * gyd * gzd : gx5 * g5;
+    if (!(parts & 2)) {
+      HIP_TRY(hipGetLastError());
+      return PDHG_OK;
+    }
+    int nrows_d;
+    if (fast_dual) {
+      if (split > 0) {
+        ProfScope ps(this, "dual");
+        launch_dual_fast(p, 0, split, gz_in);
+      }
+      nrows_d = gxd * gyd * (gz_in + (split > 0 ? 1 : 0));
+    } else {
+      ProfScope ps(this, "dual");
+      dim3 g(gx5, g5);
+      switch (pb.egno) {
+        case 1: hipLaunchKernelGGL((k_dual_2d<R, 1>), g, dim3(256), 0, stream, p); break;
+        case 2: hipLaunchKernelGGL((k_dual_2d<R, 2>), g, dim3(256), 0, stream, p); break;
+        default: hipLaunchKernelGGL((k_dual_2d<R, 3>), g, dim3(256), 0, stream, p); break;
+      }
+      nrows_d = gx5 * g5;
+    }
     hipLaunchKernelGGL(k_reduce_vec, dim3(1), dim3(256), 0, stream, p.partials, nrows_d, 3 + 3 * na, 0.0, sums);
     HIP_TRY(hipGetLastError());
     return PDHG_OK;
@@ -1345,6 +1384,9 @@ int pdhg_slab_carry_gain(pdhg_ctx* ctx, void* GS_out) {
   if (!GS_out) return fail(PDHG_ERR_ARG, "null plane");
   return slab_dispatch(ctx, [&](auto& im) { return im.slab_G(static_cast<float*>(GS_out)); });
 }
+int pdhg_slab_residual(pdhg_ctx* ctx, int parts) {
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_residual(parts); });
+}
 int pdhg_slab_forward(pdhg_ctx* ctx, double tau) {
   return slab_dispatch(ctx, [&](auto& im) { return im.slab_forward((float)tau); });
 }
@@ -1363,9 +1405,9 @@ int pdhg_slab_primal_finalize(pdhg_ctx* ctx, const double* sums) {
   if (!sums) return fail(PDHG_ERR_ARG, "null sums");
   return slab_dispatch(ctx, [&](auto& im) { return im.slab_primal_finalize(sums); });
 }
-int pdhg_slab_dual(pdhg_ctx* ctx, double sigma, int rho_alp_iters, int sub, double* sums) {
+int pdhg_slab_dual(pdhg_ctx* ctx, double sigma, int rho_alp_iters, int sub, double* sums, int parts) {
   if (!sums) return fail(PDHG_ERR_ARG, "null sums");
-  return slab_dispatch(ctx, [&](auto& im) { return im.slab_dual((float)sigma, rho_alp_iters, sub, sums); });
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_dual((float)sigma, rho_alp_iters, sub, sums, parts); });
 }
 int pdhg_slab_dual_finalize(pdhg_ctx* ctx, double eps, int sub, const double* sums) {
   if (!sums) return fail(PDHG_ERR_ARG, "null sums");

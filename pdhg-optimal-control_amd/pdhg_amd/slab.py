@@ -7,7 +7,8 @@ exchanges, over RCCL on xGMI:
 
 * halos, point to point: rho row j1 from the next slab (the continuity residual's rho_{j+1},
   update_fns_in_pdhg.py:83-96) and phi_bar row j0 from the previous slab (the dual's phi_bar_j,
-  :150-165), one plane each;
+  :150-165), one plane each, moved on a second stream (over RCCL: on a communicator of their own)
+  while the rows that do not read the halo are computed;
 * the distributed t-solve of the H1 preconditioner (utils_precond.py:142-178): ONE allgather per
   iteration of two spectral planes per slab (D = the zero-carry forward sweep's last row, S1 =
   sum P'_k b0_k); every slab folds the upstream carry and the downstream X0 values itself
@@ -29,6 +30,7 @@ from .context import PDHGContext
 
 RHO_ROW0, PHIBAR_LAST, CARRY_DS = 0, 1, 2               # pdhg_slab_plane_out
 RHO_HALO, PHIBAR_ROW0 = 0, 1                             # pdhg_slab_plane_in
+INTERIOR, EDGE = 1, 2                                    # pdhg_slab_residual / pdhg_slab_dual parts
 
 
 def slab_bounds(T, P):
@@ -78,6 +80,9 @@ class SlabContext(PDHGContext):
     def carry_gain(self, GS):
         N.check(self._lib.pdhg_slab_carry_gain(self._h, _ptr(GS)))
 
+    def residual(self, parts=INTERIOR | EDGE):
+        N.check(self._lib.pdhg_slab_residual(self._h, int(parts)))
+
     def forward(self, tau):
         N.check(self._lib.pdhg_slab_forward(self._h, float(tau)))
 
@@ -90,8 +95,8 @@ class SlabContext(PDHGContext):
     def primal_finalize(self, sums):
         N.check(self._lib.pdhg_slab_primal_finalize(self._h, _ptr(sums)))
 
-    def dual(self, sigma, k, sub, sums):
-        N.check(self._lib.pdhg_slab_dual(self._h, float(sigma), int(k), int(sub), _ptr(sums)))
+    def dual(self, sigma, k, sub, sums, parts=INTERIOR | EDGE):
+        N.check(self._lib.pdhg_slab_dual(self._h, float(sigma), int(k), int(sub), _ptr(sums), int(parts)))
 
     def dual_finalize(self, eps, sub, sums):
         N.check(self._lib.pdhg_slab_dual_finalize(self._h, float(eps), int(sub), _ptr(sums)))
@@ -160,6 +165,10 @@ class DistComm:
         self.nranks = dist.get_world_size()
         self.ranks = [self.rank]
         self.gloo = dist.get_backend() == "gloo"
+        # the halo shifts get a communicator of their own: on one communicator RCCL runs operations in
+        # issue order, so the sums all-reduce issued behind a halo would wait for it and stall the
+        # main stream -- on a second one the halo overlaps the kernels and the small collectives
+        self.halo_group = dist.new_group(list(range(self.nranks))) if self.nranks > 1 else None
 
     # gloo moves host memory: device tensors are staged through the host (functional rehearsal of the
     # multi-rank path; the GPU runs use RCCL on device buffers directly)
@@ -190,9 +199,9 @@ class DistComm:
         r_buf = recv[0].cpu() if stage else recv[0]
         ops = []
         if 0 <= dst < self.nranks:
-            ops.append(self.dist.P2POp(self.dist.isend, s_buf, dst))
+            ops.append(self.dist.P2POp(self.dist.isend, s_buf, dst, group=self.halo_group))
         if 0 <= src < self.nranks:
-            ops.append(self.dist.P2POp(self.dist.irecv, r_buf, src))
+            ops.append(self.dist.P2POp(self.dist.irecv, r_buf, src, group=self.halo_group))
         if ops:
             for w in self.dist.batch_isend_irecv(ops):
                 w.wait()
@@ -213,10 +222,11 @@ class SlabRunner:
     """Drives the slabs of this process through outer iterations (pdhg_iterate's loop, split at
     every point where slabs exchange data)."""
 
-    def __init__(self, slabs, comm):
+    def __init__(self, slabs, comm, overlap=True):
         import torch
         self.torch = torch
         self.slabs, self.comm = list(slabs), comm
+        self.side = torch.cuda.Stream() if overlap else None   # halo stream
         dev = torch.device("cuda", torch.cuda.current_device())
         sp, spec = self.slabs[0].plane_sizes()
         f32, f64 = torch.float32, torch.float64
@@ -236,15 +246,35 @@ class SlabRunner:
         for s in self.slabs:
             getattr(s, name)(*args)
 
+    def _halo(self, shift, send, recv):
+        """Run a halo shift on the side stream after everything enqueued so far on the main stream;
+        returns at once (join with _join before the halo plane is used)."""
+        torch = self.torch
+        if self.side is None:
+            shift(send, recv)
+            return
+        self.side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.side):
+            shift(send, recv)
+
+    def _join(self):
+        if self.side is not None:
+            self.torch.cuda.current_stream().wait_stream(self.side)
+
     def step(self, tau, sigma, eps, k):
         S, B, C = self.slabs, self.b, self.comm
-        # halo: rho row 0 of slab r+1 -> slab r (the residual's rho_{j+1} on its last row)
+        # rho halo (row 0 of slab r+1 -> slab r: the residual's rho_{j+1} on its last row), overlapped
+        # with the residual of the rows that do not read it
         for s, b in zip(S, B):
             s.plane_out(RHO_ROW0, b["rho_send"])
-        C.shift_up([b["rho_send"] for b in B], [b["rho_recv"] for b in B])
+        self._halo(C.shift_up, [b["rho_send"] for b in B], [b["rho_recv"] for b in B])
+        for s in S:
+            s.residual(INTERIOR)
+        self._join()
         for s, b in zip(S, B):
             if not s.last:
                 s.plane_in(RHO_HALO, b["rho_recv"])
+            s.residual(EDGE)
         # primal: zero-carry forward sweeps, ONE allgather of [D, S1], carry folds, backward sweeps + update
         self._each("forward", tau)
         for s, b in zip(S, B):
@@ -253,20 +283,24 @@ class SlabRunner:
         for i, s in enumerate(S):
             s.fixup(allDS[i], self.allGS[i])
             s.backward(tau, B[i]["sums"])
+        # phi_bar halo (row T of slab r -> row 0 of slab r+1: the dual's phi_bar_j), overlapped with the
+        # primal sums all-reduce and the dual of the rows that do not read it
+        for s, b in zip(S, B):
+            s.plane_out(PHIBAR_LAST, b["pb_send"])
+        self._halo(C.shift_down, [b["pb_send"] for b in B], [b["pb_recv"] for b in B])
         C.allreduce([b["sums"] for b in B])
         for s, b in zip(S, B):
             s.primal_finalize(b["sums"])
-        # halo: phi_bar row T of slab r -> phi_bar row 0 of slab r+1 (the dual's phi_bar_j)
-        for s, b in zip(S, B):
-            s.plane_out(PHIBAR_LAST, b["pb_send"])
-        C.shift_down([b["pb_send"] for b in B], [b["pb_recv"] for b in B])
-        for s, b in zip(S, B):
-            if s.rank > 0:
-                s.plane_in(PHIBAR_ROW0, b["pb_recv"])
         # dual sub-iterations (device-side early exit once the global inner error is below eps)
         for sub in range(k):
             for s, b in zip(S, B):
-                s.dual(sigma, k, sub, b["sums"])
+                s.dual(sigma, k, sub, b["sums"], INTERIOR if sub == 0 else INTERIOR | EDGE)
+            if sub == 0:
+                self._join()
+                for s, b in zip(S, B):
+                    if s.rank > 0:
+                        s.plane_in(PHIBAR_ROW0, b["pb_recv"])
+                    s.dual(sigma, k, sub, b["sums"], EDGE)
             C.allreduce([b["sums"] for b in B])
             for s, b in zip(S, B):
                 s.dual_finalize(eps, sub, b["sums"])

@@ -17,6 +17,8 @@ CASES = [
     (2, 4096, 256, 6, 2, 1),
     (1, 4096, 256, 4, 3, 2),
     (2, 8192, 256, 5, 2, 1),    # half-real x blocks (C4's nx)
+    (1, 512, 256, 3, 3, 1),     # one-row slabs: the halo row is the whole slab
+    (2, 512, 256, 19, 2, 1),    # residual tiles of 8 rows + untiled remainder rows
 ]
 
 
@@ -26,9 +28,10 @@ def _slabs(P, nranks, k):
                         epsl=P["epsl"], rho_alp_iters=k) for r in range(nranks)]
 
 
+@pytest.mark.parametrize("overlap", [True, False], ids=["overlap", "serial"])
 @pytest.mark.parametrize("egno,nx,ny,T,nr,k", CASES, ids=[f"e{c[0]}_{c[1]}x{c[2]}_T{c[3]}_P{c[4]}_k{c[5]}"
                                                          for c in CASES])
-def test_slabs_match_single_context(native, egno, nx, ny, T, nr, k):
+def test_slabs_match_single_context(native, egno, nx, ny, T, nr, k, overlap):
     import torch
     from pdhg_amd.context import PDHGContext
     from pdhg_amd.slab import LocalComm, SlabRunner, join_state, slab_bounds, split_state
@@ -43,7 +46,7 @@ def test_slabs_match_single_context(native, egno, nx, ny, T, nr, k):
     slabs = _slabs(P, nr, k)
     for s, part in zip(slabs, split_state(P["phi"], P["rho"], P["alp"], slab_bounds(T, nr))):
         s.set_state(*part)
-    runner = SlabRunner(slabs, LocalComm(nr))
+    runner = SlabRunner(slabs, LocalComm(nr), overlap=overlap)
     st = runner.iterate(n, tau, sigma, -1.0, k)
     torch.cuda.synchronize()
     phi_s, rho_s, alp_s = join_state([s.get_state() for s in slabs])
