@@ -198,7 +198,7 @@ def main():
 
     if world > 1:
         import torch
-        runner = SlabRunner([ctx], DistComm())
+        runner = SlabRunner([ctx], DistComm(), exchange=os.environ.get("PDHG_SLAB_EXCHANGE", "neighbour"))
 
         def run(n):
             s = runner.iterate(n, tau, sigma, eps, k)
@@ -276,9 +276,11 @@ def main():
         "data": "synthetic (reference initial state phi=g, rho=70, alp=0)",
         "config": {"workload": "egno{} ndim{} epsl{} nx={} ny={} nt={}: one PDHG window of T={} rows, "
                                "rho_alp_iters={}".format(egno, ndim, epsl, nx, ny, nt, T, k),
-                   "parallelism": "t-slab x{} (RCCL halos + carry allgathers)".format(world) if world > 1
+                   "parallelism": "t-slab x{} (RCCL point-to-point halos and carries, overlapped)".format(world) if world > 1
                    else "single GPU",
                    "iters_executed": iters, "stop_status": st["status"], "state_nonfinite": bool(st["nan_seen"])},
+        **({"slab_exchange": {"carries": runner.exchange, "long_range_modes": runner.n_long,
+                              "halo_overlap": runner.side is not None}} if runner is not None else {}),
         "hbm_gbps_iteration": it_bytes / (ms_per_step * 1e-3) / 1e9,
         "iteration_bytes": it_bytes,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",

@@ -164,6 +164,12 @@ int pdhg_algorithmic_bytes(pdhg_ctx* ctx, int k, const char* kernel_class, doubl
  *   -> plane_in(1, previous slab's phi_bar row T) -> dual(sigma, k, 0, sums, 2) -> [allreduce]
  *   -> dual_finalize(eps, 0, sums) -> per further sub-iteration s: dual(sigma, k, s, sums, 3) -> [allreduce]
  *   -> dual_finalize(eps, s, sums) -> outer(k, sums) -> [allreduce when k > 1] -> outer_finalize(eps, k, sums).
+ * Neighbour-exchange form (pdhg_amd.slab default): instead of the allgather of full [D, S1] planes,
+ * classify the modes once (pdhg_slab_long_modes: long-range where some slab's gain G >= delta, a few
+ * thousand low frequencies), then per iteration send D to the next slab and S1 to the previous one
+ * (point to point), allgather only plane_out(3) = [D, S1] of the long-range modes, and call
+ * fixup_nb(D from the previous slab, S1 from the next, allLong, allGS, rank, n).  The terms dropped for
+ * the other modes are below delta relative (oracle/slab_oracle.py thomas_slabs_neighbour).
  * `parts` bit 0 = the rows that do not read a halo plane, bit 1 = the row that does (residual: the last
  * row unless this is the window's last slab; dual: row 0 unless it is the first slab, then the sums).
  * The Thomas recurrences are affine in the carries entering a slab (oracle/slab_oracle.py): D = the
@@ -180,13 +186,17 @@ int pdhg_slab_carry_gain(pdhg_ctx* ctx, void* GS_out);                    /* [G,
 int pdhg_slab_residual(pdhg_ctx* ctx, int parts);                          /* residual + y-DHT of rows */
 int pdhg_slab_forward(pdhg_ctx* ctx, double tau);                          /* x-DHT + forward sweep, [D, S1] */
 int pdhg_slab_fixup(pdhg_ctx* ctx, const void* all_DS, const void* all_GS, int rank, int nranks);
+int pdhg_slab_long_modes(pdhg_ctx* ctx, const void* all_GS, int nranks, double delta, int* K);
+int pdhg_slab_fixup_nb(pdhg_ctx* ctx, const void* D_left, const void* S1_right, const void* all_long,
+                       const void* all_GS, int rank, int nranks);
 int pdhg_slab_backward(pdhg_ctx* ctx, double tau, double* sums);           /* backward + inverse + update */
 int pdhg_slab_primal_finalize(pdhg_ctx* ctx, const double* sums);
 int pdhg_slab_dual(pdhg_ctx* ctx, double sigma, int rho_alp_iters, int sub, double* sums, int parts);
 int pdhg_slab_dual_finalize(pdhg_ctx* ctx, double eps, int sub, const double* sums);
 int pdhg_slab_outer(pdhg_ctx* ctx, int rho_alp_iters, double* sums);
 int pdhg_slab_outer_finalize(pdhg_ctx* ctx, double eps, int rho_alp_iters, const double* sums);
-int pdhg_slab_plane_out(pdhg_ctx* ctx, int which, void* dst); /* 0 rho row 0, 1 phi_bar row T, 2 [D, S1] */
+int pdhg_slab_plane_out(pdhg_ctx* ctx, int which, void* dst); /* 0 rho row 0, 1 phi_bar row T, 2 [D, S1],
+                                                                 3 [D, S1] of the long-range modes */
 int pdhg_slab_plane_in(pdhg_ctx* ctx, int which, const void* src); /* 0 rho halo, 1 phi_bar row 0 */
 int pdhg_slab_status(pdhg_ctx* ctx, pdhg_stats* st);
 

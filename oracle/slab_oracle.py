@@ -172,3 +172,42 @@ def thomas_slabs_single(diag, r, ae, P):
         b, _ = fixup(fw[q][0], g, j0, c)
         out.append(local_backward(b, g, j0, y))
     return np.concatenate(out, axis=0)
+
+
+# ---- neighbour-exchange variant: only the long-range modes need every slab's planes ---------------
+#   G_q = prod g over slab q depends only on the mode; where G_q < delta for every slab the far terms
+#   G_{q-1} c_in(q-1) and G_{q+1} y_{q+1} are below delta relative, so
+#     c_in(q) = D_{q-1},   y_q = S1_{q+1} + (D_q + G_q c_in(q)) S2_{q+1}
+#   (kernels_common.hpp k_slab_fix_nb); the other ("long-range") modes fold exactly.
+
+def long_range_mask(G, delta):
+    """Modes where some slab's gain reaches delta (they take the exact all-slab folds)."""
+    return ~(np.max(np.abs(np.stack(G)), axis=0) < delta)
+
+
+def carries_neighbour(D, S1, G, S2, q, long_mask):
+    P = len(D)
+    c = D[q - 1] if q > 0 else np.zeros_like(D[0])
+    if q + 1 < P:
+        y = S1[q + 1] + (D[q] + G[q] * c) * S2[q + 1]
+    else:
+        y = np.zeros_like(D[0])
+    ce, ye = carries_single(D, S1, G, S2, q)
+    return np.where(long_mask, ce, c), np.where(long_mask, ye, y)
+
+
+def thomas_slabs_neighbour(diag, r, ae, P, delta=2.0 ** -40):
+    T = diag.shape[0]
+    bounds = slab_bounds(T, P)
+    g = pivots(diag, ae)
+    fw = [local_forward(r, g, ae, j0, j1) for (j0, j1) in bounds]
+    ss = [s_sums(fw[q][0], g, bounds[q][0]) for q in range(P)]
+    D, G = [f[1] for f in fw], [f[2] for f in fw]
+    S1, S2 = [s[0] for s in ss], [s[1] for s in ss]
+    mask = long_range_mask(G, delta)
+    out = []
+    for q, (j0, j1) in enumerate(bounds):
+        c, y = carries_neighbour(D, S1, G, S2, q, mask)
+        b, _ = fixup(fw[q][0], g, j0, c)
+        out.append(local_backward(b, g, j0, y))
+    return np.concatenate(out, axis=0), mask

@@ -247,6 +247,79 @@ __global__ void __launch_bounds__(256) k_slab_fix(KP<R> p, const R* __restrict__
   }
 }
 
+// Neighbour-exchange variant of k_slab_fix.  The gain G_q = prod g over slab q's rows depends only on
+// the mode and the slab length; where every slab's G_q < delta (pos[m] < 0: "short-range" modes, all
+// but a few thousand low frequencies) the far terms G_{q-1} c_in(q-1) and G_{q+1} y_{q+1} are below
+// delta relative and
+//   c_in(rank) = D_{rank-1},   y = X0_{rank+1} = S1_{rank+1} + (D_rank + G_rank c_in(rank)) S2_{rank+1},
+// so only the neighbours' D (from the left) and S1 (from the right) are needed.  The long-range modes
+// (pos[m] = their index in the compact list of K) fold exactly as k_slab_fix from everybody's compact
+// [D, S1] (allLong[q] = [D_q(K), S1_q(K)]).  oracle/slab_oracle.py: thomas_slabs_neighbour.
+template <typename R>
+__global__ void __launch_bounds__(256) k_slab_fix_nb(KP<R> p, const R* __restrict__ ownDS, const R* __restrict__ D_left,
+                                                     const R* __restrict__ S1_right, const R* __restrict__ allLong,
+                                                     const int* __restrict__ pos, int K, const R* __restrict__ allGS,
+                                                     int rank, int nranks, R* __restrict__ carry_y) {
+  if (p.ctrl->done) return;
+  const size_t M = (size_t)p.nb * p.nx * p.B;
+  const size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  double c_own = 0.0, y = 0.0;
+  const int q = pos[m];
+  if (q >= 0) {
+    double c = 0.0, W = 1.0;
+    for (int s = 0; s < nranks; ++s) {
+      const R* L = allLong + (size_t)s * 2 * K;
+      const size_t o = (size_t)s * 2 * M + m;
+      if (s == rank) c_own = c;
+      if (s > rank) {
+        y += W * ((double)L[K + q] + c * (double)allGS[o + M]);
+        W *= (double)allGS[o];
+      }
+      c = (double)L[q] + (double)allGS[o] * c;
+    }
+  } else {
+    if (rank > 0) c_own = (double)D_left[m];
+    if (rank + 1 < nranks) {
+      const size_t o = (size_t)rank * 2 * M + m;
+      const double cn = (double)ownDS[m] + (double)allGS[o] * c_own;   // carry into slab rank+1
+      y = (double)S1_right[m] + cn * (double)allGS[o + 3 * M];         // S2 of slab rank+1
+    }
+  }
+  carry_y[m] = (R)y;
+  if (rank > 0) {
+    double dd, h;
+    slab_mode(p, m, dd, h);
+    double P = 1.0;
+    for (int k = 0; k < p.T; ++k) {
+      P *= slab_pivot(p, k, dd, h);
+      R* w = p.work + (size_t)k * M + m;
+      *w = (R)((double)*w + P * c_own);
+    }
+  }
+}
+
+// max over slabs of the gain G_q of every mode (classifies long-range modes once)
+template <typename R>
+__global__ void __launch_bounds__(256) k_slab_gmax(const R* __restrict__ allGS, size_t M, int nranks,
+                                                   R* __restrict__ out) {
+  const size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  R g = 0;
+  for (int s = 0; s < nranks; ++s) g = fmax(g, fabs(allGS[(size_t)s * 2 * M + m]));
+  out[m] = g;
+}
+
+// compact [D(K), S1(K)] of the long-range modes from this slab's [D, S1] planes
+template <typename R>
+__global__ void __launch_bounds__(256) k_slab_gather_long(const R* __restrict__ DS, size_t M, const int* __restrict__ idx,
+                                                          int K, R* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= K) return;
+  out[i] = DS[idx[i]];
+  out[K + i] = DS[M + idx[i]];
+}
+
 // rho row 0 of the current buffer set (the set index lives on the device)
 template <typename R>
 __global__ void __launch_bounds__(256) k_copy_cur_rho(KP<R> p, R* __restrict__ dst, size_t n) {

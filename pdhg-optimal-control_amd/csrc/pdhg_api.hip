@@ -1,6 +1,7 @@
 // Host side of libpdhg: context, FFT plans, launch sequencing, C ABI (include/pdhg.h).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -127,6 +128,9 @@ struct Impl : ImplBase {
   R* halo_rho = nullptr;     // rho row j0+T from the next slab
   R* carry_y = nullptr;      // backward right carry (spectral plane)
   R* dsbuf = nullptr;        // [D, S1] exchange planes of this slab (2 x Mspec)
+  int* long_pos = nullptr;   // neighbour exchange: per mode, index in the long-range list or -1
+  int* long_idx = nullptr;   // the long-range modes (long_K of them)
+  int long_K = -1;           // -1: not classified yet
 
   ~Impl() override {
     if (stream) hipStreamSynchronize(stream);
@@ -854,6 +858,46 @@ struct Impl : ImplBase {
     HIP_TRY(hipGetLastError());
     return PDHG_OK;
   }
+  // classify the modes once from everybody's [G, S2]: long-range where some slab's gain G >= delta
+  int slab_long_modes(const R* allGS, int nranks, double delta, int* K_out) {
+    R* gmax = nullptr;
+    HIP_TRY(hipMalloc(&gmax, Mspec * sizeof(R)));
+    hipLaunchKernelGGL((k_slab_gmax<R>), dim3((unsigned)((Mspec + 255) / 256)), dim3(256), 0, stream, allGS, Mspec,
+                       nranks, gmax);
+    std::vector<R> h(Mspec);
+    hipError_t e = hipMemcpyAsync(h.data(), gmax, Mspec * sizeof(R), hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    hipFree(gmax);
+    HIP_TRY(e);
+    std::vector<int> pos(Mspec), idx;
+    for (size_t m = 0; m < Mspec; ++m) {
+      const bool lng = !((double)h[m] < delta);   // NaN counts as long (exact path)
+      pos[m] = lng ? (int)idx.size() : -1;
+      if (lng) idx.push_back((int)m);
+    }
+    int rc;
+    if (!long_pos && (rc = alloc(&long_pos, Mspec))) return rc;
+    if (long_idx) {   // re-classification: drop the old list
+      hipFree(long_idx);
+      allocs.erase(std::find(allocs.begin(), allocs.end(), (void*)long_idx));
+      long_idx = nullptr;
+    }
+    if (!idx.empty() && (rc = alloc(&long_idx, idx.size()))) return rc;
+    HIP_TRY(hipMemcpyAsync(long_pos, pos.data(), Mspec * sizeof(int), hipMemcpyHostToDevice, stream));
+    if (!idx.empty())
+      HIP_TRY(hipMemcpyAsync(long_idx, idx.data(), idx.size() * sizeof(int), hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    long_K = (int)idx.size();
+    *K_out = long_K;
+    return PDHG_OK;
+  }
+  int slab_fixup_nb(const R* D_left, const R* S1_right, const R* allLong, const R* allGS, int rank, int nranks) {
+    if (long_K < 0) return fail(PDHG_ERR_STATE, "pdhg_slab_long_modes has not been called");
+    hipLaunchKernelGGL((k_slab_fix_nb<R>), dim3((unsigned)((Mspec + 255) / 256)), dim3(256), 0, stream, kp, dsbuf,
+                       D_left, S1_right, allLong, long_pos, long_K, allGS, rank, nranks, carry_y);
+    HIP_TRY(hipGetLastError());
+    return PDHG_OK;
+  }
   int slab_fixup(const R* allDS, const R* allGS, int rank, int nranks) {
     hipLaunchKernelGGL((k_slab_fix<R>), dim3((unsigned)((Mspec + 255) / 256)), dim3(256), 0, stream, kp, allDS,
                        allGS, rank, nranks, carry_y);
@@ -925,7 +969,8 @@ struct Impl : ImplBase {
     HIP_TRY(hipGetLastError());
     return PDHG_OK;
   }
-  // planes out: 0 rho row 0 (current set), 1 phi_bar row T, 2 [D, S1] (2 spectral planes)
+  // planes out: 0 rho row 0 (current set), 1 phi_bar row T, 2 [D, S1] (2 spectral planes),
+  // 3 [D, S1] of the long-range modes (2 x long_K)
   int slab_plane_out(int which, void* dst) {
     const size_t npl = plane();
     switch (which) {
@@ -934,6 +979,12 @@ struct Impl : ImplBase {
         break;
       case 1: HIP_TRY(hipMemcpyAsync(dst, kp.phibar + (size_t)pb.T * npl, npl * sizeof(R), hipMemcpyDeviceToDevice, stream)); break;
       case 2: HIP_TRY(hipMemcpyAsync(dst, dsbuf, 2 * Mspec * sizeof(R), hipMemcpyDeviceToDevice, stream)); break;
+      case 3:
+        if (long_K < 0) return fail(PDHG_ERR_STATE, "pdhg_slab_long_modes has not been called");
+        if (long_K > 0)
+          hipLaunchKernelGGL((k_slab_gather_long<R>), dim3((unsigned)((long_K + 255) / 256)), dim3(256), 0, stream,
+                             dsbuf, Mspec, long_idx, long_K, (R*)dst);
+        break;
       default: return fail(PDHG_ERR_ARG, "unknown plane %d", which);
     }
     HIP_TRY(hipGetLastError());
@@ -1395,6 +1446,21 @@ int pdhg_slab_fixup(pdhg_ctx* ctx, const void* all_DS, const void* all_GS, int r
   if (rank < 0 || rank >= nranks) return fail(PDHG_ERR_ARG, "rank %d of %d", rank, nranks);
   return slab_dispatch(ctx, [&](auto& im) {
     return im.slab_fixup(static_cast<const float*>(all_DS), static_cast<const float*>(all_GS), rank, nranks);
+  });
+}
+int pdhg_slab_long_modes(pdhg_ctx* ctx, const void* all_GS, int nranks, double delta, int* K) {
+  if (!all_GS || !K || nranks < 1) return fail(PDHG_ERR_ARG, "null plane / count or nranks < 1");
+  return slab_dispatch(ctx, [&](auto& im) {
+    return im.slab_long_modes(static_cast<const float*>(all_GS), nranks, delta, K);
+  });
+}
+int pdhg_slab_fixup_nb(pdhg_ctx* ctx, const void* D_left, const void* S1_right, const void* all_long,
+                       const void* all_GS, int rank, int nranks) {
+  if (!D_left || !S1_right || !all_GS || rank < 0 || rank >= nranks)
+    return fail(PDHG_ERR_ARG, "null plane or rank %d outside [0, %d)", rank, nranks);
+  return slab_dispatch(ctx, [&](auto& im) {
+    return im.slab_fixup_nb(static_cast<const float*>(D_left), static_cast<const float*>(S1_right),
+                            static_cast<const float*>(all_long), static_cast<const float*>(all_GS), rank, nranks);
   });
 }
 int pdhg_slab_backward(pdhg_ctx* ctx, double tau, double* sums) {

@@ -27,7 +27,7 @@ EXPORTS = (
     "pdhg_device_bytes", "pdhg_profile_enable", "pdhg_profile_query", "pdhg_algorithmic_bytes",
     # t-slab decomposition (multi-GPU)
     "pdhg_create_slab", "pdhg_set_stream", "pdhg_slab_plane_size", "pdhg_slab_begin", "pdhg_slab_carry_gain",
-    "pdhg_slab_residual", "pdhg_slab_forward", "pdhg_slab_fixup", "pdhg_slab_backward", "pdhg_slab_primal_finalize", "pdhg_slab_dual",
+    "pdhg_slab_residual", "pdhg_slab_forward", "pdhg_slab_fixup", "pdhg_slab_long_modes", "pdhg_slab_fixup_nb", "pdhg_slab_backward", "pdhg_slab_primal_finalize", "pdhg_slab_dual",
     "pdhg_slab_dual_finalize", "pdhg_slab_outer", "pdhg_slab_outer_finalize", "pdhg_slab_plane_out",
     "pdhg_slab_plane_in", "pdhg_slab_status",
 )
@@ -118,6 +118,8 @@ def load():
         "pdhg_slab_residual": ([P, ctypes.c_int], ctypes.c_int),
         "pdhg_slab_forward": ([P, ctypes.c_double], ctypes.c_int),
         "pdhg_slab_fixup": ([P, P, P, ctypes.c_int, ctypes.c_int], ctypes.c_int),
+        "pdhg_slab_long_modes": ([P, P, ctypes.c_int, ctypes.c_double, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+        "pdhg_slab_fixup_nb": ([P, P, P, P, P, ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "pdhg_slab_backward": ([P, ctypes.c_double, P], ctypes.c_int),
         "pdhg_slab_primal_finalize": ([P, P], ctypes.c_int),
         "pdhg_slab_dual": ([P, ctypes.c_double, ctypes.c_int, ctypes.c_int, P, ctypes.c_int], ctypes.c_int),

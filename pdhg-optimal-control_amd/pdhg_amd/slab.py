@@ -28,9 +28,10 @@ import numpy as np
 from . import _native as N
 from .context import PDHGContext
 
-RHO_ROW0, PHIBAR_LAST, CARRY_DS = 0, 1, 2               # pdhg_slab_plane_out
+RHO_ROW0, PHIBAR_LAST, CARRY_DS, CARRY_LONG = 0, 1, 2, 3   # pdhg_slab_plane_out
 RHO_HALO, PHIBAR_ROW0 = 0, 1                             # pdhg_slab_plane_in
 INTERIOR, EDGE = 1, 2                                    # pdhg_slab_residual / pdhg_slab_dual parts
+LONG_RANGE_DELTA = 2.0 ** -40     # modes whose slab gains are all below this exchange with neighbours only
 
 
 def slab_bounds(T, P):
@@ -88,6 +89,15 @@ class SlabContext(PDHGContext):
 
     def fixup(self, allDS, allGS):
         N.check(self._lib.pdhg_slab_fixup(self._h, _ptr(allDS), _ptr(allGS), self.rank, self.nranks))
+
+    def long_modes(self, allGS, delta=LONG_RANGE_DELTA):
+        K = ctypes.c_int()
+        N.check(self._lib.pdhg_slab_long_modes(self._h, _ptr(allGS), self.nranks, float(delta), ctypes.byref(K)))
+        return K.value
+
+    def fixup_nb(self, D_left, S1_right, allLong, allGS):
+        N.check(self._lib.pdhg_slab_fixup_nb(self._h, _ptr(D_left), _ptr(S1_right), _ptr(allLong), _ptr(allGS),
+                                             self.rank, self.nranks))
 
     def backward(self, tau, sums):
         N.check(self._lib.pdhg_slab_backward(self._h, float(tau), _ptr(sums)))
@@ -154,6 +164,10 @@ class LocalComm:
         for r in range(self.nranks - 1):
             recv[r].copy_(send[r + 1])
 
+    def shift_both(self, send_dn, recv_dn, send_up, recv_up):
+        self.shift_down(send_dn, recv_dn)
+        self.shift_up(send_up, recv_up)
+
 
 class DistComm:
     """One slab per rank over torch.distributed (backend "nccl" = RCCL on ROCm, or "gloo")."""
@@ -192,27 +206,35 @@ class DistComm:
         else:
             self.dist.all_reduce(vecs[0])
 
-    def _shift(self, send, recv, step):
-        dst, src = self.rank + step, self.rank - step
-        stage = self.gloo and send[0].is_cuda
-        s_buf = send[0].cpu() if stage else send[0]
-        r_buf = recv[0].cpu() if stage else recv[0]
-        ops = []
-        if 0 <= dst < self.nranks:
-            ops.append(self.dist.P2POp(self.dist.isend, s_buf, dst, group=self.halo_group))
-        if 0 <= src < self.nranks:
-            ops.append(self.dist.P2POp(self.dist.irecv, r_buf, src, group=self.halo_group))
+    def _shift(self, pairs):
+        """pairs: (send tensor, recv tensor, step): send to rank+step, receive from rank-step; all in one
+        batch of point-to-point operations on the halo communicator."""
+        ops, back = [], []
+        for send, recv, step in pairs:
+            dst, src = self.rank + step, self.rank - step
+            stage = self.gloo and send.is_cuda
+            s_buf = send.cpu() if stage else send
+            r_buf = recv.cpu() if stage else recv
+            if 0 <= dst < self.nranks:
+                ops.append(self.dist.P2POp(self.dist.isend, s_buf, dst, group=self.halo_group))
+            if 0 <= src < self.nranks:
+                ops.append(self.dist.P2POp(self.dist.irecv, r_buf, src, group=self.halo_group))
+                if stage:
+                    back.append((recv, r_buf))
         if ops:
             for w in self.dist.batch_isend_irecv(ops):
                 w.wait()
-        if stage and 0 <= src < self.nranks:
-            recv[0].copy_(r_buf)
+        for recv, r_buf in back:
+            recv.copy_(r_buf)
 
     def shift_down(self, send, recv):
-        self._shift(send, recv, 1)
+        self._shift([(send[0], recv[0], 1)])
 
     def shift_up(self, send, recv):
-        self._shift(send, recv, -1)
+        self._shift([(send[0], recv[0], -1)])
+
+    def shift_both(self, send_dn, recv_dn, send_up, recv_up):
+        self._shift([(send_dn[0], recv_dn[0], 1), (send_up[0], recv_up[0], -1)])
 
 
 # ---------------------------------------------------------------------------------------------
@@ -222,10 +244,16 @@ class SlabRunner:
     """Drives the slabs of this process through outer iterations (pdhg_iterate's loop, split at
     every point where slabs exchange data)."""
 
-    def __init__(self, slabs, comm, overlap=True):
+    def __init__(self, slabs, comm, overlap=True, exchange="neighbour", delta=LONG_RANGE_DELTA):
+        """overlap: halos on a second stream while the interior rows compute.  exchange: "neighbour"
+        (D / S1 planes to the adjacent slabs + an allgather of the long-range modes only) or
+        "allgather" (every slab's full [D, S1] planes)."""
         import torch
+        if exchange not in ("neighbour", "allgather"):
+            raise ValueError("exchange must be 'neighbour' or 'allgather'")
         self.torch = torch
         self.slabs, self.comm = list(slabs), comm
+        self.exchange = exchange
         self.side = torch.cuda.Stream() if overlap else None   # halo stream
         dev = torch.device("cuda", torch.cuda.current_device())
         sp, spec = self.slabs[0].plane_sizes()
@@ -241,21 +269,29 @@ class SlabRunner:
         for s, b in zip(self.slabs, self.b):
             s.carry_gain(b["GS"])
         self.allGS = comm.allgather([b["GS"] for b in self.b])   # iteration-invariant
+        self.n_long = None
+        if exchange == "neighbour":
+            Ks = [s.long_modes(self.allGS[i], delta) for i, s in enumerate(self.slabs)]
+            self.n_long = Ks[0]
+            for b in self.b:
+                b["Dl"] = torch.zeros(spec, dtype=f32, device=dev)
+                b["S1r"] = torch.zeros(spec, dtype=f32, device=dev)
+                b["LONG"] = torch.zeros(max(1, 2 * self.n_long), dtype=f32, device=dev)
 
     def _each(self, name, *args):
         for s in self.slabs:
             getattr(s, name)(*args)
 
-    def _halo(self, shift, send, recv):
+    def _halo(self, shift, *planes):
         """Run a halo shift on the side stream after everything enqueued so far on the main stream;
         returns at once (join with _join before the halo plane is used)."""
         torch = self.torch
         if self.side is None:
-            shift(send, recv)
+            shift(*planes)
             return
         self.side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self.side):
-            shift(send, recv)
+            shift(*planes)
 
     def _join(self):
         if self.side is not None:
@@ -279,10 +315,23 @@ class SlabRunner:
         self._each("forward", tau)
         for s, b in zip(S, B):
             s.plane_out(CARRY_DS, b["DS"])
-        allDS = C.allgather([b["DS"] for b in B])
-        for i, s in enumerate(S):
-            s.fixup(allDS[i], self.allGS[i])
-            s.backward(tau, B[i]["sums"])
+        if self.exchange == "neighbour":
+            # D -> next slab, S1 -> previous slab (point to point) || allgather of the long-range modes
+            spec = B[0]["Dl"].numel()
+            for s, b in zip(S, B):
+                s.plane_out(CARRY_LONG, b["LONG"])
+            self._halo(C.shift_both, [b["DS"][:spec] for b in B], [b["Dl"] for b in B],
+                       [b["DS"][spec:] for b in B], [b["S1r"] for b in B])
+            allLong = C.allgather([b["LONG"] for b in B])
+            self._join()
+            for i, s in enumerate(S):
+                s.fixup_nb(B[i]["Dl"], B[i]["S1r"], allLong[i], self.allGS[i])
+                s.backward(tau, B[i]["sums"])
+        else:
+            allDS = C.allgather([b["DS"] for b in B])
+            for i, s in enumerate(S):
+                s.fixup(allDS[i], self.allGS[i])
+                s.backward(tau, B[i]["sums"])
         # phi_bar halo (row T of slab r -> row 0 of slab r+1: the dual's phi_bar_j), overlapped with the
         # primal sums all-reduce and the dual of the rows that do not read it
         for s, b in zip(S, B):

@@ -1,4 +1,4 @@
-"""The N > 1 path on CPU: two processes over torch.distributed "gloo" (world size 2).
+"""The N > 1 path on CPU: processes over torch.distributed "gloo" (world sizes 2 and 3).
 
 DistComm (pdhg_amd/slab.py) is the communicator the multi-GPU run uses over RCCL; here it moves CPU
 tensors.  Checked: the halo shifts, allgather and allreduce semantics, and the distributed t-solve
@@ -64,10 +64,44 @@ def _worker(rank, world, port, paths):
         y = S.right_carry(list(allX0.numpy()), list(allG.numpy()), rank)
         x = S.local_backward(b, gp, j0, y)
         assert np.allclose(x, ref[j0:j1], rtol=1e-11, atol=1e-12 * np.abs(ref).max())
+        # --- the neighbour exchange (the multi-GPU default): D -> next slab, S1 -> previous slab in one
+        # batch of point-to-point operations, an allgather of the long-range modes only
+        T, M = 12, 64
+        ae = 1.0 / (1.0 / T) ** 2
+        lam = -4.0 * np.sin(np.pi * np.arange(M) / (2 * M)) ** 2 * (M / 0.05) ** 2
+        diag = np.tile(1.0 - lam + 2 * ae, (T, 1))
+        diag[-1] -= ae
+        r = rng.standard_normal((T, M))
+        ref = S.monolithic_tridiag(diag, r, ae)
+        j0, j1 = slab_bounds(T, world)[rank]
+        gp = S.pivots(diag, ae)
+        b0, D, G = S.local_forward(r, gp, ae, j0, j1)
+        s1, s2 = S.s_sums(b0, gp, j0)
+        (allGS,) = comm.allgather([torch.from_numpy(np.concatenate([G, s2]))])
+        Gs, S2s = [a[:M] for a in allGS.numpy()], [a[M:] for a in allGS.numpy()]
+        mask = S.long_range_mask(Gs, 2.0 ** -40)
+        assert 0 < mask.sum() < M
+        Dl, S1r = [torch.zeros(M, dtype=torch.float64)], [torch.zeros(M, dtype=torch.float64)]
+        comm.shift_both([torch.from_numpy(D)], Dl, [torch.from_numpy(s1)], S1r)
+        (allLong,) = comm.allgather([torch.from_numpy(np.concatenate([D[mask], s1[mask]]))])
+        K = int(mask.sum())
+        Ds, S1s = [np.zeros(M) for _ in range(world)], [np.zeros(M) for _ in range(world)]
+        for q in range(world):
+            Ds[q][mask], S1s[q][mask] = allLong.numpy()[q][:K], allLong.numpy()[q][K:]
+        if rank > 0:
+            Ds[rank - 1][~mask] = Dl[0].numpy()[~mask]
+        if rank + 1 < world:
+            S1s[rank + 1][~mask] = S1r[0].numpy()[~mask]
+        Ds[rank] = D
+        c, y = S.carries_neighbour(Ds, S1s, Gs, S2s, rank, mask)
+        b, _ = S.fixup(b0, gp, j0, c)
+        x = S.local_backward(b, gp, j0, y)
+        assert np.allclose(x, ref[j0:j1], rtol=1e-10, atol=1e-11 * np.abs(ref).max())
     finally:
         dist.destroy_process_group()
 
 
-def test_gloo_world2_slab_exchanges():
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_slab_exchanges(world):
     paths = [os.path.join(HERE, "..", "pdhg-optimal-control_amd"), os.path.join(HERE, "..", "oracle")]
-    mp.spawn(_worker, args=(2, _free_port(), [os.path.abspath(p) for p in paths]), nprocs=2, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), [os.path.abspath(p) for p in paths]), nprocs=world, join=True)

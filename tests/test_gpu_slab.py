@@ -1,6 +1,8 @@
 """t-slab decomposition on the GPU: P slab contexts on one device, exchanging planes
 through LocalComm, must reproduce the single-context iteration (pdhg_iterate) of the same window --
-same state after n outer iterations within fp32 rounding, same error history and stop decisions.
+same state after n outer iterations within fp32 rounding, same error history and stop decisions, for
+both carry exchanges (neighbour planes + long-range modes, or the full allgather) and with the halos
+overlapped or serial.
 The single-context path is itself pinned to the oracle by test_gpu_parity.py."""
 import numpy as np
 import pytest
@@ -19,6 +21,7 @@ CASES = [
     (2, 8192, 256, 5, 2, 1),    # half-real x blocks (C4's nx)
     (1, 512, 256, 3, 3, 1),     # one-row slabs: the halo row is the whole slab
     (2, 512, 256, 19, 2, 1),    # residual tiles of 8 rows + untiled remainder rows
+    (2, 512, 256, 40, 4, 1),    # 10-row slabs: short-range modes take the neighbour-only carries
 ]
 
 
@@ -28,10 +31,11 @@ def _slabs(P, nranks, k):
                         epsl=P["epsl"], rho_alp_iters=k) for r in range(nranks)]
 
 
-@pytest.mark.parametrize("overlap", [True, False], ids=["overlap", "serial"])
+@pytest.mark.parametrize("overlap,exchange", [(True, "neighbour"), (False, "neighbour"), (True, "allgather")],
+                         ids=["overlap-nb", "serial-nb", "overlap-ag"])
 @pytest.mark.parametrize("egno,nx,ny,T,nr,k", CASES, ids=[f"e{c[0]}_{c[1]}x{c[2]}_T{c[3]}_P{c[4]}_k{c[5]}"
                                                          for c in CASES])
-def test_slabs_match_single_context(native, egno, nx, ny, T, nr, k, overlap):
+def test_slabs_match_single_context(native, egno, nx, ny, T, nr, k, overlap, exchange):
     import torch
     from pdhg_amd.context import PDHGContext
     from pdhg_amd.slab import LocalComm, SlabRunner, join_state, slab_bounds, split_state
@@ -46,7 +50,11 @@ def test_slabs_match_single_context(native, egno, nx, ny, T, nr, k, overlap):
     slabs = _slabs(P, nr, k)
     for s, part in zip(slabs, split_state(P["phi"], P["rho"], P["alp"], slab_bounds(T, nr))):
         s.set_state(*part)
-    runner = SlabRunner(slabs, LocalComm(nr), overlap=overlap)
+    runner = SlabRunner(slabs, LocalComm(nr), overlap=overlap, exchange=exchange)
+    if exchange == "neighbour":
+        assert 0 <= runner.n_long <= nx * ny
+        if T // nr >= 8:        # long slabs: most modes exchange with the neighbours only
+            assert runner.n_long < nx * ny // 4
     st = runner.iterate(n, tau, sigma, -1.0, k)
     torch.cuda.synchronize()
     phi_s, rho_s, alp_s = join_state([s.get_state() for s in slabs])

@@ -35,6 +35,23 @@ def test_single_exchange_variant_equals_monolithic(T, P):
     assert np.allclose(S.thomas_slabs_single(diag, r, ae, P), ref, rtol=1e-11, atol=1e-12 * np.abs(ref).max())
 
 
+@pytest.mark.parametrize("T,P", [(12, 3), (40, 8), (200, 8)])
+def test_neighbour_exchange_variant_equals_monolithic(T, P):
+    """Short-range modes (every slab gain < 2^-40) use only the adjacent slabs' planes; the error stays
+    at the level of the exact variants.  The symbol spans low (long-range) and high frequencies."""
+    M = 64
+    dt = 1.0 / T
+    ae = 1.0 / dt ** 2
+    lam = -4.0 * np.sin(np.pi * np.arange(M) / (2 * M)) ** 2 * (M / 0.05) ** 2
+    diag = np.tile(1.0 - lam + 2 * ae, (T, 1))
+    diag[-1] -= ae
+    r = rng.standard_normal((T, M))
+    ref = S.monolithic_tridiag(diag, r, ae)
+    out, mask = S.thomas_slabs_neighbour(diag, r, ae, P)
+    assert 0 < mask.sum() < M          # both classes present
+    assert np.allclose(out, ref, rtol=1e-10, atol=1e-11 * np.abs(ref).max())
+
+
 def test_slab_bounds_cover_rows():
     for T in (1, 7, 200):
         for P in (1, 2, 3, 8):
