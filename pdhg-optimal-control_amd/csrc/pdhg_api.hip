@@ -16,6 +16,7 @@
 #include "kernels_1d.hpp"
 #include "kernels_2d.hpp"
 #include "kernels_2d_fast.hpp"
+#include "kernels_dual_lds.hpp"
 #include "kernels_common.hpp"
 
 using namespace pdhg;
@@ -102,6 +103,7 @@ struct Impl : ImplBase {
   int rows_var = 0;                       // row-kernel shape variant (see with_fast_rows)
   bool fast_dual = false;                 // fp32 time-marching float4 dual kernel (k_dual_fast_2d)
   int NTd = 256, gxd = 0, gyd = 0, gzd = 0, jchunk_d = 1;
+  int dual_rx = 0;   // > 0: k_dual_lds_2d with dual_rx x rows per workgroup (x neighbours through LDS)
   size_t lds_res = 0, lds_xt = 0;
   // fast row kernels (fp32, power-of-two ny): RW rows per workgroup, NTf threads
   bool fast_rows = false;
@@ -240,9 +242,14 @@ struct Impl : ImplBase {
       }
       if (sizeof(R) == 4 && ny % 256 == 0) {
         fast_dual = true;
-        NTd = std::min(256, ny / 4);
-        gxd = nx;
-        gyd = (ny / 4 + NTd - 1) / NTd;
+        dual_rx = (nx % 8 == 0) ? 8 : 0;
+        if (const char* e = getenv("PDHG_DUAL_RX")) {   // tuning override: 0 = row-per-thread kernel
+          const int v = atoi(e);
+          if (v == 0 || ((v == 4 || v == 8 || v == 16) && nx % v == 0)) dual_rx = v;
+        }
+        NTd = dual_rx ? dual_rx * 64 : std::min(256, ny / 4);
+        gxd = dual_rx ? nx / dual_rx : nx;
+        gyd = dual_rx ? ny / 256 : (ny / 4 + NTd - 1) / NTd;
         const int nJ0 = std::max(1, std::min(T, (2048 + gxd * gyd - 1) / (gxd * gyd)));
         jchunk_d = (T + nJ0 - 1) / nJ0;
         gzd = (T + jchunk_d - 1) / jchunk_d;
@@ -708,8 +715,15 @@ struct Impl : ImplBase {
   // fast dual over time rows [lo, hi); its partials start at block row zbase.  Returns the z extent.
   template <int EGNO>
   void launch_dual_fast_e(const KP<R>& p, int lo, int hi, int gz, int zbase) {
-    if constexpr (std::is_same<R, float>::value)
-      hipLaunchKernelGGL((k_dual_fast_2d<EGNO>), dim3(gxd, gyd, gz), dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase);
+    if constexpr (std::is_same<R, float>::value) {
+      const dim3 g(gxd, gyd, gz);
+      switch (dual_rx) {
+        case 4: hipLaunchKernelGGL((k_dual_lds_2d<EGNO, 4>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase); break;
+        case 8: hipLaunchKernelGGL((k_dual_lds_2d<EGNO, 8>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase); break;
+        case 16: hipLaunchKernelGGL((k_dual_lds_2d<EGNO, 16>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase); break;
+        default: hipLaunchKernelGGL((k_dual_fast_2d<EGNO>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase);
+      }
+    }
   }
   int launch_dual_fast(const KP<R>& p, int lo = 0, int hi = -1, int zbase = 0) {
     if (hi < 0) hi = pb.T;
