@@ -139,6 +139,12 @@ int pdhg_synchronize(pdhg_ctx* ctx);
 /* Device bytes held by the context. */
 int pdhg_device_bytes(pdhg_ctx* ctx, unsigned long long* bytes);
 
+/* Which kernel variant a context selected (no reference counterpart; tests and benches assert the fast
+ * paths engaged): "fused_residual" 1/0 (the dual sweep forms the next residual, k_dual_lds_2d FR),
+ * "fast_rows" 1/0 (fp32 8/4-row y-transform kernels), "fast_dual" (-1 generic, 0 row-per-thread,
+ * RX rows through LDS), "fast_xt" (0 generic, 1 single-role, 2 warp-specialised x-transform). */
+int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value);
+
 /* Per-launch kernel timing for the benchmark: HIP events recorded on the
  * context's stream around every launch of the named kernel class
  * ("dual", "precond_fwd", "precond_bwd", "residual", "update") while

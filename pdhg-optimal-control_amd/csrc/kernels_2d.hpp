@@ -361,7 +361,7 @@ __global__ void __launch_bounds__(256) k_invy_update_2d(KP<R> p, F ply, const cp
 // f0c: phi_bar row j at (x, y).
 template <typename R, int EGNO>
 __device__ __forceinline__ R dual_point(const KP<R>& p, R pc, R pxm, R pxp, R pym, R pyp, R f0c, R rho, const R* ao,
-                                        R axc, R ayc, R* an) {
+                                        R axc, R ayc, R* an, R* fo = nullptr) {
   const R DxR = (pxp - pc) * p.inv_dx;
   const R DxL = (pc - pxm) * p.inv_dx;
   const R DyR = (pyp - pc) * p.inv_dy;
@@ -388,6 +388,12 @@ __device__ __forceinline__ R dual_point(const KP<R>& p, R pc, R pxm, R pxp, R py
   if (p.epsl != (R)0) {
     vec = vec - p.epsl * ((pxp + pxm - (R)2 * pc) * p.inv_dx2);
     vec = vec - p.epsl * ((pyp + pym - (R)2 * pc) * p.inv_dy2);
+  }
+  if (fo) {   // f1x, f2x, f1y, f2y of the new controls (the next residual's fluxes, :13-47)
+    fo[0] = f1x;
+    fo[1] = f2x;
+    fo[2] = f1y;
+    fo[3] = f2y;
   }
   vec = vec - (DxR * f1x + DxL * f2x + DyR * f1y + DyL * f2y);
   vec = vec - L;

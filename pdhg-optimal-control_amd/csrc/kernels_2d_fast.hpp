@@ -246,6 +246,156 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const floa
   }
 }
 
+// Residual rows formed by the fused dual sweep (k_dual_lds_2d<.., FR = true>, 8-row x 256-column tiles)
+// + forward DHT along y.  Completes the terms the sweep could not see (update_fns_in_pdhg.py:83-96):
+// row x0 gets eps*rho'(x0-1)/dx^2 + m1x(x0-1)/dx and row x0+RW-1 gets eps*rho'(x0+RW)/dx^2 - m2x(x0+RW)/dx,
+// both from the rho' / alp' rows (periodic wrap); the first / last column of every 256-wide strip gets
+// eps*rho'/dy^2 +- m/dy of the neighbouring strip's edge column from p.ey.  Then the same in-place
+// 4-line FFT and blocked-layout unpack as k_res_fwdy_fast_2d.  Needs RW = 8 (the sweep's tile height),
+// bc (0, 0), ny % 256 == 0.
+// Persistent: G workgroups (one per CU: the 4 lines take 139 KiB of LDS) stride over the T * nx/RW
+// row-group tasks, and the next task's rows are loaded into registers while the current one is
+// transformed and stored, so the CU's memory pipe is not idle during the FFT.
+// grid: G <= T * nx/RW; block NT (N/4 % NT == 0); LDS RW/2 * (N + N/16) * 8 B.
+template <int EGNO, int N, int RW, int NT>
+__global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const float2* __restrict__ twy) {
+  using C = float2;
+  constexpr int NL = RW / 2;
+  constexpr int GPT = (N / 4) / NT;
+  constexpr bool PREFETCH_SIDE = NT <= 512;   // 1024 threads (ny = 4096): no registers for it
+  constexpr int YW = 256, NSTRIP = N / YW;
+  static_assert(RW == 8 && N % YW == 0 && (N / 4) % NT == 0, "fused residual tiles are 8 rows x 256 columns");
+  if (p.ctrl->done) return;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  C* A = reinterpret_cast<C*>(smem_raw);
+  const int cur = p.ctrl->cur;
+  const int nx = p.nx;
+  const int ngx = nx / RW;
+  const int ntask = ngx * p.T;
+  const size_t plane = (size_t)nx * N;
+  const bool use_eps = p.epsl != 0.f;
+  const int B = p.B;
+  const int CS4 = RW * B / 4;
+  const int nb = p.nb;
+  // next task's inputs: the residual rows are loaded before this task's FFT (they fly during it), the
+  // halo rows and strip-edge values after it (they fly during the unpack and stores)
+  struct Rows {
+    float4 v[RW];              // residual rows x0 .. x0+RW-1
+  };
+  struct Side {
+    float4 rm, a1m, rp, a2p;   // rho', alp1x of row x0-1; rho', alp2x of row x0+RW
+    float2 e[RW];              // strip-edge lanes: the neighbouring strip's (rho', m1y) or (rho', m2y)
+  };
+  auto load_rows = [&](int task, Rows (&in)[GPT]) {
+    const int j = task / ngx, x0 = (task - j * ngx) * RW;
+    const float* R0 = p.res + (size_t)j * plane + (size_t)x0 * N;
+#pragma unroll
+    for (int gi = 0; gi < GPT; ++gi) {
+      const int y = 4 * (threadIdx.x + gi * NT);
+#pragma unroll
+      for (int r = 0; r < RW; ++r) in[gi].v[r] = ld4(R0 + (size_t)r * N + y);
+    }
+  };
+  auto load_side = [&](int task, Side (&in)[GPT]) {
+    const int j = task / ngx, x0 = (task - j * ngx) * RW;
+    const int xm = x0 == 0 ? nx - 1 : x0 - 1, xp = x0 + RW == nx ? 0 : x0 + RW;   // periodic
+    const size_t om = (size_t)j * plane + (size_t)xm * N, op = (size_t)j * plane + (size_t)xp * N;
+    const float2* ey = reinterpret_cast<const float2*>(p.ey) + ((size_t)j * nx + x0) * NSTRIP * 2;
+#pragma unroll
+    for (int gi = 0; gi < GPT; ++gi) {
+      const int y = 4 * (threadIdx.x + gi * NT);
+      in[gi].rm = ld4(p.rho[cur] + om + y);
+      in[gi].a1m = ld4(p.alp[cur][0] + om + y);
+      in[gi].rp = ld4(p.rho[cur] + op + y);
+      in[gi].a2p = ld4(p.alp[cur][1] + op + y);
+      // first column of a strip: (rho', m1y) of the previous strip's last column (float2 slot 1);
+      // last column: (rho', m2y) of the next strip's first column (slot 0); other lanes: a dummy read
+      const int s = y / YW, yo = y - s * YW;
+      const bool first = yo == 0, last = yo == YW - 4;
+      const int sn = first ? (s == 0 ? NSTRIP - 1 : s - 1) : (s == NSTRIP - 1 ? 0 : s + 1);
+      const int slot = first ? 2 * sn + 1 : last ? 2 * sn : 0;
+#pragma unroll
+      for (int r = 0; r < RW; ++r) in[gi].e[r] = ey[(size_t)r * NSTRIP * 2 + slot];
+    }
+  };
+  Rows nrow[GPT];
+  Side nside[GPT];
+  int task = blockIdx.x;
+  if (task < ntask) {
+    load_rows(task, nrow);
+    load_side(task, nside);
+  }
+  for (; task < ntask; task += gridDim.x) {
+    const int j = task / ngx, x0 = (task - j * ngx) * RW;
+    const int xm = x0 == 0 ? nx - 1 : x0 - 1, xp = x0 + RW == nx ? 0 : x0 + RW;
+    const float axm = p.ax[xm], axp = p.ax[xp];
+    if (!PREFETCH_SIDE && task != (int)blockIdx.x) load_side(task, nside);
+#pragma unroll
+    for (int gi = 0; gi < GPT; ++gi) {
+      const int y = 4 * (threadIdx.x + gi * NT);
+      const Side& in = nside[gi];
+      float4 v[RW];
+#pragma unroll
+      for (int r = 0; r < RW; ++r) v[r] = nrow[gi].v[r];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float m1 = m1f<EGNO>(f4(in.rm, e), f4(in.a1m, e), axm);
+        const float m2 = m2f<EGNO>(f4(in.rp, e), f4(in.a2p, e), axp);
+        float c0 = m1 * p.inv_dx, c7 = -m2 * p.inv_dx;
+        if (use_eps) {
+          c0 = c0 + p.epsl * (f4(in.rm, e) * p.inv_dx2);
+          c7 = c7 + p.epsl * (f4(in.rp, e) * p.inv_dx2);
+        }
+        f4set(v[0], e, f4(v[0], e) + c0);
+        f4set(v[RW - 1], e, f4(v[RW - 1], e) + c7);
+      }
+      const int yo = y & (YW - 1);
+      if (yo == 0) {
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+          float c = in.e[r].y * p.inv_dy;
+          if (use_eps) c = c + p.epsl * (in.e[r].x * p.inv_dy2);
+          v[r].x += c;
+        }
+      } else if (yo == YW - 4) {
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+          float c = -in.e[r].y * p.inv_dy;
+          if (use_eps) c = c + p.epsl * (in.e[r].x * p.inv_dy2);
+          v[r].w += c;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < RW; ++r) {
+        float* Af = reinterpret_cast<float*>(A + (r >> 1) * Pad<N>::LINE + pix(y)) + (r & 1);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Af[2 * e] = f4(v[r], e);
+      }
+    }
+    const bool more = task + (int)gridDim.x < ntask;
+    if (more) load_rows(task + gridDim.x, nrow);
+    lds_sync();
+    lds_fft_inplace<C, N, NL, NT>(A, twy);
+    if (PREFETCH_SIDE && more) load_side(task + gridDim.x, nside);
+    float* wk = p.work + (size_t)j * nb * nx * B;
+    for (int t = threadIdx.x; t < nb * CS4; t += NT) {
+      const int b = t / CS4, part = t - b * CS4;
+      float4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int f = part * 4 + e;
+        const int r = f / B, c = f - r * B;
+        const int ky = b * B + c;
+        float ha = 0.f, hb = 0.f;
+        if (ky < N) hartley_padded<C, float>(A + (r >> 1) * Pad<N>::LINE, N, ky, ha, hb);
+        f4set(v, e, (r & 1) ? hb : ha);
+      }
+      st4(wk + ((size_t)b * nx + x0) * B + part * 4, v);
+    }
+    lds_sync();
+  }
+}
+
 // G workgroups striding over the T * nx/RW row-group tasks; block NT; LDS RW/2 * (N + N/16) * 8 B.
 // sums: [0] sum (phi'-phi)^2, [1] sum phi^2 (old), [2] sum phi'^2
 template <int N, int RW, int NT>

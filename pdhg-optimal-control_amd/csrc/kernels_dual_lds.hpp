@@ -13,13 +13,27 @@
 
 namespace pdhg {
 
-template <int EGNO, int RX>
-__global__ void __launch_bounds__(RX * 64, 3) k_dual_lds_2d(KP<float> p, int jchunk, int jbase, int jend, int zbase) {
+//
+// FR (fused residual, rho_alp_iters = 1, periodic bc, egno 1/2, one time chunk per workgroup): the sweep
+// also forms the NEXT primal's continuity residual (update_fns_in_pdhg.py:72-96) from the rho', alp'
+// it has just computed, so the residual kernel does not re-read rho and the four alp arrays.  Row j's
+// fluxes m = (rho'+1e-4) f(alp') are exchanged between the waves through a second LDS double buffer
+// (x neighbours) and the adjacent lanes (y neighbours); R_j needs rho'_{j+1}, so it is completed and
+// stored one step later (R_{T-1} with rho_T = 0 and + c/dt after the loop).  Terms that need values
+// outside the workgroup's 8 x 256 tile are left out: the rows x0-1 / x0+RX (added by
+// k_res_fwdy_fused_2d from the rho', alp' rows themselves) and the columns outside the 256-wide strip
+// (added from p.ey, where the strip's first / last columns leave [rho', m2y] / [rho', m1y]).
+template <int EGNO, int RX, bool FR = false>
+__global__ void __launch_bounds__(RX * 64, FR ? 2 : 3) k_dual_lds_2d(KP<float> p, int jchunk, int jbase, int jend,
+                                                                     int zbase) {
   if (p.ctrl->done || p.ctrl->inner_done) return;
   constexpr int NA = (EGNO == 3) ? 2 : 4;
   constexpr int NS = 3 + 3 * NA;
   constexpr int YW = 256;                         // y strip per workgroup (64 lanes x float4)
+  static_assert(!FR || EGNO != 3, "fused residual: egno 1/2 (four live controls)");
   __shared__ __align__(16) float4 strip[2][RX + 2][YW / 4];
+  // FR: [buffer][row][rho', m1x, m2x][lane]
+  __shared__ __align__(16) float4 flux[FR ? 2 : 1][FR ? RX : 1][3][YW / 4];
   const int cur = p.ctrl->cur;
   const int src_set = (p.inplace || p.sub == 0) ? cur : 1 - cur;
   const int dst_set = p.inplace ? cur : 1 - cur;
@@ -77,6 +91,34 @@ __global__ void __launch_bounds__(RX * 64, 3) k_dual_lds_2d(KP<float> p, int jch
     strip[buf][r + 1][lane] = in.pc;
     if (has_h) strip[buf][hslot][lane] = zh ? z4() : in.ph;
   };
+  // FR state: the y part of row j-1's residual (eps*Dyy rho' and the y flux divergence), completed at
+  // step j once rho'_j and the x neighbours' fluxes (LDS) are known
+  float yeps[4] = {0.f, 0.f, 0.f, 0.f}, ydiv[4] = {0.f, 0.f, 0.f, 0.f};
+  const bool use_eps = p.epsl != 0.f;
+  const int nstrip = ny / YW;
+  // R_{jr} (row jr of the next residual) = (rho'_{jr+1} - rho'_{jr})/dt + eps*Lap rho' - div m, from the
+  // flux buffer fb (row jr's values) and rnext = rho'_{jr+1} at this thread's 4 points
+  auto finish_res = [&](int jr, int fb, const float4& rnext, float cdt) {
+    const float4 rc = flux[fb][r][0][lane], m1c = flux[fb][r][1][lane], m2c = flux[fb][r][2][lane];
+    const int rmi = r > 0 ? r - 1 : r, rpi = r < RX - 1 ? r + 1 : r;   // wave-uniform
+    float4 rm = flux[fb][rmi][0][lane], m1m = flux[fb][rmi][1][lane];
+    float4 rp = flux[fb][rpi][0][lane], m2p = flux[fb][rpi][2][lane];
+    if (r == 0) rm = m1m = z4();            // row x0-1: added by the residual kernel
+    if (r == RX - 1) rp = m2p = z4();       // row x0+RX: likewise
+    float4 out;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float r0 = f4(rc, e);
+      float res = (f4(rnext, e) - r0) * p.inv_dt;
+      if (use_eps) {
+        res = res + p.epsl * ((f4(rp, e) + f4(rm, e) - 2.f * r0) * p.inv_dx2);
+        res = res + yeps[e];
+      }
+      const float div = (f4(m1c, e) - f4(m1m, e)) * p.inv_dx + (f4(m2p, e) - f4(m2c, e)) * p.inv_dx + ydiv[e];
+      f4set(out, e, res - div + cdt);
+    }
+    st4(p.res + (size_t)jr * plane + rxc + y, out);
+  };
   if (j0 < j1) {
     float4 f0 = ld4(p.phibar + (size_t)j0 * plane + rxc + y);   // phi_bar row j
     In nxt = load(j0);
@@ -91,18 +133,27 @@ __global__ void __launch_bounds__(RX * 64, 3) k_dual_lds_2d(KP<float> p, int jch
       const float pyl = lane_from_prev(pc.w, zym ? 0.f : in.el);
       const float pyr = lane_from_next(pc.x, zyp ? 0.f : in.er);
       float4 rn4, an4[NA];
+      float4 m1x4, m2x4;
+      float m1y[4], m2y[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float c = f4(pc, e);
         const float lft = e == 0 ? pyl : f4(pc, e - 1);
         const float rgt = e == 3 ? pyr : f4(pc, e + 1);
-        float ao[4], an[4];
+        float ao[4], an[4], fo[4];
 #pragma unroll
         for (int a = 0; a < NA; ++a) ao[a] = f4(in.al[a], e);
         const float rho = f4(in.rho, e);
         const float rn = dual_point<float, EGNO>(p, c, f4(pm, e), f4(pp, e), lft, rgt, f4(f0, e), rho, ao, axc,
-                                                 f4(ay4, e), an);
+                                                 f4(ay4, e), an, FR ? fo : nullptr);
         f4set(rn4, e, rn);
+        if constexpr (FR) {   // fluxes (rho'+1e-4) f(alp') of row j (m1f / m2f of the residual kernel)
+          const float rq = rn + 1e-4f;
+          f4set(m1x4, e, rq * fo[0]);
+          f4set(m2x4, e, rq * fo[1]);
+          m1y[e] = rq * fo[2];
+          m2y[e] = rq * fo[3];
+        }
         const double dr = (double)rn - (double)rho;
         s[0] += dr * dr;
         s[1] += (double)rn * (double)rn;
@@ -121,10 +172,35 @@ __global__ void __launch_bounds__(RX * 64, 3) k_dual_lds_2d(KP<float> p, int jch
 #pragma unroll
       for (int a = 0; a < NA; ++a) st4(ad[a] + o, an4[a]);
       f0 = pc;
+      if constexpr (FR) {
+        if (j > j0) finish_res(j - 1, buf ^ 1, rn4, 0.f);   // row j-1, with rho'_j
+        flux[buf][r][0][lane] = rn4;
+        flux[buf][r][1][lane] = m1x4;
+        flux[buf][r][2][lane] = m2x4;
+        // y part of row j: neighbours from the adjacent lanes; the strip's outer columns are left out
+        // (0 here) and handed to the residual kernel through p.ey
+        const float rym = lane_from_prev(rn4.w, 0.f), ryp = lane_from_next(rn4.x, 0.f);
+        const float m1ym = lane_from_prev(m1y[3], 0.f), m2yp = lane_from_next(m2y[0], 0.f);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float r0 = f4(rn4, e);
+          const float lo = e == 0 ? rym : f4(rn4, e - 1), hi = e == 3 ? ryp : f4(rn4, e + 1);
+          const float m1l = e == 0 ? m1ym : m1y[e - 1], m2h = e == 3 ? m2yp : m2y[e + 1];
+          yeps[e] = p.epsl * ((hi + lo - 2.f * r0) * p.inv_dy2);
+          ydiv[e] = (m1y[e] - m1l) * p.inv_dy + (m2h - m2y[e]) * p.inv_dy;
+        }
+        float* eyr = p.ey + (((size_t)j * nx + x) * nstrip + blockIdx.y) * 4;
+        if (lane == 0) *reinterpret_cast<float2*>(eyr) = make_float2(rn4.x, m2y[0]);
+        if (lane == kWave - 1) *reinterpret_cast<float2*>(eyr + 2) = make_float2(rn4.w, m1y[3]);
+      }
       if (j + 1 < j1) {     // uniform over the workgroup
         stage(nxt, buf ^ 1);
         __syncthreads();
       }
+    }
+    if constexpr (FR) {   // the window's last row: rho_T = 0, + c/dt (update_fns_in_pdhg.py:80, 95)
+      __syncthreads();
+      finish_res(j1 - 1, (j1 - 1 - j0) & 1, z4(), p.c_over_dt);
     }
   }
   block_reduce_store<NS>(s, p.partials, ((zbase + (int)blockIdx.z) * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x);

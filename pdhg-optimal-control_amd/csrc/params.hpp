@@ -46,6 +46,9 @@ struct KP {
   // bc_x = 1 (egno 3, utils_precond.py:159-174): DCT-II along x instead of the DHT
   const R* cx;             // y-symbol factor per x mode: 2 cos(pi kx / 2nx) (DCT) or 1 [nx]
   const cplx<R>* dctw;     // e^{-i pi k / 2nx}, k < nx (DCT only)
+  // fused residual (k_dual_lds_2d FR / k_res_fwdy_fused_2d): residual rows formed by the dual sweep
+  R* res;                  // [T][nx][ny]
+  R* ey;                   // [T][nx][ny/256][4]: strip edge columns (rho', m2y first; rho', m1y last)
 };
 
 // neighbour index along an axis of length n with boundary condition bc

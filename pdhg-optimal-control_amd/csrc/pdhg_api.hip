@@ -104,6 +104,11 @@ struct Impl : ImplBase {
   bool fast_dual = false;                 // fp32 time-marching float4 dual kernel (k_dual_fast_2d)
   int NTd = 256, gxd = 0, gyd = 0, gzd = 0, jchunk_d = 1;
   int dual_rx = 0;   // > 0: k_dual_lds_2d with dual_rx x rows per workgroup (x neighbours through LDS)
+  // fused residual: the dual sweep also forms the next primal's residual rows (k_dual_lds_2d FR), the
+  // residual kernel only completes the tile-edge terms and transforms (k_res_fwdy_fused_2d)
+  bool fuse_res = false;
+  bool res_valid = false;   // p.res / p.ey hold the residual of the current (rho, alp)
+  int n_cu = 256;           // compute units (persistent grids)
   size_t lds_res = 0, lds_xt = 0;
   // fast row kernels (fp32, power-of-two ny): RW rows per workgroup, NTf threads
   bool fast_rows = false;
@@ -164,6 +169,7 @@ struct Impl : ImplBase {
     const int nx = pb.nx, ny = pb.ny, T = pb.T;
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    HIP_TRY(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
     HIP_TRY(hipHostMalloc((void**)&h_done, sizeof(int), hipHostMallocDefault));
     const bool is2d = pb.ndim == 2;
     na = (pb.ndim == 1 || pb.egno == 3) ? 2 : 4;
@@ -274,6 +280,19 @@ struct Impl : ImplBase {
           g_fast_upd = std::min((nx / RWf) * T, 2048);
         }
       }
+      // fused residual: fp32 fast kernels with 8-row tiles on both sides, rho_alp_iters = 1 (in place),
+      // periodic bc, egno 1/2, single context; each dual workgroup must march the whole window (the
+      // residual row j needs rho'_{j+1}), so only grids with enough (x, y) tiles to fill the chip
+      // (PDHG_FUSE_RES=1 forces it for any eligible size, =0 turns it off)
+      if (sizeof(R) == 4 && fast_dual && dual_rx == 8 && fast_rows && RWf == 8 && pb.bc_x == 0 && pb.bc_y == 0 &&
+          pb.egno != 3 && !two_sets && !slab) {
+        fuse_res = gxd * gyd >= 1024;
+        if (const char* e = getenv("PDHG_FUSE_RES")) fuse_res = atoi(e) != 0;
+        if (fuse_res) {
+          jchunk_d = T;
+          gzd = 1;
+        }
+      }
     } else {
       p.B = 1;
       p.lB = 0;
@@ -328,6 +347,11 @@ struct Impl : ImplBase {
       C* g = nullptr;
       if ((rc = alloc(&g, (size_t)gx1 * 2 * nx))) return rc;
       p.gscr = g;
+    }
+    p.res = p.ey = nullptr;
+    if (fuse_res) {
+      if ((rc = alloc(&p.res, (size_t)T * npl))) return rc;
+      if ((rc = alloc(&p.ey, (size_t)T * nx * (ny / 256) * 4))) return rc;
     }
     if (slab) {
       Mspec = (size_t)p.nb * nx * p.B;
@@ -527,6 +551,29 @@ struct Impl : ImplBase {
   int launch_residual(KP<R> p, int lo, int hi) {
     if (hi <= lo) return PDHG_OK;
     int rc = PDHG_OK;
+    if (fuse_res && res_valid && lo == 0 && hi == pb.T) {
+      ProfScope ps(this, "residual");
+      rc = with_fast_rows([&](auto Nc, auto RWc, auto NTc) {
+        constexpr int N_ = decltype(Nc)::value, RW_ = decltype(RWc)::value, NT_ = decltype(NTc)::value;
+        int r2;
+        constexpr int NTF = NT_;
+        if constexpr (sizeof(R) == 4 && RW_ == 8 && N_ % 256 == 0 && (N_ / 4) % NTF == 0) {
+          const dim3 g(std::min((pb.nx / RW_) * pb.T, n_cu));   // persistent, one workgroup per CU (LDS)
+          if (pb.egno == 1) {
+            if ((r2 = ensure_lds(k_res_fwdy_fused_2d<1, N_, RW_, NTF>, lds_fast))) return r2;
+            hipLaunchKernelGGL((k_res_fwdy_fused_2d<1, N_, RW_, NTF>), g, dim3(NTF), lds_fast, stream, p, twy);
+          } else {
+            if ((r2 = ensure_lds(k_res_fwdy_fused_2d<2, N_, RW_, NTF>, lds_fast))) return r2;
+            hipLaunchKernelGGL((k_res_fwdy_fused_2d<2, N_, RW_, NTF>), g, dim3(NTF), lds_fast, stream, p, twy);
+          }
+          return (int)PDHG_OK;
+        }
+        return fail(PDHG_ERR_STATE, "fused residual without 8-row fast kernels (ny=%d)", pb.ny);
+      });
+      if (rc) return rc;
+      HIP_TRY(hipGetLastError());
+      return PDHG_OK;
+    }
     if (fast_rows) {
       ProfScope ps(this, "residual");
       p.row_base = lo;
@@ -717,6 +764,14 @@ struct Impl : ImplBase {
   void launch_dual_fast_e(const KP<R>& p, int lo, int hi, int gz, int zbase) {
     if constexpr (std::is_same<R, float>::value) {
       const dim3 g(gxd, gyd, gz);
+      if constexpr (EGNO != 3) {
+        if (fuse_res && p.inplace && lo == 0 && hi == pb.T && gz == 1) {
+          hipLaunchKernelGGL((k_dual_lds_2d<EGNO, 8, true>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase);
+          res_valid = true;
+          return;
+        }
+      }
+      res_valid = false;
       switch (dual_rx) {
         case 4: hipLaunchKernelGGL((k_dual_lds_2d<EGNO, 4>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase); break;
         case 8: hipLaunchKernelGGL((k_dual_lds_2d<EGNO, 8>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase); break;
@@ -1054,6 +1109,7 @@ struct Impl : ImplBase {
   }
 
   int set_state(const double* phi, const double* rho, const double* alp) {
+    res_valid = false;
     const size_t npl = plane();
     const int T = pb.T;
     const int cur = 0;
@@ -1142,6 +1198,7 @@ struct Impl : ImplBase {
   }
 
   int init_state(const double* g) {
+    res_valid = false;
     const size_t npl = plane();
     const int T = pb.T;
     std::vector<R> row(npl);
@@ -1216,8 +1273,12 @@ struct Impl : ImplBase {
       if (d2) return S * N * (14.0 + 11.0 * k + 5.0 * (k > 1));
       return S * N * (12.0 + 7.0 * k + 3.0 * (k > 1));
     }
-    if (cls == "dual") return S * N * (1.0 + 2.0 * nr);      // read phi_bar, rho, alp; write rho, alp
-    if (cls == "residual") return S * N * (nr + 1.0);        // read rho, alp; write spectrum
+    // fused residual: the dual also writes the residual rows (+1, plus the strip-edge columns), the
+    // residual kernel reads them, the halo rows rho'/alp' x0-1 and x0+8 (4 rows per 8) and the edge
+    // columns, and writes the spectrum
+    const double ey = fuse_res ? 4.0 / 256.0 : 0.0;
+    if (cls == "dual") return S * N * (1.0 + 2.0 * nr + (fuse_res ? 1.0 + ey : 0.0));
+    if (cls == "residual") return S * N * (fuse_res ? 2.5 + ey : nr + 1.0);
     if (cls == "precond") return S * N * (d2 ? 4.0 : 2.0);   // 2-D: x-DHT+Thomas fwd (2N) + bwd+x-DHT (2N)
     if (cls == "update") return S * N * 4.0;                 // read U, phi; write phi, phi_bar
     return -1.0;
@@ -1373,6 +1434,18 @@ int pdhg_device_bytes(pdhg_ctx* ctx, unsigned long long* bytes) {
   if (!bytes) return fail(PDHG_ERR_ARG, "null bytes");
   return dispatch(ctx, [&](auto& im) {
     *bytes = im.dev_bytes;
+    return (int)PDHG_OK;
+  });
+}
+int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
+  if (!key || !value) return fail(PDHG_ERR_ARG, "null argument");
+  return dispatch(ctx, [&](auto& im) {
+    const std::string k(key);
+    if (k == "fused_residual") *value = im.fuse_res ? 1 : 0;
+    else if (k == "fast_rows") *value = im.fast_rows ? 1 : 0;
+    else if (k == "fast_dual") *value = im.fast_dual ? im.dual_rx : -1;
+    else if (k == "fast_xt") *value = im.fast_xt ? (im.ws_xt ? 2 : 1) : 0;
+    else return fail(PDHG_ERR_ARG, "unknown path key %s", key);
     return (int)PDHG_OK;
   });
 }

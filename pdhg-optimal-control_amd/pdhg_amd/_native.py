@@ -24,7 +24,7 @@ EXPORTS = (
     "pdhg_last_error", "pdhg_abi_version", "pdhg_device_count", "pdhg_create", "pdhg_destroy",
     "pdhg_set_state", "pdhg_get_state", "pdhg_get_phi_bar", "pdhg_set_phi_bar", "pdhg_init_state",
     "pdhg_update_primal", "pdhg_update_dual", "pdhg_errors", "pdhg_inner_error", "pdhg_iterate", "pdhg_set_stop_rules", "pdhg_synchronize",
-    "pdhg_device_bytes", "pdhg_profile_enable", "pdhg_profile_query", "pdhg_algorithmic_bytes",
+    "pdhg_device_bytes", "pdhg_path_info", "pdhg_profile_enable", "pdhg_profile_query", "pdhg_algorithmic_bytes",
     # t-slab decomposition (multi-GPU)
     "pdhg_create_slab", "pdhg_set_stream", "pdhg_slab_plane_size", "pdhg_slab_begin", "pdhg_slab_carry_gain",
     "pdhg_slab_residual", "pdhg_slab_forward", "pdhg_slab_fixup", "pdhg_slab_long_modes", "pdhg_slab_fixup_nb", "pdhg_slab_backward", "pdhg_slab_primal_finalize", "pdhg_slab_dual",
@@ -105,6 +105,7 @@ def load():
         "pdhg_set_stop_rules": ([P, ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "pdhg_synchronize": ([P], ctypes.c_int),
         "pdhg_device_bytes": ([P, ctypes.POINTER(ctypes.c_ulonglong)], ctypes.c_int),
+        "pdhg_path_info": ([P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
         "pdhg_profile_enable": ([P, ctypes.c_int], ctypes.c_int),
         "pdhg_profile_query": ([P, ctypes.c_char_p, dp, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
         "pdhg_algorithmic_bytes": ([P, ctypes.c_int, ctypes.c_char_p, dp], ctypes.c_int),

@@ -132,6 +132,13 @@ class PDHGContext:
         N.check(self._lib.pdhg_device_bytes(self._h, ctypes.byref(b)))
         return b.value
 
+    def path_info(self, key):
+        """Kernel variant selected for this context (pdhg_path_info): "fused_residual", "fast_rows",
+        "fast_dual", "fast_xt"."""
+        v = ctypes.c_int()
+        N.check(self._lib.pdhg_path_info(self._h, key.encode(), ctypes.byref(v)))
+        return v.value
+
     def profile_enable(self, on=True):
         N.check(self._lib.pdhg_profile_enable(self._h, 1 if on else 0))
 

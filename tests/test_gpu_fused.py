@@ -1,0 +1,117 @@
+"""Fused residual path (k_dual_lds_2d FR + k_res_fwdy_fused_2d) vs the float64 oracle and vs the unfused
+kernels (pytest -m gpu).
+
+With rho_alp_iters = 1 the fp32 dual sweep also forms the next primal's continuity residual
+(update_fns_in_pdhg.py:72-96) from the rho', alp' it has just written; the residual kernel only completes
+the terms at its 8-row x 256-column tile edges.  PDHG_FUSE_RES=1 forces the path on grids smaller than the
+default threshold, =0 turns it off.  Bounds: the fp32 bounds of test_gpu_parity (phi 1e-5, rho 2e-4 after
+10 iterations from the seeded state); fused vs unfused device runs agree to fp32 reassociation (1e-5).
+"""
+import numpy as np
+import pytest
+
+from _problems import device_ctx, make_problem, rel
+from test_gpu_parity import SIGMA, TAU, _oracle_iterate
+
+pytestmark = pytest.mark.gpu
+
+FUSED = [
+    # egno, ndim, nx, ny, T, epsl
+    (1, 2, 256, 256, 3, 0.0),
+    (2, 2, 256, 512, 5, 1e-5),   # 2 strips along y: strip-edge columns through p.ey
+    (1, 2, 512, 1024, 4, 1e-5),  # 4 strips, 64 row groups
+    (2, 2, 64, 256, 1, 0.0),     # T = 1: the residual row is formed after the loop only
+    (2, 2, 128, 1024, 2, 1e-4),
+]
+IDS = ["e{}d{}_{}x{}_T{}_eps{}".format(*c) for c in FUSED]
+# epsl = 0.1 at these dx is the reference's unstable regime (explicit sigma*epsl*Lap in the dual, see
+# test_fp32_from_reference_init): fp32 rounding is amplified every iteration, so there the fused path is
+# held to the unfused path's own distance from the oracle
+UNSTABLE = [(2, 2, 256, 512, 3, 0.1), (1, 2, 256, 256, 2, 0.1)]
+UNSTABLE_IDS = ["e{}d{}_{}x{}_T{}_eps{}".format(*c) for c in UNSTABLE]
+
+
+def _ctx(P, fuse, monkeypatch):
+    monkeypatch.setenv("PDHG_FUSE_RES", "1" if fuse else "0")
+    ctx = device_ctx(P, "fp32")
+    assert ctx.path_info("fused_residual") == (1 if fuse else 0)
+    return ctx
+
+
+def _run(P, fuse, n, monkeypatch):
+    ctx = _ctx(P, fuse, monkeypatch)
+    ctx.set_state(P["phi"], P["rho"], P["alp"])
+    st = ctx.iterate(n, TAU, SIGMA, -1.0, 1)
+    assert st["iters_run"] == n and st["status"] == 0
+    out = ctx.get_state()
+    ctx.close()
+    return out, st
+
+
+@pytest.mark.parametrize("case", FUSED, ids=IDS)
+def test_fused_iterate_vs_oracle(native, case, monkeypatch):
+    P = make_problem(*case)
+    n = 10
+    phi_o, rho_o, alp_o, e1_o, e2_o = _oracle_iterate(P, n)
+    (phi_d, rho_d, alp_d), st = _run(P, True, n, monkeypatch)
+    assert rel(phi_d, phi_o) < 1e-5
+    assert rel(rho_d, rho_o) < 2e-4
+    for a_d, a_o in zip(alp_d, alp_o):
+        assert rel(a_d, a_o) < 2e-4
+    assert abs(st["err1"] - e1_o) <= 1e-2 * e1_o
+
+
+@pytest.mark.parametrize("case", UNSTABLE, ids=UNSTABLE_IDS)
+def test_fused_unstable_regime_no_worse_than_unfused(native, case, monkeypatch):
+    P = make_problem(*case)
+    n = 3
+    phi_o, rho_o, alp_o, _, _ = _oracle_iterate(P, n)
+    errs = []
+    for fuse in (False, True):
+        (phi_d, rho_d, alp_d), _ = _run(P, fuse, n, monkeypatch)
+        errs.append([rel(phi_d, phi_o), rel(rho_d, rho_o)] + [rel(a, b) for a, b in zip(alp_d, alp_o)])
+    unf, fus = errs
+    for f, u in zip(fus, unf):
+        assert f <= 2.0 * u + 1e-6, (fus, unf)
+
+
+@pytest.mark.parametrize("case", FUSED, ids=IDS)
+def test_fused_matches_unfused(native, case, monkeypatch):
+    """Same kernels up to where the residual is formed: the states after a few iterations agree to
+    fp32 reassociation, and so do the err1/err2 stop quantities."""
+    P = make_problem(*case)
+    (s0, st0), (s1, st1) = [_run(P, fuse, 4, monkeypatch) for fuse in (False, True)]
+    assert rel(s1[0], s0[0]) < 1e-5
+    assert rel(s1[1], s0[1]) < 1e-5
+    for a1, a0 in zip(s1[2], s0[2]):
+        assert rel(a1, a0) < 1e-5
+    assert abs(st1["err1"] - st0["err1"]) <= 1e-4 * st0["err1"]
+    assert abs(st1["err2"] - st0["err2"]) <= 1e-4 * st0["err2"]
+
+
+def test_fused_dropin_calls_and_state_reset(native, monkeypatch):
+    """The per-call drop-ins (update_primal / update_dual) use the fused residual after a fused dual;
+    set_state invalidates it (the next primal forms the residual from the new rho, alp)."""
+    P = make_problem(2, 2, 256, 512, 3, 1e-5)
+    ref = _ctx(P, False, monkeypatch)
+    ctx = _ctx(P, True, monkeypatch)
+    for c in (ref, ctx):
+        c.set_state(P["phi"], P["rho"], P["alp"])
+        for _ in range(3):
+            c.update_primal(TAU)
+            c.update_dual(SIGMA, -1.0, 1)
+    for a, b in zip(ctx.get_state(), ref.get_state()):
+        if isinstance(a, tuple):
+            for x, y in zip(a, b):
+                assert rel(x, y) < 1e-5
+        else:
+            assert rel(a, b) < 1e-5
+    # new state: a stale fused residual would give the old state's primal
+    rng = np.random.default_rng(7)
+    rho2 = P["rho"] * rng.uniform(0.8, 1.2, P["rho"].shape)
+    for c in (ref, ctx):
+        c.set_state(P["phi"], rho2, P["alp"])
+        c.update_primal(TAU)
+    assert rel(ctx.get_state()[0], ref.get_state()[0]) < 1e-6
+    ref.close()
+    ctx.close()
