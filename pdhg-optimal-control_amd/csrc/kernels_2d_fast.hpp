@@ -247,123 +247,89 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const floa
 }
 
 // Residual rows formed by the fused dual sweep (k_dual_lds_2d<.., FR = true>, 8-row x 256-column tiles)
-// + forward DHT along y.  Completes the terms the sweep could not see (update_fns_in_pdhg.py:83-96):
-// row x0 gets eps*rho'(x0-1)/dx^2 + m1x(x0-1)/dx and row x0+RW-1 gets eps*rho'(x0+RW)/dx^2 - m2x(x0+RW)/dx,
-// both from the rho' / alp' rows (periodic wrap); the first / last column of every 256-wide strip gets
-// eps*rho'/dy^2 +- m/dy of the neighbouring strip's edge column from p.ey.  Then the same in-place
-// 4-line FFT and blocked-layout unpack as k_res_fwdy_fast_2d.  Needs RW = 8 (the sweep's tile height),
-// bc (0, 0), ny % 256 == 0.
+// + forward DHT along y.  Adds the terms the sweep could not form inside its tile
+// (update_fns_in_pdhg.py:83-96), which the neighbouring tiles' sweeps wrote for it: p.ex holds, per tile,
+// eps*rho'(x0-1)/dx^2 + m1x(x0-1)/dx for row x0 and eps*rho'(x0+RW)/dx^2 - m2x(x0+RW)/dx for row x0+RW-1
+// (periodic wrap); p.ey holds eps*rho'/dy^2 +- m/dy of the neighbouring strip's edge column for the first /
+// last column of every 256-wide strip.  Then the same in-place 4-line FFT and blocked-layout unpack as
+// k_res_fwdy_fast_2d.  Needs RW = 8 (the sweep's tile height), bc (0, 0), ny % 256 == 0.
 // Persistent: G workgroups (one per CU: the 4 lines take 139 KiB of LDS) stride over the T * nx/RW
-// row-group tasks, and the next task's rows are loaded into registers while the current one is
-// transformed and stored, so the CU's memory pipe is not idle during the FFT.
-// grid: G <= T * nx/RW; block NT (N/4 % NT == 0); LDS RW/2 * (N + N/16) * 8 B.
+// row-group tasks.  The next task's rows are loaded into registers before the current FFT and its edge rows
+// after it, so the CU's memory pipe is not idle during the transform; its strip-edge terms (RW * ny/256 * 2
+// floats) go through a small LDS double buffer, so only the edge lanes read them.
+// grid: G <= T * nx/RW; block NT (N/4 % NT == 0); LDS RW/2 * (N + N/16) * 8 B (+ 2 * RW * ny/128 floats).
 template <int EGNO, int N, int RW, int NT>
 __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const float2* __restrict__ twy) {
   using C = float2;
   constexpr int NL = RW / 2;
   constexpr int GPT = (N / 4) / NT;
-  constexpr bool PREFETCH_SIDE = NT <= 512;   // 1024 threads (ny = 4096): no registers for it
   constexpr int YW = 256, NSTRIP = N / YW;
+  constexpr int NEY = RW * NSTRIP * 2;   // strip-edge terms of one task
   static_assert(RW == 8 && N % YW == 0 && (N / 4) % NT == 0, "fused residual tiles are 8 rows x 256 columns");
+  static_assert(NEY <= NT, "one strip-edge term per thread");
   if (p.ctrl->done) return;
   extern __shared__ __align__(16) unsigned char smem_raw[];
+  __shared__ float eyl[2][NEY];
   C* A = reinterpret_cast<C*>(smem_raw);
-  const int cur = p.ctrl->cur;
   const int nx = p.nx;
   const int ngx = nx / RW;
   const int ntask = ngx * p.T;
   const size_t plane = (size_t)nx * N;
-  const bool use_eps = p.epsl != 0.f;
   const int B = p.B;
   const int CS4 = RW * B / 4;
   const int nb = p.nb;
-  // next task's inputs: the residual rows are loaded before this task's FFT (they fly during it), the
-  // halo rows and strip-edge values after it (they fly during the unpack and stores)
-  struct Rows {
-    float4 v[RW];              // residual rows x0 .. x0+RW-1
-  };
-  struct Side {
-    float4 rm, a1m, rp, a2p;   // rho', alp1x of row x0-1; rho', alp2x of row x0+RW
-    float2 e[RW];              // strip-edge lanes: the neighbouring strip's (rho', m1y) or (rho', m2y)
-  };
-  auto load_rows = [&](int task, Rows (&in)[GPT]) {
+  const int tid = threadIdx.x;
+  float4 rows[GPT][RW];        // next task's residual rows x0 .. x0+RW-1
+  float4 e0[GPT], e1[GPT];     // next task's edge-row terms (row x0, row x0+RW-1)
+  float ev = 0.f;              // next task's strip-edge term number tid
+  auto load_rows = [&](int task) {
     const int j = task / ngx, x0 = (task - j * ngx) * RW;
+    if (tid < NEY) ev = p.ey[((size_t)j * nx + x0) * NSTRIP * 2 + tid];   // first: waited for alone
     const float* R0 = p.res + (size_t)j * plane + (size_t)x0 * N;
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
-      const int y = 4 * (threadIdx.x + gi * NT);
+      const int y = 4 * (tid + gi * NT);
 #pragma unroll
-      for (int r = 0; r < RW; ++r) in[gi].v[r] = ld4(R0 + (size_t)r * N + y);
+      for (int r = 0; r < RW; ++r) rows[gi][r] = ld4(R0 + (size_t)r * N + y);
     }
   };
-  auto load_side = [&](int task, Side (&in)[GPT]) {
-    const int j = task / ngx, x0 = (task - j * ngx) * RW;
-    const int xm = x0 == 0 ? nx - 1 : x0 - 1, xp = x0 + RW == nx ? 0 : x0 + RW;   // periodic
-    const size_t om = (size_t)j * plane + (size_t)xm * N, op = (size_t)j * plane + (size_t)xp * N;
-    const float2* ey = reinterpret_cast<const float2*>(p.ey) + ((size_t)j * nx + x0) * NSTRIP * 2;
+  auto load_edges = [&](int task) {
+    const int j = task / ngx, tile = task - j * ngx;
+    const float* E = p.ex + ((size_t)j * ngx + tile) * 2 * N;
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
-      const int y = 4 * (threadIdx.x + gi * NT);
-      in[gi].rm = ld4(p.rho[cur] + om + y);
-      in[gi].a1m = ld4(p.alp[cur][0] + om + y);
-      in[gi].rp = ld4(p.rho[cur] + op + y);
-      in[gi].a2p = ld4(p.alp[cur][1] + op + y);
-      // first column of a strip: (rho', m1y) of the previous strip's last column (float2 slot 1);
-      // last column: (rho', m2y) of the next strip's first column (slot 0); other lanes: a dummy read
-      const int s = y / YW, yo = y - s * YW;
-      const bool first = yo == 0, last = yo == YW - 4;
-      const int sn = first ? (s == 0 ? NSTRIP - 1 : s - 1) : (s == NSTRIP - 1 ? 0 : s + 1);
-      const int slot = first ? 2 * sn + 1 : last ? 2 * sn : 0;
-#pragma unroll
-      for (int r = 0; r < RW; ++r) in[gi].e[r] = ey[(size_t)r * NSTRIP * 2 + slot];
+      const int y = 4 * (tid + gi * NT);
+      e0[gi] = ld4(E + y);
+      e1[gi] = ld4(E + N + y);
     }
   };
-  Rows nrow[GPT];
-  Side nside[GPT];
-  int task = blockIdx.x;
+  int task = blockIdx.x, buf = 0;
   if (task < ntask) {
-    load_rows(task, nrow);
-    load_side(task, nside);
+    load_rows(task);
+    load_edges(task);
+    if (tid < NEY) eyl[0][tid] = ev;
   }
-  for (; task < ntask; task += gridDim.x) {
+  __syncthreads();
+  for (; task < ntask; task += gridDim.x, buf ^= 1) {
     const int j = task / ngx, x0 = (task - j * ngx) * RW;
-    const int xm = x0 == 0 ? nx - 1 : x0 - 1, xp = x0 + RW == nx ? 0 : x0 + RW;
-    const float axm = p.ax[xm], axp = p.ax[xp];
-    if (!PREFETCH_SIDE && task != (int)blockIdx.x) load_side(task, nside);
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
-      const int y = 4 * (threadIdx.x + gi * NT);
-      const Side& in = nside[gi];
+      const int y = 4 * (tid + gi * NT);
       float4 v[RW];
 #pragma unroll
-      for (int r = 0; r < RW; ++r) v[r] = nrow[gi].v[r];
+      for (int r = 0; r < RW; ++r) v[r] = rows[gi][r];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float m1 = m1f<EGNO>(f4(in.rm, e), f4(in.a1m, e), axm);
-        const float m2 = m2f<EGNO>(f4(in.rp, e), f4(in.a2p, e), axp);
-        float c0 = m1 * p.inv_dx, c7 = -m2 * p.inv_dx;
-        if (use_eps) {
-          c0 = c0 + p.epsl * (f4(in.rm, e) * p.inv_dx2);
-          c7 = c7 + p.epsl * (f4(in.rp, e) * p.inv_dx2);
-        }
-        f4set(v[0], e, f4(v[0], e) + c0);
-        f4set(v[RW - 1], e, f4(v[RW - 1], e) + c7);
+        f4set(v[0], e, f4(v[0], e) + f4(e0[gi], e));
+        f4set(v[RW - 1], e, f4(v[RW - 1], e) + f4(e1[gi], e));
       }
-      const int yo = y & (YW - 1);
+      const int s = y / YW, yo = y - s * YW;
       if (yo == 0) {
 #pragma unroll
-        for (int r = 0; r < RW; ++r) {
-          float c = in.e[r].y * p.inv_dy;
-          if (use_eps) c = c + p.epsl * (in.e[r].x * p.inv_dy2);
-          v[r].x += c;
-        }
+        for (int r = 0; r < RW; ++r) v[r].x += eyl[buf][(r * NSTRIP + s) * 2];
       } else if (yo == YW - 4) {
 #pragma unroll
-        for (int r = 0; r < RW; ++r) {
-          float c = -in.e[r].y * p.inv_dy;
-          if (use_eps) c = c + p.epsl * (in.e[r].x * p.inv_dy2);
-          v[r].w += c;
-        }
+        for (int r = 0; r < RW; ++r) v[r].w += eyl[buf][(r * NSTRIP + s) * 2 + 1];
       }
 #pragma unroll
       for (int r = 0; r < RW; ++r) {
@@ -373,12 +339,15 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
       }
     }
     const bool more = task + (int)gridDim.x < ntask;
-    if (more) load_rows(task + gridDim.x, nrow);
+    if (more) load_rows(task + gridDim.x);
     lds_sync();
     lds_fft_inplace<C, N, NL, NT>(A, twy);
-    if (PREFETCH_SIDE && more) load_side(task + gridDim.x, nside);
+    if (more) {
+      if (tid < NEY) eyl[buf ^ 1][tid] = ev;   // read one barrier after its last use two tasks ago
+      load_edges(task + gridDim.x);
+    }
     float* wk = p.work + (size_t)j * nb * nx * B;
-    for (int t = threadIdx.x; t < nb * CS4; t += NT) {
+    for (int t = tid; t < nb * CS4; t += NT) {
       const int b = t / CS4, part = t - b * CS4;
       float4 v;
 #pragma unroll

@@ -20,9 +20,10 @@ namespace pdhg {
 // fluxes m = (rho'+1e-4) f(alp') are exchanged between the waves through a second LDS double buffer
 // (x neighbours) and the adjacent lanes (y neighbours); R_j needs rho'_{j+1}, so it is completed and
 // stored one step later (R_{T-1} with rho_T = 0 and + c/dt after the loop).  Terms that need values
-// outside the workgroup's 8 x 256 tile are left out: the rows x0-1 / x0+RX (added by
-// k_res_fwdy_fused_2d from the rho', alp' rows themselves) and the columns outside the 256-wide strip
-// (added from p.ey, where the strip's first / last columns leave [rho', m2y] / [rho', m1y]).
+// outside the workgroup's 8 x 256 tile are left out of R; instead each sweep writes the terms its own
+// edge rows / columns contribute to the neighbouring tiles (p.ex: eps rho'/dx^2 + m1x/dx of row x0+RX-1
+// for the next tile's first row, eps rho'/dx^2 - m2x/dx of row x0 for the previous tile's last row;
+// p.ey: likewise per strip-edge column with m1y / m2y), and k_res_fwdy_fused_2d adds them.
 template <int EGNO, int RX, bool FR = false>
 __global__ void __launch_bounds__(RX * 64, FR ? 2 : 3) k_dual_lds_2d(KP<float> p, int jchunk, int jbase, int jend,
                                                                      int zbase) {
@@ -189,9 +190,32 @@ __global__ void __launch_bounds__(RX * 64, FR ? 2 : 3) k_dual_lds_2d(KP<float> p
           yeps[e] = p.epsl * ((hi + lo - 2.f * r0) * p.inv_dy2);
           ydiv[e] = (m1y[e] - m1l) * p.inv_dy + (m2h - m2y[e]) * p.inv_dy;
         }
-        float* eyr = p.ey + (((size_t)j * nx + x) * nstrip + blockIdx.y) * 4;
-        if (lane == 0) *reinterpret_cast<float2*>(eyr) = make_float2(rn4.x, m2y[0]);
-        if (lane == kWave - 1) *reinterpret_cast<float2*>(eyr + 2) = make_float2(rn4.w, m1y[3]);
+        // the neighbouring strips' outer-column terms that need this strip's edge column: lane 0 feeds the
+        // previous strip's last column (eps rho'/dy^2 - m2y/dy), lane 63 the next strip's first column
+        // (eps rho'/dy^2 + m1y/dy); k_res_fwdy_fused_2d adds them (p.ey)
+        if (lane == 0 || lane == kWave - 1) {
+          const bool first = lane == 0;
+          float c = first ? -m2y[0] * p.inv_dy : m1y[3] * p.inv_dy;
+          if (use_eps) c = c + p.epsl * ((first ? rn4.x : rn4.w) * p.inv_dy2);
+          const int sy = first ? (blockIdx.y == 0 ? nstrip - 1 : blockIdx.y - 1)
+                               : (blockIdx.y + 1 == nstrip ? 0 : blockIdx.y + 1);
+          p.ey[(((size_t)j * nx + x) * nstrip + sy) * 2 + (first ? 1 : 0)] = c;
+        }
+        // likewise the neighbouring tiles' edge rows (wave-uniform): the last wave feeds row 0 of the next
+        // tile (eps rho'/dx^2 + m1x/dx), wave 0 row RX-1 of the previous tile (eps rho'/dx^2 - m2x/dx) (p.ex)
+        if (r == 0 || r == RX - 1) {
+          const bool top = r == 0;
+          const int ngx = nx / RX, tile = x0 / RX;
+          const int tt = top ? (tile == 0 ? ngx - 1 : tile - 1) : (tile + 1 == ngx ? 0 : tile + 1);
+          float4 c;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float v = top ? -f4(m2x4, e) * p.inv_dx : f4(m1x4, e) * p.inv_dx;
+            if (use_eps) v = v + p.epsl * (f4(rn4, e) * p.inv_dx2);
+            f4set(c, e, v);
+          }
+          st4(p.ex + (((size_t)j * ngx + tt) * 2 + (top ? 1 : 0)) * ny + y, c);
+        }
       }
       if (j + 1 < j1) {     // uniform over the workgroup
         stage(nxt, buf ^ 1);

@@ -48,7 +48,8 @@ struct KP {
   const cplx<R>* dctw;     // e^{-i pi k / 2nx}, k < nx (DCT only)
   // fused residual (k_dual_lds_2d FR / k_res_fwdy_fused_2d): residual rows formed by the dual sweep
   R* res;                  // [T][nx][ny]
-  R* ey;                   // [T][nx][ny/256][4]: strip edge columns (rho', m2y first; rho', m1y last)
+  R* ex;                   // [T][nx/8][2][ny]: tile-edge row terms (0: row x0 from x0-1, 1: row x0+7 from x0+8)
+  R* ey;                   // [T][nx][ny/256][2]: strip-edge column terms (0: first column, 1: last column)
 };
 
 // neighbour index along an axis of length n with boundary condition bc

@@ -348,10 +348,11 @@ struct Impl : ImplBase {
       if ((rc = alloc(&g, (size_t)gx1 * 2 * nx))) return rc;
       p.gscr = g;
     }
-    p.res = p.ey = nullptr;
+    p.res = p.ex = p.ey = nullptr;
     if (fuse_res) {
       if ((rc = alloc(&p.res, (size_t)T * npl))) return rc;
-      if ((rc = alloc(&p.ey, (size_t)T * nx * (ny / 256) * 4))) return rc;
+      if ((rc = alloc(&p.ex, (size_t)T * (nx / 8) * 2 * ny))) return rc;
+      if ((rc = alloc(&p.ey, (size_t)T * nx * (ny / 256) * 2))) return rc;
     }
     if (slab) {
       Mspec = (size_t)p.nb * nx * p.B;
@@ -1273,12 +1274,11 @@ struct Impl : ImplBase {
       if (d2) return S * N * (14.0 + 11.0 * k + 5.0 * (k > 1));
       return S * N * (12.0 + 7.0 * k + 3.0 * (k > 1));
     }
-    // fused residual: the dual also writes the residual rows (+1, plus the strip-edge columns), the
-    // residual kernel reads them, the halo rows rho'/alp' x0-1 and x0+8 (4 rows per 8) and the edge
-    // columns, and writes the spectrum
-    const double ey = fuse_res ? 4.0 / 256.0 : 0.0;
-    if (cls == "dual") return S * N * (1.0 + 2.0 * nr + (fuse_res ? 1.0 + ey : 0.0));
-    if (cls == "residual") return S * N * (fuse_res ? 2.5 + ey : nr + 1.0);
+    // fused residual: the dual also writes the residual rows (+1), the tile-edge row terms (2 rows per 8)
+    // and the strip-edge column terms (2 per 256); the residual kernel reads them and writes the spectrum
+    const double edge = fuse_res ? 2.0 / 8.0 + 2.0 / 256.0 : 0.0;
+    if (cls == "dual") return S * N * (1.0 + 2.0 * nr + (fuse_res ? 1.0 + edge : 0.0));
+    if (cls == "residual") return S * N * (fuse_res ? 2.0 + edge : nr + 1.0);
     if (cls == "precond") return S * N * (d2 ? 4.0 : 2.0);   // 2-D: x-DHT+Thomas fwd (2N) + bwd+x-DHT (2N)
     if (cls == "update") return S * N * 4.0;                 // read U, phi; write phi, phi_bar
     return -1.0;
