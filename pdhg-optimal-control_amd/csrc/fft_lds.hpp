@@ -313,6 +313,10 @@ struct TwLds {
   static constexpr int SIZE = 3 * ((N > 16 ? 16 : 0) + (N > 256 ? 256 : 0) + (N > 4096 ? 4096 : 0));
 };
 __host__ __device__ constexpr int twlds_off(int LS) { return LS >= 4096 ? 816 : LS >= 256 ? 48 : 0; }
+// complex entries of TwLds<n> (host side: LDS sizing of the kernels that keep the table)
+__host__ __device__ constexpr int twlds_size(int n) {
+  return 3 * ((n > 16 ? 16 : 0) + (n > 256 ? 256 : 0) + (n > 4096 ? 4096 : 0));
+}
 
 template <typename C, int N, int NL, int NT, int LS, int R, bool REG>
 __device__ __forceinline__ void inplace_pass(C* __restrict__ a, const C* __restrict__ tw, const C* twl) {

@@ -271,6 +271,11 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
   extern __shared__ __align__(16) unsigned char smem_raw[];
   __shared__ float eyl[2][NEY];
   C* A = reinterpret_cast<C*>(smem_raw);
+  // twiddle seeds in LDS behind the lines (N <= 4096): the passes then issue no global loads, so the next
+  // task's rows stay in flight across the whole transform (vmcnt drains in order)
+  constexpr bool TWL = N <= 4096;
+  C* twl = A + NL * Pad<N>::LINE;
+  if constexpr (TWL) fill_twlds<C, N>(twl, twy);
   const int nx = p.nx;
   const int ngx = nx / RW;
   const int ntask = ngx * p.T;
@@ -341,7 +346,8 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
     const bool more = task + (int)gridDim.x < ntask;
     if (more) load_rows(task + gridDim.x);
     lds_sync();
-    lds_fft_inplace<C, N, NL, NT>(A, twy);
+    if constexpr (TWL) lds_fft_inplace_tl<C, N, NL, NT>(A, twl);
+    else lds_fft_inplace<C, N, NL, NT>(A, twy);
     if (more) {
       if (tid < NEY) eyl[buf ^ 1][tid] = ev;   // read one barrier after its last use two tasks ago
       load_edges(task + gridDim.x);
@@ -376,6 +382,9 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
   extern __shared__ __align__(16) unsigned char smem_raw[];
   C* A = reinterpret_cast<C*>(smem_raw);
   float* Af = reinterpret_cast<float*>(A);
+  constexpr bool TWL = N <= 4096;   // twiddle seeds in LDS (see k_res_fwdy_fused_2d)
+  C* twl = A + NL * Pad<N>::LINE;
+  if constexpr (TWL) fill_twlds<C, N>(twl, twy);
   const int nx = p.nx, B = p.B, nb = p.nb;
   const int ngx = nx / RW;
   const int ntask = ngx * p.T;
@@ -410,7 +419,8 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
     float4 nx0, nx1;
     ldpair(0, 0, nx0, nx1);
     lds_sync();
-    if (!(p.dbg & 16)) lds_fft_inplace<C, N, NL, NT>(A, twy);
+    if constexpr (TWL) lds_fft_inplace_tl<C, N, NL, NT>(A, twl);
+    else lds_fft_inplace<C, N, NL, NT>(A, twy);
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
       const int y = 4 * (threadIdx.x + gi * NT);

@@ -119,7 +119,7 @@ struct Impl : ImplBase {
   bool ws_xt = false;             // warp-specialised variant (k_precond_xt_ws_2d)            // fp32 power-of-two nx: k_precond_xt_fast_2d
   size_t lds_fast_xt = 0;
   int RWf = 8, NTf = 1024, g_fast_upd = 1;
-  size_t lds_fast = 0;
+  size_t lds_fast = 0, lds_fast_tw = 0;
   size_t partial_rows = 0;
   bool primal_done = false;
   int stop_conv = 1, stop_nan = 1;   // reference stop rules (utils_pdhg_solver.py:74-80)
@@ -277,6 +277,8 @@ struct Impl : ImplBase {
             if (v >= 1 && (v == 1 || (nx / RWf) % 4 == 0)) p.tile_j = v;
           }
           lds_fast = (size_t)(RWf / 2) * (ny + ny / 16) * sizeof(C);
+          // + the twiddle-seed table of the persistent kernels (fused residual, update; ny <= 4096)
+          lds_fast_tw = lds_fast + (ny <= 4096 ? (size_t)twlds_size(ny) * sizeof(C) : 0);
           g_fast_upd = std::min((nx / RWf) * T, 2048);
         }
       }
@@ -561,11 +563,11 @@ struct Impl : ImplBase {
         if constexpr (sizeof(R) == 4 && RW_ == 8 && N_ % 256 == 0 && (N_ / 4) % NTF == 0) {
           const dim3 g(std::min((pb.nx / RW_) * pb.T, n_cu));   // persistent, one workgroup per CU (LDS)
           if (pb.egno == 1) {
-            if ((r2 = ensure_lds(k_res_fwdy_fused_2d<1, N_, RW_, NTF>, lds_fast))) return r2;
-            hipLaunchKernelGGL((k_res_fwdy_fused_2d<1, N_, RW_, NTF>), g, dim3(NTF), lds_fast, stream, p, twy);
+            if ((r2 = ensure_lds(k_res_fwdy_fused_2d<1, N_, RW_, NTF>, lds_fast_tw))) return r2;
+            hipLaunchKernelGGL((k_res_fwdy_fused_2d<1, N_, RW_, NTF>), g, dim3(NTF), lds_fast_tw, stream, p, twy);
           } else {
-            if ((r2 = ensure_lds(k_res_fwdy_fused_2d<2, N_, RW_, NTF>, lds_fast))) return r2;
-            hipLaunchKernelGGL((k_res_fwdy_fused_2d<2, N_, RW_, NTF>), g, dim3(NTF), lds_fast, stream, p, twy);
+            if ((r2 = ensure_lds(k_res_fwdy_fused_2d<2, N_, RW_, NTF>, lds_fast_tw))) return r2;
+            hipLaunchKernelGGL((k_res_fwdy_fused_2d<2, N_, RW_, NTF>), g, dim3(NTF), lds_fast_tw, stream, p, twy);
           }
           return (int)PDHG_OK;
         }
@@ -698,8 +700,8 @@ struct Impl : ImplBase {
           constexpr int N_ = decltype(Nc)::value, RW_ = decltype(RWc)::value, NT_ = decltype(NTc)::value;
           int r2;
           if constexpr (sizeof(R) == 4) {
-            if ((r2 = ensure_lds(k_invy_update_fast_2d<N_, RW_, NT_>, lds_fast))) return r2;
-            hipLaunchKernelGGL((k_invy_update_fast_2d<N_, RW_, NT_>), dim3(g_fast_upd), dim3(NT_), lds_fast, stream,
+            if ((r2 = ensure_lds(k_invy_update_fast_2d<N_, RW_, NT_>, lds_fast_tw))) return r2;
+            hipLaunchKernelGGL((k_invy_update_fast_2d<N_, RW_, NT_>), dim3(g_fast_upd), dim3(NT_), lds_fast_tw, stream,
                                p, twy);
           }
           return (int)PDHG_OK;
