@@ -228,15 +228,16 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const floa
   // Hartley unpack -> blocked layout: chunk (j, b, x0..x0+RW-1, 0..B-1) = RW*B contiguous floats
   const int B = p.B;
   const int CS4 = RW * B / 4;                 // float4 per chunk
+  const int lCS4 = p.lB + (RW == 8 ? 1 : RW == 4 ? 0 : RW == 2 ? -1 : -2);   // log2(CS4), B power of two
   const int nb = p.nb;
   float* wk = p.work + (size_t)j * nb * nx * B;
   for (int t = threadIdx.x; t < nb * CS4; t += NT) {
-    const int b = t / CS4, part = t - b * CS4;
+    const int b = t >> lCS4, part = t & (CS4 - 1);
     float4 v;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int f = part * 4 + e;
-      const int r = f / B, c = f - r * B;
+      const int r = f >> p.lB, c = f & (B - 1);
       const int ky = b * B + c;
       float ha = 0.f, hb = 0.f;
       if (ky < N) hartley_padded<C, float>(A + (r >> 1) * Pad<N>::LINE, N, ky, ha, hb);
@@ -282,6 +283,7 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
   const size_t plane = (size_t)nx * N;
   const int B = p.B;
   const int CS4 = RW * B / 4;
+  const int lCS4 = p.lB + (RW == 8 ? 1 : RW == 4 ? 0 : RW == 2 ? -1 : -2);   // log2(CS4), B power of two
   const int nb = p.nb;
   const int tid = threadIdx.x;
   float4 rows[GPT][RW];        // next task's residual rows x0 .. x0+RW-1
@@ -354,12 +356,12 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
     }
     float* wk = p.work + (size_t)j * nb * nx * B;
     for (int t = tid; t < nb * CS4; t += NT) {
-      const int b = t / CS4, part = t - b * CS4;
+      const int b = t >> lCS4, part = t & (CS4 - 1);
       float4 v;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int f = part * 4 + e;
-        const int r = f / B, c = f - r * B;
+        const int r = f >> p.lB, c = f & (B - 1);
         const int ky = b * B + c;
         float ha = 0.f, hb = 0.f;
         if (ky < N) hartley_padded<C, float>(A + (r >> 1) * Pad<N>::LINE, N, ky, ha, hb);
@@ -391,28 +393,31 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
   const size_t plane = (size_t)nx * N;
   const float scale = p.tau * p.inv_n;
   const int CS4 = RW * B / 4;
+  const int lB = p.lB;
+  const int lCS4 = lB + (RW == 8 ? 1 : RW == 4 ? 0 : RW == 2 ? -1 : -2);   // log2(CS4), B power of two
+  const int tid = threadIdx.x;
   double s[3] = {0.0, 0.0, 0.0};
+  // Per task: the spectrum goes to LDS, the first old-phi row pair is issued, and the transform runs on
+  // LDS only (twiddle seeds in LDS), so that pair stays in flight across it; each pair prefetches the next.
   for (int task = xcd_remap(blockIdx.x, gridDim.x); task < ntask; task += gridDim.x) {
     const int j = task / ngx;
     const int x0 = (task - j * ngx) * RW;
     const float* wk = p.work + (size_t)j * nb * nx * B;
-    for (int t = threadIdx.x; t < nb * CS4; t += NT) {
-      const int b = t / CS4, part = t - b * CS4;
+    for (int t = tid; t < nb * CS4; t += NT) {
+      const int b = t >> lCS4, part = t & (CS4 - 1);
       const float4 v = ld4(wk + ((size_t)b * nx + x0) * B + part * 4);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int f = part * 4 + e;
-        const int r = f / B, c = f - r * B;
+        const int r = f >> lB, c = f & (B - 1);
         const int ky = b * B + c;
         if (ky < N) Af[((r >> 1) * Pad<N>::LINE + pix(ky)) * 2 + (r & 1)] = f4(v, e);
       }
     }
     float* phi = p.phi + (size_t)(j + 1) * plane;
     float* pbar = p.phibar + (size_t)(j + 1) * plane;
-    // old phi of rows (0, 1): issued now, consumed after the transform (LDS-only barriers keep
-    // them in flight); each row pair prefetches the next pair while it computes
     auto ldpair = [&](int gi, int l, float4& o0, float4& o1) {
-      const size_t idx = (size_t)(x0 + 2 * l) * N + 4 * (threadIdx.x + gi * NT);
+      const size_t idx = (size_t)(x0 + 2 * l) * N + 4 * (tid + gi * NT);
       o0 = ld4(phi + idx);
       o1 = ld4(phi + idx + N);
     };
@@ -423,7 +428,7 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
     else lds_fft_inplace<C, N, NL, NT>(A, twy);
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
-      const int y = 4 * (threadIdx.x + gi * NT);
+      const int y = 4 * (tid + gi * NT);
 #pragma unroll
       for (int l = 0; l < NL; ++l) {   // rows 2l (real part) and 2l+1 (imaginary part) of line l
         const float4 o4[2] = {nx0, nx1};

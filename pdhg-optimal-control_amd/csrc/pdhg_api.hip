@@ -101,6 +101,7 @@ struct Impl : ImplBase {
   int NT2 = 512;
   int gx1 = 0, gx4 = 0, g4 = 1, gx5 = 0, g5 = 1, g_outer = 1;
   int rows_var = 0;                       // row-kernel shape variant (see with_fast_rows)
+  int half_nt = 1;                        // ny = 4096 row kernels with 512 threads (bit 0 residual, bit 1 update)
   bool fast_dual = false;                 // fp32 time-marching float4 dual kernel (k_dual_fast_2d)
   int NTd = 256, gxd = 0, gyd = 0, gzd = 0, jchunk_d = 1;
   int dual_rx = 0;   // > 0: k_dual_lds_2d with dual_rx x rows per workgroup (x neighbours through LDS)
@@ -261,6 +262,7 @@ struct Impl : ImplBase {
         gzd = (T + jchunk_d - 1) / jchunk_d;
       }
       if (const char* e = getenv("PDHG_ROWS_VAR")) rows_var = atoi(e);   // tuning override
+      if (const char* e = getenv("PDHG_HALF_NT")) half_nt = atoi(e);     // tuning: 1 fused residual, 2 update
       if (sizeof(R) == 4 && ply.pow2 && ny >= 256 && ny <= 8192) {
         RWf = (ny == 8192) ? 4 : 8;
         NTf = std::min(1024, ny / 4);
@@ -559,17 +561,24 @@ struct Impl : ImplBase {
       rc = with_fast_rows([&](auto Nc, auto RWc, auto NTc) {
         constexpr int N_ = decltype(Nc)::value, RW_ = decltype(RWc)::value, NT_ = decltype(NTc)::value;
         int r2;
-        constexpr int NTF = NT_;
-        if constexpr (sizeof(R) == 4 && RW_ == 8 && N_ % 256 == 0 && (N_ / 4) % NTF == 0) {
+        if constexpr (sizeof(R) == 4 && RW_ == 8 && N_ % 256 == 0 && (N_ / 4) % NT_ == 0) {
           const dim3 g(std::min((pb.nx / RW_) * pb.T, n_cu));   // persistent, one workgroup per CU (LDS)
-          if (pb.egno == 1) {
-            if ((r2 = ensure_lds(k_res_fwdy_fused_2d<1, N_, RW_, NTF>, lds_fast_tw))) return r2;
-            hipLaunchKernelGGL((k_res_fwdy_fused_2d<1, N_, RW_, NTF>), g, dim3(NTF), lds_fast_tw, stream, p, twy);
-          } else {
-            if ((r2 = ensure_lds(k_res_fwdy_fused_2d<2, N_, RW_, NTF>, lds_fast_tw))) return r2;
-            hipLaunchKernelGGL((k_res_fwdy_fused_2d<2, N_, RW_, NTF>), g, dim3(NTF), lds_fast_tw, stream, p, twy);
+          auto go = [&](auto ntc) {
+            constexpr int NTF = decltype(ntc)::value;
+            int r3;
+            if (pb.egno == 1) {
+              if ((r3 = ensure_lds(k_res_fwdy_fused_2d<1, N_, RW_, NTF>, lds_fast_tw))) return r3;
+              hipLaunchKernelGGL((k_res_fwdy_fused_2d<1, N_, RW_, NTF>), g, dim3(NTF), lds_fast_tw, stream, p, twy);
+            } else {
+              if ((r3 = ensure_lds(k_res_fwdy_fused_2d<2, N_, RW_, NTF>, lds_fast_tw))) return r3;
+              hipLaunchKernelGGL((k_res_fwdy_fused_2d<2, N_, RW_, NTF>), g, dim3(NTF), lds_fast_tw, stream, p, twy);
+            }
+            return (int)PDHG_OK;
+          };
+          if constexpr (NT_ == 1024) {
+            if (half_nt & 1) return go(std::integral_constant<int, 512>{});
           }
-          return (int)PDHG_OK;
+          return go(std::integral_constant<int, NT_>{});
         }
         return fail(PDHG_ERR_STATE, "fused residual without 8-row fast kernels (ny=%d)", pb.ny);
       });
@@ -700,6 +709,14 @@ struct Impl : ImplBase {
           constexpr int N_ = decltype(Nc)::value, RW_ = decltype(RWc)::value, NT_ = decltype(NTc)::value;
           int r2;
           if constexpr (sizeof(R) == 4) {
+            if constexpr (NT_ == 1024 && RW_ == 8) {
+              if (half_nt & 2) {
+                if ((r2 = ensure_lds(k_invy_update_fast_2d<N_, RW_, 512>, lds_fast_tw))) return r2;
+                hipLaunchKernelGGL((k_invy_update_fast_2d<N_, RW_, 512>), dim3(g_fast_upd), dim3(512), lds_fast_tw,
+                                   stream, p, twy);
+                return (int)PDHG_OK;
+              }
+            }
             if ((r2 = ensure_lds(k_invy_update_fast_2d<N_, RW_, NT_>, lds_fast_tw))) return r2;
             hipLaunchKernelGGL((k_invy_update_fast_2d<N_, RW_, NT_>), dim3(g_fast_upd), dim3(NT_), lds_fast_tw, stream,
                                p, twy);
