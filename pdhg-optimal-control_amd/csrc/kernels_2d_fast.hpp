@@ -396,6 +396,8 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
   const int lB = p.lB;
   const int lCS4 = lB + (RW == 8 ? 1 : RW == 4 ? 0 : RW == 2 ? -1 : -2);   // log2(CS4), B power of two
   const int tid = threadIdx.x;
+  constexpr int NLD = RW * N / 4 / NT, BATCH = NLD < 8 ? NLD : 8;
+  static_assert((RW * N / 4) % NT == 0 && NLD % BATCH == 0, "whole spectrum batches per thread");
   double s[3] = {0.0, 0.0, 0.0};
   // Per task: the spectrum goes to LDS, the first old-phi row pair is issued, and the transform runs on
   // LDS only (twiddle seeds in LDS), so that pair stays in flight across it; each pair prefetches the next.
@@ -403,15 +405,29 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
     const int j = task / ngx;
     const int x0 = (task - j * ngx) * RW;
     const float* wk = p.work + (size_t)j * nb * nx * B;
-    for (int t = tid; t < nb * CS4; t += NT) {
-      const int b = t >> lCS4, part = t & (CS4 - 1);
-      const float4 v = ld4(wk + ((size_t)b * nx + x0) * B + part * 4);
+    // the task's spectrum (RW*B/4 float4 per block, N/B blocks = NLD per thread), in batches of up to 8
+    // loads issued together: one memory round trip per batch, not per float4.  The thread index is
+    // laundered per task so the 4*BATCH LDS addresses are not hoisted out of the task loop (registers).
+    int tl = tid;
+    asm volatile("" : "+v"(tl));
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int f = part * 4 + e;
-        const int r = f >> lB, c = f & (B - 1);
-        const int ky = b * B + c;
-        if (ky < N) Af[((r >> 1) * Pad<N>::LINE + pix(ky)) * 2 + (r & 1)] = f4(v, e);
+    for (int i0 = 0; i0 < NLD; i0 += BATCH) {
+      float4 v[BATCH];
+#pragma unroll
+      for (int i = 0; i < BATCH; ++i) {
+        const int t = tl + (i0 + i) * NT;
+        v[i] = ld4(wk + ((size_t)(t >> lCS4) * nx + x0) * B + (t & (CS4 - 1)) * 4);
+      }
+#pragma unroll
+      for (int i = 0; i < BATCH; ++i) {
+        const int t = tl + (i0 + i) * NT;
+        const int b = t >> lCS4, part = t & (CS4 - 1);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int f = part * 4 + e;
+          const int r = f >> lB, c = f & (B - 1);
+          Af[((r >> 1) * Pad<N>::LINE + pix(b * B + c)) * 2 + (r & 1)] = f4(v[i], e);
+        }
       }
     }
     float* phi = p.phi + (size_t)(j + 1) * plane;

@@ -101,7 +101,7 @@ struct Impl : ImplBase {
   int NT2 = 512;
   int gx1 = 0, gx4 = 0, g4 = 1, gx5 = 0, g5 = 1, g_outer = 1;
   int rows_var = 0;                       // row-kernel shape variant (see with_fast_rows)
-  int half_nt = 1;                        // ny = 4096 row kernels with 512 threads (bit 0 residual, bit 1 update)
+  int half_nt = 3;                        // ny = 4096 row kernels with 512 threads (bit 0 residual, bit 1 update)
   bool fast_dual = false;                 // fp32 time-marching float4 dual kernel (k_dual_fast_2d)
   int NTd = 256, gxd = 0, gyd = 0, gzd = 0, jchunk_d = 1;
   int dual_rx = 0;   // > 0: k_dual_lds_2d with dual_rx x rows per workgroup (x neighbours through LDS)
