@@ -206,6 +206,38 @@ int pdhg_slab_plane_out(pdhg_ctx* ctx, int which, void* dst); /* 0 rho row 0, 1 
 int pdhg_slab_plane_in(pdhg_ctx* ctx, int which, const void* src); /* 0 rho halo, 1 phi_bar row 0 */
 int pdhg_slab_status(pdhg_ctx* ctx, pdhg_stats* st);
 
+/* ---------------- x-slab decomposition (multi-GPU for T = 1 marching windows) -----------
+ * New capability (the reference has no distributed path).  The reference's default marches windows of
+ * T = time_step_per_PDHG - 1 = 1 rows (run_example.py:425, utils_pdhg_solver.py:121-206), which a t-slab
+ * cannot split; an x-slab splits the GLOBAL grid's nx rows into nranks contiguous slabs of nloc = nx/nranks
+ * rows (a multiple of 8), one context per GPU.  `p` describes the global problem (nx, xs global).  The
+ * context's spatial arrays are local: nx_local = nloc + 16 rows, row i = global row (x0 - xl0 + i) mod nx,
+ * live rows [xl0, xl0 + nloc) (xl0 = 8); pdhg_set_state / get_state / init_state take and return arrays of
+ * that shape (ghost and padding rows filled from the global arrays by periodic wrap).  One outer iteration
+ * of utils_pdhg_solver.py:51-88:
+ *   halo_out(0, buf) -> [allgather] -> halo_in(0, left's, right's) -> residual -> wire(0, send)
+ *   -> [all-to-all] -> wire(1, recv) -> precond -> wire(2, send) -> [all-to-all] -> wire(3, recv)
+ *   -> update(tau, sums) -> halo_out(1, buf) -> [allgather] || [allreduce sums] -> slab_primal_finalize(sums)
+ *   -> halo_in(1, left's, right's) -> slab_dual(sigma, k, s, sums, 3) -> [allreduce] -> slab_dual_finalize ...
+ *   -> slab_outer -> [allreduce when k > 1] -> slab_outer_finalize   (the t-slab phase functions).
+ * halo_out: [2][nq][T][ny] (nq = 1 + live controls for which 0 = rho/alp of the current set, 1 for
+ * which 1 = phi_bar rows 1..T); side 0 = the first live row (to the left neighbour), side 1 = the last.
+ * halo_in takes the left neighbour's and the right neighbour's halo_out buffers (periodic ring).
+ * wire: [nranks][T][nb/nranks][nloc][B] floats (pdhg_xslab_sizes), chunk q = for / from rank q; stage 0
+ * packs the y-transformed rows, 1 unpacks the received rows into whole x lines, 2 packs the
+ * preconditioned lines, 3 unpacks them back into rows.  fp32, ndim 2, bc (0,0), power-of-two ny in
+ * [256, 8192], (ny/B) % nranks == 0. */
+int pdhg_create_xslab(const pdhg_problem* p, int rank, int nranks, int device, pdhg_ctx** out);
+int pdhg_xslab_layout(pdhg_ctx* ctx, int* x0, int* nloc, int* nx_local, int* xl0);
+int pdhg_xslab_sizes(pdhg_ctx* ctx, unsigned long long* wire, unsigned long long* halo_state,
+                     unsigned long long* halo_phibar);                     /* float counts */
+int pdhg_xslab_halo_out(pdhg_ctx* ctx, int which, void* dst);
+int pdhg_xslab_halo_in(pdhg_ctx* ctx, int which, const void* from_left, const void* from_right);
+int pdhg_xslab_residual(pdhg_ctx* ctx);                                    /* residual + y-DHT, local rows */
+int pdhg_xslab_wire(pdhg_ctx* ctx, int stage, void* buf);
+int pdhg_xslab_precond(pdhg_ctx* ctx);                                     /* x-DHT, Thomas, inverse x-DHT */
+int pdhg_xslab_update(pdhg_ctx* ctx, double tau, double* sums);            /* inverse y-DHT + update + sums */
+
 #ifdef __cplusplus
 }
 #endif

@@ -404,6 +404,7 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
   for (int task = xcd_remap(blockIdx.x, gridDim.x); task < ntask; task += gridDim.x) {
     const int j = task / ngx;
     const int x0 = (task - j * ngx) * RW;
+    if (x0 + RW <= p.xl0 || x0 >= p.xl1) continue;   // x-slab padding / ghost rows only (workgroup-uniform)
     const float* wk = p.work + (size_t)j * nb * nx * B;
     // the task's spectrum (RW*B/4 float4 per block, N/B blocks = NLD per thread), in batches of up to 8
     // loads issued together: one memory round trip per batch, not per float4.  The thread index is
@@ -461,7 +462,9 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
         }
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const size_t idx = (size_t)(x0 + 2 * l + h) * N + y;
+          const int xr = x0 + 2 * l + h;
+          if (xr < p.xl0 || xr >= p.xl1) continue;   // x-slab ghost row (workgroup-uniform)
+          const size_t idx = (size_t)xr * N + y;
           float4 nw, pb;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {

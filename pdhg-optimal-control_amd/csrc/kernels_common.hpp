@@ -70,7 +70,12 @@ __global__ void __launch_bounds__(256) k_outer_sums(KP<R> p, size_t n) {
   const int cur = p.ctrl->cur;
   double s[kNumSums];
   for (int i = 0; i < kNumSums; ++i) s[i] = 0.0;
+  const bool all_rows = p.xl0 == 0 && p.xl1 == p.nx;   // else x-slab: live rows [xl0, xl1) only
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    if (!all_rows) {
+      const int x = (int)((i / p.ny) % p.nx);
+      if (x < p.xl0 || x >= p.xl1) continue;
+    }
     const double ri = p.rho[cur][i], rf = p.rho[1 - cur][i];
     s[0] += (rf - ri) * (rf - ri);
     s[2] += ri * ri;

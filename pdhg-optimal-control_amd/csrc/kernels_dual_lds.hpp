@@ -43,6 +43,7 @@ __global__ void __launch_bounds__(RX * 64, FR ? 2 : 3) k_dual_lds_2d(KP<float> p
   const int lane = threadIdx.x & 63, r = threadIdx.x >> 6;
   const int x0 = xcd_remap(blockIdx.x, gridDim.x) * RX;
   const int x = x0 + r;
+  const bool live = x >= p.xl0 && x < p.xl1;   // wave-uniform (x-slab ghost / padding rows: neither stored nor summed)
   const int y = blockIdx.y * YW + 4 * lane;
   const int j0 = jbase + blockIdx.z * jchunk;
   const int j1 = min(jend, j0 + jchunk);
@@ -155,13 +156,15 @@ __global__ void __launch_bounds__(RX * 64, FR ? 2 : 3) k_dual_lds_2d(KP<float> p
           m1y[e] = rq * fo[2];
           m2y[e] = rq * fo[3];
         }
+#pragma unroll
+        for (int a = 0; a < NA; ++a) f4set(an4[a], e, an[a]);
+        if (!live) continue;
         const double dr = (double)rn - (double)rho;
         s[0] += dr * dr;
         s[1] += (double)rn * (double)rn;
         s[2] += (double)rho * (double)rho;
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
-          f4set(an4[a], e, an[a]);
           const double da = (double)an[a] - (double)ao[a];
           s[3 + 3 * a] += da * da;
           s[4 + 3 * a] += (double)an[a] * (double)an[a];
@@ -169,9 +172,11 @@ __global__ void __launch_bounds__(RX * 64, FR ? 2 : 3) k_dual_lds_2d(KP<float> p
         }
       }
       const size_t o = (size_t)j * plane + rxc + y;
-      st4(rd + o, rn4);
+      if (live) {
+        st4(rd + o, rn4);
 #pragma unroll
-      for (int a = 0; a < NA; ++a) st4(ad[a] + o, an4[a]);
+        for (int a = 0; a < NA; ++a) st4(ad[a] + o, an4[a]);
+      }
       f0 = pc;
       if constexpr (FR) {
         if (j > j0) finish_res(j - 1, buf ^ 1, rn4, 0.f);   // row j-1, with rho'_j

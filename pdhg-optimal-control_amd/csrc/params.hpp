@@ -50,6 +50,9 @@ struct KP {
   R* res;                  // [T][nx][ny]
   R* ex;                   // [T][nx/8][2][ny]: tile-edge row terms (0: row x0 from x0-1, 1: row x0+7 from x0+8)
   R* ey;                   // [T][nx][ny/256][2]: strip-edge column terms (0: first column, 1: last column)
+  // x-slab decomposition (pdhg_create_xslab): rows [xl0, xl1) are this rank's own rows; the others are
+  // ghost / padding rows, which the dual neither stores nor sums (all rows otherwise: 0, nx)
+  int xl0, xl1;
 };
 
 // neighbour index along an axis of length n with boundary condition bc

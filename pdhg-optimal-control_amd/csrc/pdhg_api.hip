@@ -18,6 +18,7 @@
 #include "kernels_2d_fast.hpp"
 #include "kernels_dual_lds.hpp"
 #include "kernels_common.hpp"
+#include "kernels_xslab.hpp"
 
 using namespace pdhg;
 
@@ -139,6 +140,13 @@ struct Impl : ImplBase {
   int* long_pos = nullptr;   // neighbour exchange: per mode, index in the long-range list or -1
   int* long_idx = nullptr;   // the long-range modes (long_K of them)
   int long_K = -1;           // -1: not classified yet
+  // x-slab decomposition (multi-GPU for T = 1 marching windows): this context owns global x rows
+  // [xs_x0, xs_x0 + xs_nloc) of xs_nxg; its spatial arrays hold nx = xs_nloc + 16 rows (kernels_xslab.hpp)
+  bool xslab = false;
+  int xs_rank = 0, xs_P = 1, xs_nxg = 0, xs_nloc = 0, xs_x0 = 0, xs_nbs = 0;
+  R* colwork = nullptr;      // [T][nbs][nxg][B]: this rank's column blocks, whole x lines
+  const R* lamy_base = nullptr;
+  std::vector<double> xs_local;   // x coordinates of the nx local rows (ghost / padding rows wrap periodically)
 
   ~Impl() override {
     if (stream) hipStreamSynchronize(stream);
@@ -168,6 +176,7 @@ struct Impl : ImplBase {
 
   int setup() {
     const int nx = pb.nx, ny = pb.ny, T = pb.T;
+    const int nxg = xslab ? xs_nxg : nx;   // length of the x transform (global nx for an x-slab)
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     HIP_TRY(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device));
@@ -177,9 +186,9 @@ struct Impl : ImplBase {
     n_dead = (pb.ndim == 2 && pb.egno == 3) ? 2 : 0;
     two_sets = pb.rho_alp_iters > 1;
     bool ok1 = true, ok2 = true;
-    plx = make_plan(nx, ok1);
+    plx = make_plan(nxg, ok1);
     if (is2d) ply = make_plan(ny, ok2);
-    if (!ok1 || !ok2) return fail(PDHG_ERR_UNSUPPORTED, "FFT plan too deep for nx=%d ny=%d", nx, ny);
+    if (!ok1 || !ok2) return fail(PDHG_ERR_UNSUPPORTED, "FFT plan too deep for nx=%d ny=%d", nxg, ny);
 
     KP<R>& p = kp;
     p.egno = pb.egno;
@@ -198,7 +207,7 @@ struct Impl : ImplBase {
     p.epsl = (R)pb.epsl;
     p.c_over_dt = (R)(pb.c_on_rho / pb.dt);
     p.C = (R)pb.C;
-    p.inv_n = (R)(1.0 / ((double)nx * (double)ny));
+    p.inv_n = (R)(1.0 / ((double)nxg * (double)ny));
     // t-Laplacian off-diagonal: Ct/dt^2 in 1-D (utils_precond.py:128-131); 2-D ignores Ct (:164-168)
     p.ae = (R)((is2d ? 1.0 : pb.Ct) / (pb.dt * pb.dt));
 
@@ -208,15 +217,15 @@ struct Impl : ImplBase {
       // M = nx*B modes with 5*M*sizeof(R) bytes of LDS (FFT ping-pong + Thomas carries)
       const size_t cap = (sizeof(R) == 4) ? 8192 : 4096;
       int B = 16;
-      while (B > 2 && (size_t)nx * B > cap) B >>= 1;
+      while (B > 2 && (size_t)nxg * B > cap) B >>= 1;
       int nyp = 2;
       while (nyp < ny) nyp <<= 1;
       if (B > nyp) B = nyp;
       // fp32 nx = 8192 (C4): one real column per block, packed into a 4096-point FFT (half_real)
-      half_real = sizeof(R) == 4 && nx == 8192 && pb.bc_x == 0;
+      half_real = sizeof(R) == 4 && nxg == 8192 && pb.bc_x == 0;
       if (half_real) B = 1;
-      if (!half_real && (size_t)nx * B > cap)
-        return fail(PDHG_ERR_UNSUPPORTED, "nx=%d too large for the x-transform slab (max %zu in this precision)", nx,
+      if (!half_real && (size_t)nxg * B > cap)
+        return fail(PDHG_ERR_UNSUPPORTED, "nx=%d too large for the x-transform slab (max %zu in this precision)", nxg,
                     cap / 2);
       p.half_real = half_real ? 1 : 0;
       p.B = B;
@@ -225,7 +234,7 @@ struct Impl : ImplBase {
       p.nb = (ny + B - 1) / B;
       p.rows_per_wg = 2;
       lds_res = 2 * (size_t)ny * csz;
-      const int nmodes = nx * B;
+      const int nmodes = nxg * B;
       lds_xt = (size_t)5 * nmodes * sizeof(R);
       if (lds_res > kLdsBytes) return fail(PDHG_ERR_UNSUPPORTED, "ny=%d exceeds the LDS row transform", ny);
       NT2 = std::min(512, ((nmodes + 63) / 64) * 64);
@@ -239,9 +248,9 @@ struct Impl : ImplBase {
         fast_xt = true;
         ws_xt = true;
         lds_fast_xt = (size_t)(2 * (4096 + 4096 / 16) + 816 + 4096) * sizeof(C);   // + split twiddles
-      } else if (sizeof(R) == 4 && plx.pow2 && nx * (B / 2) == 4096 && nx >= 512 && pb.bc_x == 0) {
+      } else if (sizeof(R) == 4 && plx.pow2 && nxg * (B / 2) == 4096 && nxg >= 512 && pb.bc_x == 0) {
         fast_xt = true;
-        ws_xt = (nx == 4096);   // the other widths spill registers in the warp-specialised form
+        ws_xt = (nxg == 4096);   // the other widths spill registers in the warp-specialised form
         if (const char* e = getenv("PDHG_XT_WS")) ws_xt = atoi(e) != 0;   // tuning override
         // padded FFT buffer + theta, E, b' (float2 per item) + twiddle seeds (TwLds<nx>)
         lds_fast_xt = ws_xt ? (size_t)(2 * (4096 + 4096 / 16) + 816) * sizeof(C)
@@ -289,7 +298,7 @@ struct Impl : ImplBase {
       // residual row j needs rho'_{j+1}), so only grids with enough (x, y) tiles to fill the chip
       // (PDHG_FUSE_RES=1 forces it for any eligible size, =0 turns it off)
       if (sizeof(R) == 4 && fast_dual && dual_rx == 8 && fast_rows && RWf == 8 && pb.bc_x == 0 && pb.bc_y == 0 &&
-          pb.egno != 3 && !two_sets && !slab) {
+          pb.egno != 3 && !two_sets && !slab && !xslab) {
         fuse_res = gxd * gyd >= 1024;
         if (const char* e = getenv("PDHG_FUSE_RES")) fuse_res = atoi(e) != 0;
         if (fuse_res) {
@@ -324,6 +333,15 @@ struct Impl : ImplBase {
     p.xt_phase = 0;
     p.row_base = 0;
     p.row_cnt = T;
+    p.xl0 = xslab ? 8 : 0;
+    p.xl1 = xslab ? 8 + xs_nloc : nx;
+    if (xslab) {
+      if (!(is2d && sizeof(R) == 4 && fast_rows && fast_dual && dual_rx == 8 && pb.bc_x == 0 && pb.bc_y == 0))
+        return fail(PDHG_ERR_UNSUPPORTED, "x-slab decomposition needs ndim 2, fp32, bc (0,0) and a power-of-two ny "
+                                          "in [256, 8192] (fast row and dual kernels)");
+      if (p.nb % xs_P) return fail(PDHG_ERR_UNSUPPORTED, "%d column blocks do not split over %d ranks", p.nb, xs_P);
+      xs_nbs = p.nb / xs_P;
+    }
     if (slab && !(is2d && fast_xt))
       return fail(PDHG_ERR_UNSUPPORTED, "t-slab decomposition needs ndim 2, fp32 and a power-of-two nx in "
                                         "[512, 4096] (fast x-transform kernels)");
@@ -358,6 +376,7 @@ struct Impl : ImplBase {
       if ((rc = alloc(&p.ex, (size_t)T * (nx / 8) * 2 * ny))) return rc;
       if ((rc = alloc(&p.ey, (size_t)T * nx * (ny / 256) * 2))) return rc;
     }
+    if (xslab && (rc = alloc(&colwork, (size_t)T * xs_nbs * nxg * p.B))) return rc;
     if (slab) {
       Mspec = (size_t)p.nb * nx * p.B;
       if ((rc = alloc(&halo_rho, npl))) return rc;
@@ -371,7 +390,7 @@ struct Impl : ImplBase {
     HIP_TRY(hipMemsetAsync(p.ctrl, 0, sizeof(Ctrl), stream));
 
     // ---- coefficient / symbol tables (host fp64 -> R) ----
-    std::vector<R> ax(nx), ay(std::max(ny, 1)), lamx(nx), d0(nx);
+    std::vector<R> ax(nx), ay(std::max(ny, 1)), lamx(nxg), d0(nxg);
     for (int i = 0; i < nx; ++i) {
       const double x = pb.xs[i];
       ax[i] = (R)(pb.egno == 3 ? x : (x - 1.0) * (x - 1.0) + 0.1);   // set_fns.py:145 / :117-118 / :98
@@ -385,34 +404,34 @@ struct Impl : ImplBase {
     // bc (1,0) (egno 3): fv = fft_y(dct_x(lap)) = DCT-II(x stencil)[kx] + 2 cos(pi kx/2nx) * lam_y[ky]
     // -- the reference transforms the periodic stencil array with the DCT, and DCT-II(e_0) = 2 cos(.)
     const bool dct_x = is2d && pb.bc_x == 1;
-    std::vector<R> cx(nx, (R)1);
+    std::vector<R> cx(nxg, (R)1);
     std::vector<C> dctw;
-    for (int k = 0; k < nx; ++k) {
-      double l = -2.0 * (1.0 - std::cos(2.0 * M_PI * k / nx)) / (pb.dx * pb.dx);
+    for (int k = 0; k < nxg; ++k) {
+      double l = -2.0 * (1.0 - std::cos(2.0 * M_PI * k / nxg)) / (pb.dx * pb.dx);
       if (dct_x) {
-        auto c2 = [&](int n) { return 2.0 * std::cos(M_PI * k * (2.0 * n + 1.0) / (2.0 * nx)); };
-        l = (-2.0 * c2(0) + c2(1) + c2(nx - 1)) / (pb.dx * pb.dx);
+        auto c2 = [&](int n) { return 2.0 * std::cos(M_PI * k * (2.0 * n + 1.0) / (2.0 * nxg)); };
+        l = (-2.0 * c2(0) + c2(1) + c2(nxg - 1)) / (pb.dx * pb.dx);
         cx[k] = (R)c2(0);
       }
       lamx[k] = (R)l;
       d0[k] = (R)std::pow(pb.C - l, pb.pow_);   // 1-D thomas_b = (C - fv)^pow, :125-126
     }
     if (dct_x) {
-      dctw.resize(nx);
-      for (int k = 0; k < nx; ++k) {
-        dctw[k].x = (R)std::cos(-M_PI * k / (2.0 * nx));
-        dctw[k].y = (R)std::sin(-M_PI * k / (2.0 * nx));
+      dctw.resize(nxg);
+      for (int k = 0; k < nxg; ++k) {
+        dctw[k].x = (R)std::cos(-M_PI * k / (2.0 * nxg));
+        dctw[k].y = (R)std::sin(-M_PI * k / (2.0 * nxg));
       }
     }
     R *d_ax, *d_ay, *d_lamx, *d_lamy, *d_d0;
     if ((rc = alloc(&d_ax, nx))) return rc;
     if ((rc = alloc(&d_ay, std::max(ny, 1)))) return rc;
-    if ((rc = alloc(&d_lamx, nx))) return rc;
-    if ((rc = alloc(&d_d0, nx))) return rc;
+    if ((rc = alloc(&d_lamx, nxg))) return rc;
+    if ((rc = alloc(&d_d0, nxg))) return rc;
     HIP_TRY(hipMemcpy(d_ax, ax.data(), nx * sizeof(R), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(d_ay, ay.data(), ay.size() * sizeof(R), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(d_lamx, lamx.data(), nx * sizeof(R), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(d_d0, d0.data(), nx * sizeof(R), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d_lamx, lamx.data(), nxg * sizeof(R), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(d_d0, d0.data(), nxg * sizeof(R), hipMemcpyHostToDevice));
     const int nyp = is2d ? p.nb * p.B : 1;
     std::vector<R> lamy(nyp, (R)0);
     if (is2d)
@@ -421,14 +440,14 @@ struct Impl : ImplBase {
     HIP_TRY(hipMemcpy(d_lamy, lamy.data(), nyp * sizeof(R), hipMemcpyHostToDevice));
     {
       R* d_cx;
-      if ((rc = alloc(&d_cx, nx))) return rc;
-      HIP_TRY(hipMemcpy(d_cx, cx.data(), nx * sizeof(R), hipMemcpyHostToDevice));
+      if ((rc = alloc(&d_cx, nxg))) return rc;
+      HIP_TRY(hipMemcpy(d_cx, cx.data(), nxg * sizeof(R), hipMemcpyHostToDevice));
       p.cx = d_cx;
       p.dctw = nullptr;
       if (dct_x) {
         C* d_w;
-        if ((rc = alloc(&d_w, nx))) return rc;
-        HIP_TRY(hipMemcpy(d_w, dctw.data(), nx * sizeof(C), hipMemcpyHostToDevice));
+        if ((rc = alloc(&d_w, nxg))) return rc;
+        HIP_TRY(hipMemcpy(d_w, dctw.data(), nxg * sizeof(C), hipMemcpyHostToDevice));
         p.dctw = d_w;
       }
     }
@@ -436,11 +455,12 @@ struct Impl : ImplBase {
     p.ay = d_ay;
     p.lamx = d_lamx;
     p.lamy = d_lamy;
+    lamy_base = d_lamy;
     p.d0_1d = d_d0;
     {
-      auto t = twiddles<R>(nx);
-      if ((rc = alloc(&twx, nx))) return rc;
-      HIP_TRY(hipMemcpy(twx, t.data(), nx * sizeof(C), hipMemcpyHostToDevice));
+      auto t = twiddles<R>(nxg);
+      if ((rc = alloc(&twx, nxg))) return rc;
+      HIP_TRY(hipMemcpy(twx, t.data(), nxg * sizeof(C), hipMemcpyHostToDevice));
     }
     if (is2d) {
       auto t = twiddles<R>(ny);
@@ -642,6 +662,55 @@ struct Impl : ImplBase {
   }
 
   // ---------------- launches ----------------
+  // x transform + Thomas in t + inverse x transform of the spectral blocks in p.work (p.nx-point lines,
+  // p.nb blocks); p.xt_phase selects the sweeps (t-slab)
+  int launch_precond(const KP<R>& p) {
+    int rc = PDHG_OK;
+    if (fast_xt) {
+      ProfScope ps(this, "precond");
+      rc = PDHG_OK;
+      if constexpr (sizeof(R) == 4) {
+        const dim3 g(p.nb);
+        auto go = [&](auto kern) -> int {
+          int r2;
+          if ((r2 = ensure_lds(kern, lds_fast_xt))) return r2;
+          hipLaunchKernelGGL(kern, g, dim3(512), lds_fast_xt, stream, p, twx);
+          return (int)PDHG_OK;
+        };
+        if (ws_xt) {
+          switch (p.nx) {
+            case 8192: rc = go(k_precond_xt_ws_2d<4096, 1, true>); break;
+            case 4096: rc = go(k_precond_xt_ws_2d<4096, 1>); break;
+            case 2048: rc = go(k_precond_xt_ws_2d<2048, 2>); break;
+            case 1024: rc = go(k_precond_xt_ws_2d<1024, 4>); break;
+            case 512: rc = go(k_precond_xt_ws_2d<512, 8>); break;
+            default: rc = fail(PDHG_ERR_UNSUPPORTED, "no fast x kernel for nx=%d", p.nx);
+          }
+        } else switch (p.nx) {
+          case 4096: rc = go(k_precond_xt_fast_2d<4096, 1, 512>); break;
+          case 2048: rc = go(k_precond_xt_fast_2d<2048, 2, 512>); break;
+          case 1024: rc = go(k_precond_xt_fast_2d<1024, 4, 512>); break;
+          case 512: rc = go(k_precond_xt_fast_2d<512, 8, 512>); break;
+          default: rc = fail(PDHG_ERR_UNSUPPORTED, "no fast x kernel for nx=%d", p.nx);
+        }
+      }
+      if (rc) return rc;
+    } else {
+      ProfScope ps(this, "precond");
+      dim3 g(p.nb);
+      if (p.xt_phase != 0) return fail(PDHG_ERR_UNSUPPORTED, "t-slab sweeps need the fp32 power-of-two x kernels");
+      rc = with_xt_fft([&](auto f) {
+        using F = decltype(f);
+        int r2;
+        if ((r2 = ensure_lds(k_precond_xt_2d<R, F>, lds_xt))) return r2;
+        hipLaunchKernelGGL((k_precond_xt_2d<R, F>), g, dim3(NT2), lds_xt, stream, p, f, twx);
+        return (int)PDHG_OK;
+      });
+      if (rc) return rc;
+    }
+    return PDHG_OK;
+  }
+
   // stages: 1 residual (+ forward y transform), 2 x transform + Thomas (sweeps per xt_phase: 0 both,
   // 1 forward, 2 backward), 4 inverse transforms + phi/phi_bar update + primal sums.  sums_out != null
   // (t-slab mode): the primal sums go to that vector (all-reduced by the caller) instead of ctrl.
@@ -654,49 +723,7 @@ struct Impl : ImplBase {
       int rc = PDHG_OK;
       if (stages & 1)
         if ((rc = launch_residual(p, 0, T))) return rc;
-      if (!(stages & 2)) {
-      } else if (fast_xt) {
-        ProfScope ps(this, "precond");
-        rc = PDHG_OK;
-        if constexpr (sizeof(R) == 4) {
-          const dim3 g(p.nb);
-          auto go = [&](auto kern) -> int {
-            int r2;
-            if ((r2 = ensure_lds(kern, lds_fast_xt))) return r2;
-            hipLaunchKernelGGL(kern, g, dim3(512), lds_fast_xt, stream, p, twx);
-            return (int)PDHG_OK;
-          };
-          if (ws_xt) {
-            switch (pb.nx) {
-              case 8192: rc = go(k_precond_xt_ws_2d<4096, 1, true>); break;
-              case 4096: rc = go(k_precond_xt_ws_2d<4096, 1>); break;
-              case 2048: rc = go(k_precond_xt_ws_2d<2048, 2>); break;
-              case 1024: rc = go(k_precond_xt_ws_2d<1024, 4>); break;
-              case 512: rc = go(k_precond_xt_ws_2d<512, 8>); break;
-              default: rc = fail(PDHG_ERR_UNSUPPORTED, "no fast x kernel for nx=%d", pb.nx);
-            }
-          } else switch (pb.nx) {
-            case 4096: rc = go(k_precond_xt_fast_2d<4096, 1, 512>); break;
-            case 2048: rc = go(k_precond_xt_fast_2d<2048, 2, 512>); break;
-            case 1024: rc = go(k_precond_xt_fast_2d<1024, 4, 512>); break;
-            case 512: rc = go(k_precond_xt_fast_2d<512, 8, 512>); break;
-            default: rc = fail(PDHG_ERR_UNSUPPORTED, "no fast x kernel for nx=%d", pb.nx);
-          }
-        }
-        if (rc) return rc;
-      } else {
-        ProfScope ps(this, "precond");
-        dim3 g(p.nb);
-        if (xt_phase != 0) return fail(PDHG_ERR_UNSUPPORTED, "t-slab sweeps need the fp32 power-of-two x kernels");
-        rc = with_xt_fft([&](auto f) {
-          using F = decltype(f);
-          int r2;
-          if ((r2 = ensure_lds(k_precond_xt_2d<R, F>, lds_xt))) return r2;
-          hipLaunchKernelGGL((k_precond_xt_2d<R, F>), g, dim3(NT2), lds_xt, stream, p, f, twx);
-          return (int)PDHG_OK;
-        });
-        if (rc) return rc;
-      }
+      if ((stages & 2) && (rc = launch_precond(p))) return rc;
       if (!(stages & 4)) {
         HIP_TRY(hipGetLastError());
         return PDHG_OK;
@@ -1096,6 +1123,61 @@ struct Impl : ImplBase {
     own_stream = false;
     return PDHG_OK;
   }
+  // ---------------- x-slab phases (multi-GPU for T = 1 windows; the caller moves data between ranks) ------------
+  // One outer iteration (include/pdhg.h): halo_out(0) -> [allgather] -> halo_in(0) -> residual ->
+  // wire(0) -> [all-to-all] -> wire(1) -> precond -> wire(2) -> [all-to-all] -> wire(3) -> update(sums) ->
+  // halo_out(1) -> [allgather] || [allreduce sums] -> primal_finalize -> halo_in(1) -> dual ... as a t-slab.
+  int need_xslab() const { return xslab ? PDHG_OK : fail(PDHG_ERR_STATE, "not an x-slab context"); }
+  KP<R> col_params() const {   // the x transform of this rank's column blocks (whole x lines)
+    KP<R> q = kp;
+    q.nx = xs_nxg;
+    q.nb = xs_nbs;
+    q.work = colwork;
+    q.lamy = lamy_base + (size_t)xs_rank * xs_nbs * kp.B;
+    q.xt_phase = 0;
+    q.xl0 = 0;
+    q.xl1 = xs_nxg;
+    return q;
+  }
+  size_t xs_chunk() const { return (size_t)pb.T * xs_nbs * xs_nloc * kp.B; }   // wire floats per rank pair
+  size_t xs_halo_elems(int which) const { return (size_t)2 * (which == 0 ? 1 + na : 1) * pb.T * pb.ny; }
+  int xs_wire(int stage, void* buf) {
+    // 0: rows -> wire (after the residual), 1: wire -> cols, 2: cols -> wire (after the precond), 3: wire -> rows
+    const size_t L = (size_t)xs_nloc * kp.B;
+    const size_t total4 = xs_chunk() * xs_P / 4;
+    const unsigned g = (unsigned)std::max<size_t>(1, std::min<size_t>((total4 + 255) / 256, 8192));
+    R* S = static_cast<R*>(buf);
+    if (stage == 0 || stage == 3)
+      hipLaunchKernelGGL((k_xs_rows_wire<R>), dim3(g), dim3(256), 0, stream, kp.work, S, stage == 0 ? 0 : 1, xs_P,
+                         pb.T, kp.nb, xs_nbs, pb.nx, kp.xl0, kp.B, L);
+    else if (stage == 1 || stage == 2)
+      hipLaunchKernelGGL((k_xs_cols_wire<R>), dim3(g), dim3(256), 0, stream, colwork, S, stage == 2 ? 0 : 1, xs_P,
+                         pb.T, xs_nbs, xs_nxg, xs_nloc, kp.B, L);
+    else
+      return fail(PDHG_ERR_ARG, "unknown wire stage %d", stage);
+    HIP_TRY(hipGetLastError());
+    return PDHG_OK;
+  }
+  int xs_halo_out(int which, void* dst) {
+    if (which != 0 && which != 1) return fail(PDHG_ERR_ARG, "unknown halo %d", which);
+    const unsigned g = (unsigned)std::max<size_t>(1, std::min<size_t>((xs_halo_elems(which) + 255) / 256, 4096));
+    hipLaunchKernelGGL((k_xs_halo_out<R>), dim3(g), dim3(256), 0, stream, kp, which, static_cast<R*>(dst));
+    HIP_TRY(hipGetLastError());
+    return PDHG_OK;
+  }
+  int xs_halo_in(int which, const void* left, const void* right) {
+    if (which != 0 && which != 1) return fail(PDHG_ERR_ARG, "unknown halo %d", which);
+    const unsigned g = (unsigned)std::max<size_t>(1, std::min<size_t>((xs_halo_elems(which) + 255) / 256, 4096));
+    hipLaunchKernelGGL((k_xs_halo_in<R>), dim3(g), dim3(256), 0, stream, kp, which, static_cast<const R*>(left),
+                       static_cast<const R*>(right));
+    HIP_TRY(hipGetLastError());
+    if (which == 0) res_valid = false;
+    return PDHG_OK;
+  }
+  int xs_residual() { return launch_residual(kp, 0, pb.T); }
+  int xs_precond() { return launch_precond(col_params()); }
+  int xs_update(R tau, double* sums) { return launch_primal(tau, 4, 0, sums); }
+
   int slab_status(pdhg_stats* st) {
     Ctrl h;
     int rc;
@@ -1123,8 +1205,9 @@ struct Impl : ImplBase {
   int n_alp_ref() const { return pb.ndim == 1 ? 2 : 4; }
 
   void compute_row0_sq(const std::vector<R>& row0) {
-    double s = 0.0;
-    for (R v : row0) s += (double)v * (double)v;
+    double s = 0.0;   // live rows only (x-slab: [xl0, xl1) of the padded local rows)
+    const size_t ny = pb.ny;
+    for (size_t i = (size_t)kp.xl0 * ny; i < (size_t)kp.xl1 * ny; ++i) s += (double)row0[i] * (double)row0[i];
     row0_sq = s;
   }
 
@@ -1284,7 +1367,7 @@ struct Impl : ImplBase {
   }
 
   double algorithmic_bytes(int k, const std::string& cls) const {
-    const double N = (double)pb.T * (double)plane();
+    const double N = (double)pb.T * (double)(kp.xl1 - kp.xl0) * (double)pb.ny;   // live rows (x-slab)
     const double S = (double)sizeof(R);
     const bool d2 = pb.ndim == 2;
     const double nr = 1.0 + na;   // rho + live alp arrays
@@ -1315,6 +1398,27 @@ int dispatch(pdhg_ctx* ctx, F&& f) {
   CtxBox* b = reinterpret_cast<CtxBox*>(ctx);
   if (b->precision == 8) return f(*static_cast<Impl<double>*>(b->impl.get()));
   return f(*static_cast<Impl<float>*>(b->impl.get()));
+}
+
+// phases shared by the t-slab and x-slab contexts (begin, finalizers, dual, outer, status)
+template <typename F>
+int phase_dispatch(pdhg_ctx* ctx, F&& f) {
+  if (!ctx) return fail(PDHG_ERR_ARG, "null context");
+  CtxBox* b = reinterpret_cast<CtxBox*>(ctx);
+  if (b->precision != 4) return fail(PDHG_ERR_STATE, "not a t-slab / x-slab context");
+  auto& im = *static_cast<Impl<float>*>(b->impl.get());
+  if (!im.slab && !im.xslab) return fail(PDHG_ERR_STATE, "not a t-slab / x-slab context");
+  return f(im);
+}
+
+template <typename F>
+int xslab_dispatch(pdhg_ctx* ctx, F&& f) {
+  if (!ctx) return fail(PDHG_ERR_ARG, "null context");
+  CtxBox* b = reinterpret_cast<CtxBox*>(ctx);
+  if (b->precision != 4) return fail(PDHG_ERR_STATE, "not an x-slab context");
+  auto& im = *static_cast<Impl<float>*>(b->impl.get());
+  int rc = im.need_xslab();
+  return rc ? rc : f(im);
 }
 
 template <typename F>
@@ -1535,7 +1639,7 @@ int pdhg_set_stream(pdhg_ctx* ctx, void* hip_stream) {   // null = the device's 
   return dispatch(ctx, [&](auto& im) { return im.set_stream(static_cast<hipStream_t>(hip_stream)); });
 }
 int pdhg_slab_begin(pdhg_ctx* ctx) {
-  return slab_dispatch(ctx, [&](auto& im) { return im.reset_ctrl(); });
+  return phase_dispatch(ctx, [&](auto& im) { return im.reset_ctrl(); });
 }
 int pdhg_slab_carry_gain(pdhg_ctx* ctx, void* GS_out) {
   if (!GS_out) return fail(PDHG_ERR_ARG, "null plane");
@@ -1575,23 +1679,23 @@ int pdhg_slab_backward(pdhg_ctx* ctx, double tau, double* sums) {
 }
 int pdhg_slab_primal_finalize(pdhg_ctx* ctx, const double* sums) {
   if (!sums) return fail(PDHG_ERR_ARG, "null sums");
-  return slab_dispatch(ctx, [&](auto& im) { return im.slab_primal_finalize(sums); });
+  return phase_dispatch(ctx, [&](auto& im) { return im.slab_primal_finalize(sums); });
 }
 int pdhg_slab_dual(pdhg_ctx* ctx, double sigma, int rho_alp_iters, int sub, double* sums, int parts) {
   if (!sums) return fail(PDHG_ERR_ARG, "null sums");
-  return slab_dispatch(ctx, [&](auto& im) { return im.slab_dual((float)sigma, rho_alp_iters, sub, sums, parts); });
+  return phase_dispatch(ctx, [&](auto& im) { return im.slab_dual((float)sigma, rho_alp_iters, sub, sums, parts); });
 }
 int pdhg_slab_dual_finalize(pdhg_ctx* ctx, double eps, int sub, const double* sums) {
   if (!sums) return fail(PDHG_ERR_ARG, "null sums");
-  return slab_dispatch(ctx, [&](auto& im) { return im.slab_dual_finalize(eps, sub, sums); });
+  return phase_dispatch(ctx, [&](auto& im) { return im.slab_dual_finalize(eps, sub, sums); });
 }
 int pdhg_slab_outer(pdhg_ctx* ctx, int rho_alp_iters, double* sums) {
   if (!sums) return fail(PDHG_ERR_ARG, "null sums");
-  return slab_dispatch(ctx, [&](auto& im) { return im.slab_outer(rho_alp_iters, sums); });
+  return phase_dispatch(ctx, [&](auto& im) { return im.slab_outer(rho_alp_iters, sums); });
 }
 int pdhg_slab_outer_finalize(pdhg_ctx* ctx, double eps, int rho_alp_iters, const double* sums) {
   if (!sums) return fail(PDHG_ERR_ARG, "null sums");
-  return slab_dispatch(ctx, [&](auto& im) { return im.slab_outer_finalize(eps, rho_alp_iters, sums); });
+  return phase_dispatch(ctx, [&](auto& im) { return im.slab_outer_finalize(eps, rho_alp_iters, sums); });
 }
 int pdhg_slab_plane_out(pdhg_ctx* ctx, int which, void* dst) {
   if (!dst) return fail(PDHG_ERR_ARG, "null plane");
@@ -1603,7 +1707,7 @@ int pdhg_slab_plane_in(pdhg_ctx* ctx, int which, const void* src) {
 }
 int pdhg_slab_status(pdhg_ctx* ctx, pdhg_stats* st) {
   if (!st) return fail(PDHG_ERR_ARG, "null stats");
-  return slab_dispatch(ctx, [&](auto& im) { return im.slab_status(st); });
+  return phase_dispatch(ctx, [&](auto& im) { return im.slab_status(st); });
 }
 int pdhg_slab_plane_size(pdhg_ctx* ctx, unsigned long long* spatial, unsigned long long* spectral) {
   if (!spatial || !spectral) return fail(PDHG_ERR_ARG, "null argument");
@@ -1612,6 +1716,91 @@ int pdhg_slab_plane_size(pdhg_ctx* ctx, unsigned long long* spatial, unsigned lo
     *spectral = im.Mspec;
     return (int)PDHG_OK;
   });
+}
+
+/* ---------------- x-slab decomposition ---------------- */
+int pdhg_create_xslab(const pdhg_problem* prob, int rank, int nranks, int device, pdhg_ctx** out) {
+  if (!prob || !out) return fail(PDHG_ERR_ARG, "null argument");
+  *out = nullptr;
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(PDHG_ERR_ARG, "rank %d of %d", rank, nranks);
+  if (prob->precision != 4) return fail(PDHG_ERR_UNSUPPORTED, "x-slab decomposition is fp32 only");
+  if (prob->ndim != 2) return fail(PDHG_ERR_UNSUPPORTED, "x-slab decomposition is 2-D only");
+  if (prob->bc_x != 0 || prob->bc_y != 0) return fail(PDHG_ERR_UNSUPPORTED, "x-slab decomposition needs bc (0,0)");
+  if (prob->nx % nranks || (prob->nx / nranks) % 8)
+    return fail(PDHG_ERR_UNSUPPORTED, "nx=%d must split into %d slabs of a multiple of 8 rows", prob->nx, nranks);
+  // validate the rest exactly like pdhg_create (one row of the global grid), then build the slab
+  pdhg_ctx* probe = nullptr;
+  pdhg_problem q = *prob;
+  q.T = 1;
+  int rc = pdhg_create(&q, device, &probe);
+  if (rc) return rc;
+  pdhg_destroy(probe);
+  const int nloc = prob->nx / nranks, nxl = nloc + 16, x0 = rank * nloc;
+  auto box = std::make_unique<CtxBox>();
+  box->precision = 4;
+  auto im = std::make_unique<Impl<float>>();
+  im->xslab = true;
+  im->xs_rank = rank;
+  im->xs_P = nranks;
+  im->xs_nxg = prob->nx;
+  im->xs_nloc = nloc;
+  im->xs_x0 = x0;
+  im->xs_local.resize(nxl);
+  for (int i = 0; i < nxl; ++i) {   // local row i = global row x0 - 8 + i (periodic)
+    const int g = ((x0 - 8 + i) % prob->nx + prob->nx) % prob->nx;
+    im->xs_local[i] = prob->xs[g];
+  }
+  im->pb = *prob;
+  im->pb.nx = nxl;
+  im->pb.xs = im->xs_local.data();
+  im->device = device;
+  rc = im->setup();
+  box->impl = std::move(im);
+  if (rc) return rc;
+  *out = reinterpret_cast<pdhg_ctx*>(box.release());
+  return PDHG_OK;
+}
+int pdhg_xslab_layout(pdhg_ctx* ctx, int* x0, int* nloc, int* nx_local, int* xl0) {
+  if (!x0 || !nloc || !nx_local || !xl0) return fail(PDHG_ERR_ARG, "null argument");
+  return xslab_dispatch(ctx, [&](auto& im) {
+    *x0 = im.xs_x0;
+    *nloc = im.xs_nloc;
+    *nx_local = im.pb.nx;
+    *xl0 = im.kp.xl0;
+    return (int)PDHG_OK;
+  });
+}
+int pdhg_xslab_sizes(pdhg_ctx* ctx, unsigned long long* wire, unsigned long long* halo_state,
+                     unsigned long long* halo_phibar) {
+  if (!wire || !halo_state || !halo_phibar) return fail(PDHG_ERR_ARG, "null argument");
+  return xslab_dispatch(ctx, [&](auto& im) {
+    *wire = im.xs_chunk() * im.xs_P;
+    *halo_state = im.xs_halo_elems(0);
+    *halo_phibar = im.xs_halo_elems(1);
+    return (int)PDHG_OK;
+  });
+}
+int pdhg_xslab_halo_out(pdhg_ctx* ctx, int which, void* dst) {
+  if (!dst) return fail(PDHG_ERR_ARG, "null buffer");
+  return xslab_dispatch(ctx, [&](auto& im) { return im.xs_halo_out(which, dst); });
+}
+int pdhg_xslab_halo_in(pdhg_ctx* ctx, int which, const void* from_left, const void* from_right) {
+  if (!from_left || !from_right) return fail(PDHG_ERR_ARG, "null buffer");
+  return xslab_dispatch(ctx, [&](auto& im) { return im.xs_halo_in(which, from_left, from_right); });
+}
+int pdhg_xslab_residual(pdhg_ctx* ctx) {
+  return xslab_dispatch(ctx, [&](auto& im) { return im.xs_residual(); });
+}
+int pdhg_xslab_wire(pdhg_ctx* ctx, int stage, void* buf) {
+  if (!buf) return fail(PDHG_ERR_ARG, "null buffer");
+  return xslab_dispatch(ctx, [&](auto& im) { return im.xs_wire(stage, buf); });
+}
+int pdhg_xslab_precond(pdhg_ctx* ctx) {
+  return xslab_dispatch(ctx, [&](auto& im) { return im.xs_precond(); });
+}
+int pdhg_xslab_update(pdhg_ctx* ctx, double tau, double* sums) {
+  if (!sums) return fail(PDHG_ERR_ARG, "null sums");
+  return xslab_dispatch(ctx, [&](auto& im) { return im.xs_update((float)tau, sums); });
 }
 
 }  // extern "C"

@@ -30,6 +30,9 @@ EXPORTS = (
     "pdhg_slab_residual", "pdhg_slab_forward", "pdhg_slab_fixup", "pdhg_slab_long_modes", "pdhg_slab_fixup_nb", "pdhg_slab_backward", "pdhg_slab_primal_finalize", "pdhg_slab_dual",
     "pdhg_slab_dual_finalize", "pdhg_slab_outer", "pdhg_slab_outer_finalize", "pdhg_slab_plane_out",
     "pdhg_slab_plane_in", "pdhg_slab_status",
+    # x-slab decomposition (multi-GPU for T = 1 windows)
+    "pdhg_create_xslab", "pdhg_xslab_layout", "pdhg_xslab_sizes", "pdhg_xslab_halo_out", "pdhg_xslab_halo_in",
+    "pdhg_xslab_residual", "pdhg_xslab_wire", "pdhg_xslab_precond", "pdhg_xslab_update",
 )
 
 
@@ -130,7 +133,20 @@ def load():
         "pdhg_slab_plane_out": ([P, ctypes.c_int, P], ctypes.c_int),
         "pdhg_slab_plane_in": ([P, ctypes.c_int, P], ctypes.c_int),
         "pdhg_slab_status": ([P, ctypes.POINTER(pdhg_stats)], ctypes.c_int),
+        "pdhg_create_xslab": ([ctypes.POINTER(pdhg_problem), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                               ctypes.POINTER(P)], ctypes.c_int),
+        "pdhg_xslab_layout": ([P] + [ctypes.POINTER(ctypes.c_int)] * 4, ctypes.c_int),
+        "pdhg_xslab_sizes": ([P] + [ctypes.POINTER(ctypes.c_ulonglong)] * 3, ctypes.c_int),
+        "pdhg_xslab_halo_out": ([P, ctypes.c_int, P], ctypes.c_int),
+        "pdhg_xslab_halo_in": ([P, ctypes.c_int, P, P], ctypes.c_int),
+        "pdhg_xslab_residual": ([P], ctypes.c_int),
+        "pdhg_xslab_wire": ([P, ctypes.c_int, P], ctypes.c_int),
+        "pdhg_xslab_precond": ([P], ctypes.c_int),
+        "pdhg_xslab_update": ([P, ctypes.c_double, P], ctypes.c_int),
     }
+    missing = set(EXPORTS) - set(sig)
+    if missing:
+        raise ImportError("no ctypes signature for {}".format(sorted(missing)))
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
         fn.argtypes = args

@@ -47,7 +47,40 @@ def slab_bounds(T, P):
     return out
 
 
-class SlabContext(PDHGContext):
+class PhaseOps:
+    """Phase functions shared by t-slab and x-slab contexts (pdhg_slab_begin / _primal_finalize / _dual /
+    _dual_finalize / _outer / _outer_finalize / _status, pdhg_set_stream).  Tensor arguments are device
+    tensors (float64[16] sums)."""
+
+    def set_stream(self, stream_handle):
+        N.check(self._lib.pdhg_set_stream(self._h, ctypes.c_void_p(stream_handle)))
+
+    def begin(self):
+        N.check(self._lib.pdhg_slab_begin(self._h))
+
+    def primal_finalize(self, sums):
+        N.check(self._lib.pdhg_slab_primal_finalize(self._h, _ptr(sums)))
+
+    def dual(self, sigma, k, sub, sums, parts=INTERIOR | EDGE):
+        N.check(self._lib.pdhg_slab_dual(self._h, float(sigma), int(k), int(sub), _ptr(sums), int(parts)))
+
+    def dual_finalize(self, eps, sub, sums):
+        N.check(self._lib.pdhg_slab_dual_finalize(self._h, float(eps), int(sub), _ptr(sums)))
+
+    def outer(self, k, sums):
+        N.check(self._lib.pdhg_slab_outer(self._h, int(k), _ptr(sums)))
+
+    def outer_finalize(self, eps, k, sums):
+        N.check(self._lib.pdhg_slab_outer_finalize(self._h, float(eps), int(k), _ptr(sums)))
+
+    def status(self):
+        st = N.pdhg_stats()
+        N.check(self._lib.pdhg_slab_status(self._h, ctypes.byref(st)))
+        return {"iters": st.iters_run, "status": st.status, "err1": st.err1, "err2": st.err2,
+                "inner_last": st.inner_last, "inner_total": st.inner_total, "nan_seen": st.nan_seen}
+
+
+class SlabContext(PhaseOps, PDHGContext):
     """The slab [j0, j1) of a window of T_total rows (fp32, 2-D).  Arrays at this boundary are the
     slab's rows: phi [T+1, nx, ny] (row 0 = global phi row j0), rho / alp [T, nx, ny(, n_ctrl)]."""
 
@@ -71,13 +104,8 @@ class SlabContext(PDHGContext):
         N.check(self._lib.pdhg_slab_plane_size(self._h, ctypes.byref(sp), ctypes.byref(spec)))
         return sp.value, spec.value
 
-    # thin wrappers; tensor arguments are device tensors (float32 planes, float64[16] sums)
-    def set_stream(self, stream_handle):
-        N.check(self._lib.pdhg_set_stream(self._h, ctypes.c_void_p(stream_handle)))
 
-    def begin(self):
-        N.check(self._lib.pdhg_slab_begin(self._h))
-
+    # thin wrappers; tensor arguments are device tensors (float32 planes)
     def carry_gain(self, GS):
         N.check(self._lib.pdhg_slab_carry_gain(self._h, _ptr(GS)))
 
@@ -102,32 +130,11 @@ class SlabContext(PDHGContext):
     def backward(self, tau, sums):
         N.check(self._lib.pdhg_slab_backward(self._h, float(tau), _ptr(sums)))
 
-    def primal_finalize(self, sums):
-        N.check(self._lib.pdhg_slab_primal_finalize(self._h, _ptr(sums)))
-
-    def dual(self, sigma, k, sub, sums, parts=INTERIOR | EDGE):
-        N.check(self._lib.pdhg_slab_dual(self._h, float(sigma), int(k), int(sub), _ptr(sums), int(parts)))
-
-    def dual_finalize(self, eps, sub, sums):
-        N.check(self._lib.pdhg_slab_dual_finalize(self._h, float(eps), int(sub), _ptr(sums)))
-
-    def outer(self, k, sums):
-        N.check(self._lib.pdhg_slab_outer(self._h, int(k), _ptr(sums)))
-
-    def outer_finalize(self, eps, k, sums):
-        N.check(self._lib.pdhg_slab_outer_finalize(self._h, float(eps), int(k), _ptr(sums)))
-
     def plane_out(self, which, dst):
         N.check(self._lib.pdhg_slab_plane_out(self._h, int(which), _ptr(dst)))
 
     def plane_in(self, which, src):
         N.check(self._lib.pdhg_slab_plane_in(self._h, int(which), _ptr(src)))
-
-    def status(self):
-        st = N.pdhg_stats()
-        N.check(self._lib.pdhg_slab_status(self._h, ctypes.byref(st)))
-        return {"iters": st.iters_run, "status": st.status, "err1": st.err1, "err2": st.err2,
-                "inner_last": st.inner_last, "inner_total": st.inner_total, "nan_seen": st.nan_seen}
 
 
 def _ptr(t):
@@ -148,6 +155,14 @@ class LocalComm:
         import torch
         out = torch.stack(planes)
         return [out] * len(planes)
+
+    def alltoall(self, sends, recvs):
+        """sends[q] / recvs[q]: [P * chunk] wires of slab q; chunk s of slab q's send -> chunk q of slab s's recv."""
+        P = self.nranks
+        c = sends[0].numel() // P
+        for q in range(P):
+            for s in range(P):
+                recvs[s][q * c:(q + 1) * c].copy_(sends[q][s * c:(s + 1) * c])
 
     def allreduce(self, vecs):
         tot = vecs[0].clone()
@@ -197,6 +212,17 @@ class DistComm:
         out = torch.empty((self.nranks,) + tuple(x.shape), dtype=x.dtype, device=x.device)
         self.dist.all_gather_into_tensor(out, x)
         return [out]
+
+    def alltoall(self, sends, recvs):
+        """Chunk s of this rank's send -> rank s; chunk q of recv <- rank q (equal chunks)."""
+        import torch
+        (send,), (recv,) = sends, recvs
+        if self.gloo and send.is_cuda:
+            h = torch.empty(recv.shape, dtype=recv.dtype)
+            self.dist.all_to_all_single(h, send.cpu())
+            recv.copy_(h)
+        else:
+            self.dist.all_to_all_single(recv, send)
 
     def allreduce(self, vecs):
         if self.gloo and vecs[0].is_cuda:

@@ -1,0 +1,166 @@
+"""x-slab decomposition on the GPU: P x-slab contexts on one device, exchanging halo
+rows and the transposed spectrum through LocalComm, must reproduce the single-context iteration
+(pdhg_iterate) of the same window -- same state after n outer iterations within fp32 rounding, same
+error history and stop decisions -- for T = 1 (the reference's marching default) and longer windows,
+every x-transform kernel (generic, single-role, warp-specialised, half-real) and k = 1 / k > 1.
+The single-context path is itself pinned to the oracle by test_gpu_parity.py; one case here also
+checks the x-slab state against the fp64 oracle directly."""
+import numpy as np
+import pytest
+
+from _problems import make_problem, oracle_fns, rel
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # (egno, nx, ny, T, P, k, epsl)
+    (1, 512, 256, 1, 2, 1, 0.0),     # k_precond_xt_fast_2d, T = 1 (marching default)
+    (2, 512, 256, 1, 4, 1, 0.1),
+    (1, 512, 256, 3, 2, 3, 0.0),     # two buffer sets (rho_alp_iters > 1), T = 3
+    (2, 512, 512, 2, 1, 1, 0.0),     # one slab: the halo ring is the slab itself
+    (1, 512, 256, 1, 8, 1, 0.0),     # 64-row slabs
+    (2, 4096, 256, 1, 2, 1, 0.0),    # k_precond_xt_ws_2d
+    (2, 8192, 256, 1, 2, 1, 0.0),    # half-real x blocks (C4's nx)
+    (1, 256, 256, 2, 2, 1, 0.0),     # generic x kernel (runtime plan)
+    (2, 384, 256, 1, 2, 1, 0.0),     # non-power-of-two nx (radix-3 plan), 192-row slabs
+]
+
+
+def _xslabs(P, nranks, k):
+    from pdhg_amd.xslab import XSlabContext
+    return [XSlabContext(r, nranks, P["egno"], P["nx"], P["ny"], P["T"], P["dx"], P["dy"], P["dt"], P["xs"], P["ys"],
+                         epsl=P["epsl"], rho_alp_iters=k) for r in range(nranks)]
+
+
+def _state(slabs):
+    from pdhg_amd.xslab import join_rows
+    parts = [s.get_state() for s in slabs]
+    phi = join_rows(slabs, [p[0] for p in parts])
+    rho = join_rows(slabs, [p[1] for p in parts])
+    alp = [join_rows(slabs, [p[2][a] for p in parts]) for a in range(4)]
+    return phi, rho, alp
+
+
+@pytest.mark.parametrize("egno,nx,ny,T,nr,k,epsl", CASES,
+                         ids=[f"e{c[0]}_{c[1]}x{c[2]}_T{c[3]}_P{c[4]}_k{c[5]}_eps{c[6]}" for c in CASES])
+def test_xslabs_match_single_context(native, egno, nx, ny, T, nr, k, epsl):
+    import torch
+    from pdhg_amd.context import PDHGContext
+    from pdhg_amd.xslab import LocalComm, XSlabRunner
+    P = make_problem(egno, 2, nx, ny, T, epsl)
+    tau, sigma, n = 0.1 / 1.5, 0.1 * 1.5, 6
+    ref = PDHGContext(egno, 2, nx, ny, T, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"], epsl=epsl,
+                      precision="fp32", rho_alp_iters=k)
+    ref.set_state(P["phi"], P["rho"], P["alp"])
+    st_ref = ref.iterate(n, tau, sigma, -1.0, k)
+    phi_r, rho_r, alp_r = ref.get_state()
+
+    slabs = _xslabs(P, nr, k)
+    for s in slabs:
+        assert s.nloc == nx // nr and s.nx == s.nloc + 16
+        s.set_global_state(P["phi"], P["rho"], P["alp"])
+    runner = XSlabRunner(slabs, LocalComm(nr))
+    st = runner.iterate(n, tau, sigma, -1.0, k)
+    torch.cuda.synchronize()
+    phi_s, rho_s, alp_s = _state(slabs)
+    assert not st_ref["nan_seen"] and not st["nan_seen"]
+    assert st["iters"] == st_ref["iters_run"] == n
+    assert st["inner_total"] == st_ref["inner_total"]
+    assert rel(phi_s, phi_r) < 2e-5
+    assert rel(rho_s, rho_r) < 2e-4
+    assert rel(np.stack(alp_s), np.stack(alp_r)) < 2e-4
+    assert abs(st["err1"] - st_ref["err1"]) <= 1e-4 * st_ref["err1"]
+    assert abs(st["err2"] - st_ref["err2"]) <= 1e-4 * st_ref["err2"]
+    for s in slabs:
+        s.close()
+    ref.close()
+
+
+def test_xslab_vs_oracle(native):
+    """Two x-slabs, 10 iterations from the seeded state, against the fp64 oracle (the north-star bound)."""
+    import torch
+    from pdhg_amd.xslab import LocalComm, XSlabRunner
+    P = make_problem(2, 2, 512, 256, 1, 0.0)
+    tau, sigma, n = 0.1 / 1.5, 0.1 * 1.5, 10
+    primal, dual = oracle_fns(P)
+    phi, rho, alp = P["phi"], P["rho"], P["alp"]
+    for _ in range(n):
+        phi_n = primal(phi, rho, 70.0, alp, tau, P["dt"], P["dsp"], P["fns"], P["fv"], P["epsl"], P["x_arr"], None)
+        rho, alp = dual(2 * phi_n - phi, rho, 70.0, alp, sigma, P["dt"], P["dsp"], P["epsl"], P["fns"], P["x_arr"],
+                        None, 2, -1.0)
+        phi = phi_n
+    slabs = _xslabs(P, 2, 1)
+    for s in slabs:
+        s.set_global_state(P["phi"], P["rho"], P["alp"])
+    XSlabRunner(slabs, LocalComm(2)).iterate(n, tau, sigma, -1.0, 1)
+    torch.cuda.synchronize()
+    phi_s, rho_s, _ = _state(slabs)
+    assert rel(phi_s, phi) < 1e-5
+    assert rel(rho_s, rho) < 1e-5
+
+
+def test_xslab_convergence_stop(native):
+    """The global stop decision (all-reduced err1/err2) ends every slab at the single context's iteration."""
+    import torch
+    from pdhg_amd.context import PDHGContext
+    from pdhg_amd.xslab import LocalComm, XSlabRunner
+    P = make_problem(1, 2, 512, 256, 1, 0.0, seeded=False)
+    tau, sigma, eps = 0.1 / 1.5, 0.1 * 1.5, 1e-3
+    ref = PDHGContext(1, 2, 512, 256, 1, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"], precision="fp32")
+    ref.set_state(P["phi"], P["rho"], P["alp"])
+    st_ref = ref.iterate(3000, tau, sigma, eps, 1)
+    assert st_ref["status"] == 1
+    slabs = _xslabs(P, 4, 1)
+    for s in slabs:
+        s.init_global_state(P["g"])
+    st = XSlabRunner(slabs, LocalComm(4)).iterate(3000, tau, sigma, eps, 1)
+    torch.cuda.synchronize()
+    assert st["status"] == 1
+    assert abs(st["iters"] - st_ref["iters_run"]) <= 1
+    assert rel(_state(slabs)[0], ref.get_state()[0]) < 1e-4
+
+
+def test_multi_step_xslab(native):
+    """Window marching over x-slabs (T = 1 windows, warm starts) against the single-context marching."""
+    import torch
+    from pdhg_amd.context import PDHGContext
+    from pdhg_amd.xslab import LocalComm, XSlabRunner, multi_step_xslab
+    P = make_problem(2, 2, 512, 256, 1, 0.0, seeded=False)
+    nt, eps, s_par = 4, 1e-3, 0.1
+    slabs = _xslabs(P, 2, 1)
+    res, errs = multi_step_xslab(XSlabRunner(slabs, LocalComm(2)), P["g"], nt, 70.0, stepsz_param=s_par,
+                                 N_maxiter=3000, eps=eps)
+    torch.cuda.synchronize()
+    phi_x = np.concatenate([r[1] for r in res], axis=1)
+    rho_x = np.concatenate([r[2] for r in res], axis=1)
+    assert phi_x.shape == (nt, 512, 256) and rho_x.shape == (nt - 1, 512, 256)
+    # single context, same marching (utils_pdhg_solver.py:193-206)
+    ref = PDHGContext(2, 2, 512, 256, 1, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"], precision="fp32")
+    phi0 = np.repeat(P["g"], 2, axis=0)
+    rho0, alp0 = np.full((1, 512, 256), 70.0), tuple(np.zeros((1, 512, 256, 2)) for _ in range(4))
+    phis, rhos = [], []
+    for i in range(nt - 1):
+        ref.set_state(phi0, rho0, alp0)
+        st = ref.iterate(3000, s_par / 1.5, s_par * 1.5, eps, 1)
+        assert st["status"] == 1
+        phi_c, rho_c, alp_c = ref.get_state()
+        phis.append(phi_c[:-1] if i < nt - 2 else phi_c)
+        rhos.append(rho_c)
+        phi0, rho0, alp0 = phi0 + (phi_c[-1:] - phi0[0:1]), rho_c, alp_c
+    assert rel(phi_x, np.concatenate(phis)) < 1e-4
+    assert rel(rho_x, np.concatenate(rhos)) < 1e-3
+    for s in slabs:
+        s.close()
+    ref.close()
+
+
+def test_xslab_rejects_unsupported(native):
+    from pdhg_amd import _native as N
+    from pdhg_amd.xslab import XSlabContext
+    P = make_problem(1, 2, 512, 256, 1, 0.0)
+    with pytest.raises(N.PDHGError):      # 512 rows do not split into 3 slabs
+        XSlabContext(0, 3, 1, 512, 256, 1, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"])
+    with pytest.raises(N.PDHGError):      # 4-row slabs (not a multiple of 8)
+        XSlabContext(0, 128, 1, 512, 256, 1, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"])
+    with pytest.raises(N.PDHGError):      # fp64
+        XSlabContext(0, 2, 1, 512, 256, 1, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"], precision="fp64")
