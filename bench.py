@@ -12,6 +12,11 @@ N > 1 (launched by torch.distributed.run): one process per GPU, the SAME window 
 of T/N rows (pdhg_amd/slab.py): rho / phi_bar halos point to point, the distributed
 t-solve's two plane allgathers and the stop-test allreduces over RCCL.  Total work is fixed, so the
 scaling is "strong"; value = iterations of the window / max-over-ranks time.
+
+--decomp xslab (with --config c3w1: the reference's marching default, one T = 1 window of the 4096^2
+grid): the window's x rows split into N x-slabs (pdhg_amd/xslab.py): halo-row
+allgathers and two all-to-all transposes of the spectrum per iteration.  At N = 1 it runs one x-slab
+through the same phases (LocalComm), so its line measures the decomposition's overhead.
 """
 import argparse
 import json
@@ -34,6 +39,7 @@ CONFIGS = {
     "c2": (1, 2, 0.0, 2048, 2048, 101),
     "c1": (1, 1, 0.0, 65536, 1, 401),
     "c0": (1, 1, 0.0, 160, 1, 41),
+    "c3w1": (2, 2, 0.1, 4096, 4096, 2),   # one T = 1 window of C3's grid (time_step_per_PDHG = 2 default)
 }
 
 
@@ -153,6 +159,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-T", type=int, default=2)
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
+    ap.add_argument("--decomp", default="tslab", choices=["tslab", "xslab"],
+                    help="multi-GPU decomposition of the window (xslab also at N = 1: one slab through its phases)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -170,7 +178,7 @@ def main():
         dist = tdist
 
     pmc, pmc_err = None, "disabled"
-    if world == 1 and not args.no_pmc:
+    if world == 1 and not args.no_pmc and args.decomp == "tslab":
         pmc, pmc_err = pmc_traffic(args)   # before this process initialises the GPU
 
     from pdhg_amd.context import PDHGContext
@@ -181,7 +189,13 @@ def main():
     xs, ys = grid(ndim, nx, ny)
     dt = 1.0 / (nt - 1)
     runner = None
-    if world > 1:
+    xslab = args.decomp == "xslab"
+    if xslab:
+        import torch
+        from pdhg_amd.xslab import XSlabContext
+        ctx = XSlabContext(rank, world, egno, nx, ny, T, 2.0 / nx, 2.0 / ny, dt, xs, ys, epsl=epsl,
+                           rho_alp_iters=k, device=torch.cuda.current_device())
+    elif world > 1:
         from pdhg_amd.slab import DistComm, SlabContext, SlabRunner
         ctx = SlabContext(rank, world, T, egno, nx, ny, 2.0 / nx, 2.0 / ny, dt, xs, ys, epsl=epsl,
                           rho_alp_iters=k, device=torch.cuda.current_device())
@@ -192,7 +206,10 @@ def main():
         g = np.sin(np.pi * xs)
     else:
         g = np.sin(np.pi * xs)[:, None] + np.sin(np.pi * ys)[None, :]
-    ctx.init_state(g)
+    if xslab:
+        ctx.init_global_state(g)
+    else:
+        ctx.init_state(g)
     # epsl = 0.1 on a 4096^2 grid is outside the reference algorithm's stability range (explicit
     # sigma*epsl*Lap in the dual; its fp64 restatement diverges already at 256^2): keep executing
     # exactly the requested iterations after the state goes non-finite, and report it.
@@ -200,7 +217,17 @@ def main():
     tau, sigma = 0.1 / 1.5, 0.1 * 1.5
     eps = 1e-6
 
-    if world > 1:
+    if xslab:
+        from pdhg_amd.xslab import DistComm as XComm, LocalComm as XLocal, XSlabRunner
+        xrunner = XSlabRunner([ctx], XComm() if world > 1 else XLocal(1))
+
+        def run(n):
+            s = xrunner.iterate(n, tau, sigma, eps, k)
+            return {"iters_run": s["iters"], "status": s["status"], "nan_seen": s["nan_seen"]}
+
+        def sync():
+            torch.cuda.synchronize()
+    elif world > 1:
         import torch
         runner = SlabRunner([ctx], DistComm(), exchange=os.environ.get("PDHG_SLAB_EXCHANGE", "neighbour"))
 
@@ -249,7 +276,7 @@ def main():
         ms, n = ctx.profile_query(cls)
         if n:
             kern[cls] = {"avg_ms": ms / n, "launches": n, "bytes_per_launch": ctx.algorithmic_bytes(k, cls)}
-    if world > 1:   # t-slab: sweeps and halo/interior row parts are separate launches -> per iteration
+    if world > 1 or xslab:   # slabs: sweeps and halo/interior row parts are separate launches -> per iteration
         for cls, d in kern.items():
             per = max(iters, 1) * (k if cls == "dual" else 1)
             d["avg_ms"] = d["avg_ms"] * d["launches"] / per
@@ -280,8 +307,10 @@ def main():
         "data": "synthetic (reference initial state phi=g, rho=70, alp=0)",
         "config": {"workload": "egno{} ndim{} epsl{} nx={} ny={} nt={}: one PDHG window of T={} rows, "
                                "rho_alp_iters={}".format(egno, ndim, epsl, nx, ny, nt, T, k),
-                   "parallelism": "t-slab x{} (RCCL point-to-point halos and carries, overlapped)".format(world) if world > 1
-                   else "single GPU",
+                   "parallelism": ("x-slab x{} (halo-row allgathers, two all-to-all spectrum transposes per "
+                                   "iteration)".format(world) if xslab else
+                                   "t-slab x{} (RCCL point-to-point halos and carries, overlapped)".format(world))
+                   if (world > 1 or xslab) else "single GPU",
                    "iters_executed": iters, "stop_status": st["status"], "state_nonfinite": bool(st["nan_seen"])},
         **({"slab_exchange": {"carries": runner.exchange, "long_range_modes": runner.n_long,
                               "halo_overlap": runner.side is not None}} if runner is not None else {}),

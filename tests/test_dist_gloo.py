@@ -105,3 +105,52 @@ def _worker(rank, world, port, paths):
 def test_gloo_slab_exchanges(world):
     paths = [os.path.join(HERE, "..", "pdhg-optimal-control_amd"), os.path.join(HERE, "..", "oracle")]
     mp.spawn(_worker, args=(world, _free_port(), [os.path.abspath(p) for p in paths]), nprocs=world, join=True)
+
+
+def _xslab_worker(rank, world, port, paths):
+    """x-slab exchanges over gloo: the halo ring (allgather of the first / last live rows) and the
+    preconditioner's two all-to-all transposes, restated in oracle/xslab_oracle.py, must reproduce the
+    monolithic H1_precond_2d (utils_precond.py:142-178) on this rank's rows."""
+    import sys
+    sys.path[:0] = paths
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{}".format(port), rank=rank, world_size=world)
+    try:
+        from pdhg_amd.slab import DistComm
+        import pdhg_oracle as O
+        import xslab_oracle as X
+        comm = DistComm()
+        nx, ny, T, B, dt = 48, 24, 3, 4, 0.05
+        dx, dy = 2.0 / nx, 2.0 / ny
+        nloc = nx // world
+        x0 = rank * nloc
+        rng = np.random.default_rng(11)           # same data on every rank
+        R = rng.standard_normal((T, nx, ny))
+        idx = X.local_index(x0, nloc, nx)
+        # --- halo ring: ghost rows from the neighbours' live edge rows
+        A = R[:, idx].copy()
+        A[:, X.XL0 - 1] = 0.0
+        A[:, X.XL0 + nloc] = 0.0
+        (allh,) = comm.allgather([torch.from_numpy(X.halo_out(A, nloc))])
+        X.halo_in(A, nloc, allh[(rank - 1) % world].numpy(), allh[(rank + 1) % world].numpy())
+        assert np.array_equal(A[:, X.XL0 - 1], R[:, (x0 - 1) % nx])
+        assert np.array_equal(A[:, X.XL0 + nloc], R[:, (x0 + nloc) % nx])
+
+        # --- preconditioner over the all-to-all transposes
+        def a2a(send):
+            recv = torch.empty(send.shape, dtype=torch.float64)
+            comm.alltoall([torch.from_numpy(np.ascontiguousarray(send))], [recv])
+            return recv.numpy()
+
+        lx, ly = X.symbols(nx, ny, dx, dy)
+        U = X.precond_rank(R[:, idx], rank, world, nloc, B, a2a, lx, ly, dt)
+        fv = O.compute_Dxx_fft_fv(2, (nx, ny), (dx, dy), (0, 0))
+        ref = O.H1_precond_2d(np.concatenate([np.zeros((1, nx, ny)), R]), fv, dt, (0, 0))[1:]
+        assert np.allclose(U, ref[:, x0:x0 + nloc], rtol=1e-10, atol=1e-12 * np.abs(ref).max())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_xslab_exchanges(world):
+    paths = [os.path.join(HERE, "..", "pdhg-optimal-control_amd"), os.path.join(HERE, "..", "oracle")]
+    mp.spawn(_xslab_worker, args=(world, _free_port(), [os.path.abspath(p) for p in paths]), nprocs=world, join=True)

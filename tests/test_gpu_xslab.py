@@ -164,3 +164,50 @@ def test_xslab_rejects_unsupported(native):
         XSlabContext(0, 128, 1, 512, 256, 1, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"])
     with pytest.raises(N.PDHGError):      # fp64
         XSlabContext(0, 2, 1, 512, 256, 1, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"], precision="fp64")
+
+
+def _dist_worker(rank, world, port, paths, out):
+    import sys
+    sys.path[:0] = paths
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{}".format(port), rank=rank, world_size=world)
+    try:
+        from pdhg_amd.context import PDHGContext
+        from pdhg_amd.xslab import DistComm, XSlabContext, XSlabRunner
+        P = make_problem(2, 2, 512, 256, 1, 0.0)
+        tau, sigma, n = 0.1 / 1.5, 0.1 * 1.5, 6
+        ref = PDHGContext(2, 2, 512, 256, 1, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"], precision="fp32")
+        ref.set_state(P["phi"], P["rho"], P["alp"])
+        st_ref = ref.iterate(n, tau, sigma, -1.0, 1)
+        phi_r = ref.get_state()[0]
+        s = XSlabContext(rank, world, 2, 512, 256, 1, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"])
+        s.set_global_state(P["phi"], P["rho"], P["alp"])
+        st = XSlabRunner([s], DistComm()).iterate(n, tau, sigma, -1.0, 1)
+        torch.cuda.synchronize()
+        phi_s = s.live_rows(s.get_state()[0])
+        e = rel(phi_s, phi_r[:, s.x0:s.x0 + s.nloc])
+        out.put((rank, st["iters"], st_ref["iters_run"], e, abs(st["err1"] - st_ref["err1"]) / st_ref["err1"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_xslab_distcomm_gloo_rehearsal(native):
+    """The multi-process path (DistComm: allgather / all-to-all / allreduce over torch.distributed) with two
+    ranks on the one GPU over gloo (host-staged): each rank's rows match the single context."""
+    import os
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    here = os.path.dirname(os.path.abspath(__file__))
+    paths = [os.path.join(here, "..", "pdhg-optimal-control_amd"), os.path.join(here, "..", "oracle"), here]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.spawn(_dist_worker, args=(2, port, [os.path.abspath(p) for p in paths], q), nprocs=2, join=True)
+    res = sorted(q.get() for _ in range(2))
+    for rank, it, it_ref, e_phi, e_err1 in res:
+        assert it == it_ref == 6, res
+        assert e_phi < 2e-5 and e_err1 < 1e-4, res
