@@ -40,6 +40,8 @@ CONFIGS = {
     "c1": (1, 1, 0.0, 65536, 1, 401),
     "c0": (1, 1, 0.0, 160, 1, 41),
     "c3w1": (2, 2, 0.1, 4096, 4096, 2),   # one T = 1 window of C3's grid (time_step_per_PDHG = 2 default)
+    "c3w4": (2, 2, 0.1, 4096, 4096, 5),   # short windows of C3's grid (kernel-policy crossover)
+    "c3w8": (2, 2, 0.1, 4096, 4096, 9),
 }
 
 

@@ -989,6 +989,7 @@ __global__ void __launch_bounds__(256) k_dual_fast_2d(KP<float> p, int jchunk, i
   const int nx = p.nx, ny = p.ny;
   const size_t plane = (size_t)nx * ny;
   const int x = xcd_remap(blockIdx.x, gridDim.x);
+  const bool live = x >= p.xl0 && x < p.xl1;   // workgroup-uniform (x-slab ghost / padding rows: not stored or summed)
   const int y = 4 * (blockIdx.y * blockDim.x + threadIdx.x);
   // rows [jbase, jend) in chunks of jchunk (blockIdx.z); partials of this launch start at block row zbase
   const int j0 = jbase + blockIdx.z * jchunk;
@@ -1055,13 +1056,15 @@ __global__ void __launch_bounds__(256) k_dual_fast_2d(KP<float> p, int jchunk, i
         const float rn = dual_point<float, EGNO>(p, c, f4(pm, e), f4(pp, e), lft, rgt, f4(f0, e), rho, ao, axc,
                                                  f4(ay4, e), an);
         f4set(rn4, e, rn);
+#pragma unroll
+        for (int a = 0; a < NA; ++a) f4set(an4[a], e, an[a]);
+        if (!live) continue;
         const double dr = (double)rn - (double)rho;
         s[0] += dr * dr;
         s[1] += (double)rn * (double)rn;
         s[2] += (double)rho * (double)rho;
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
-          f4set(an4[a], e, an[a]);
           const double da = (double)an[a] - (double)ao[a];
           s[3 + 3 * a] += da * da;
           s[4 + 3 * a] += (double)an[a] * (double)an[a];
@@ -1069,9 +1072,11 @@ __global__ void __launch_bounds__(256) k_dual_fast_2d(KP<float> p, int jchunk, i
         }
       }
       const size_t o = (size_t)j * plane + rxc + y;
-      st4(rd + o, rn4);
+      if (live) {
+        st4(rd + o, rn4);
 #pragma unroll
-      for (int a = 0; a < NA; ++a) st4(ad[a] + o, an4[a]);
+        for (int a = 0; a < NA; ++a) st4(ad[a] + o, an4[a]);
+      }
       f0 = pc;
     }
   }

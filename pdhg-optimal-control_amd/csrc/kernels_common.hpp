@@ -6,20 +6,35 @@
 namespace pdhg {
 
 // Fixed-order reduction of nrows partial rows (ns sums each) into out[0..ns).
+// Each thread reads whole partial rows (one pass over the rows for all ns sums), then every sum is
+// reduced across the wave (shuffles, fixed order) and across the waves (LDS, fixed order).  Call with
+// blockDim.x a multiple of 64, at most 1024; out is visible to every thread on return.
 __device__ void reduce_partials(const double* __restrict__ partials, int nrows, int ns, double* out) {
-  __shared__ double red[256];
-  for (int s = 0; s < ns; ++s) {
-    double acc = 0.0;
-    for (int r = threadIdx.x; r < nrows; r += blockDim.x) acc += partials[(size_t)r * kNumSums + s];
-    red[threadIdx.x] = acc;
-    __syncthreads();
-    for (int w = blockDim.x >> 1; w > 0; w >>= 1) {
-      if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) out[s] = red[0];
-    __syncthreads();
+  __shared__ double red[kNumSums][16];
+  double acc[kNumSums];
+#pragma unroll
+  for (int s = 0; s < kNumSums; ++s) acc[s] = 0.0;
+  for (int r = threadIdx.x; r < nrows; r += blockDim.x) {
+    const double* row = partials + (size_t)r * kNumSums;
+#pragma unroll
+    for (int s = 0; s < kNumSums; ++s)
+      if (s < ns) acc[s] += row[s];
   }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int s = 0; s < kNumSums; ++s) {
+    double v = acc[s];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    if (lane == 0) red[s][w] = v;
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < ns) {
+    double t = 0.0;
+    for (int i = 0; i < nw; ++i) t += red[threadIdx.x][i];
+    out[threadIdx.x] = t;
+  }
+  __syncthreads();
 }
 
 // After the primal update: err1 sums (utils_pdhg_solver.py:58).  row0_sq = sum phi_0^2

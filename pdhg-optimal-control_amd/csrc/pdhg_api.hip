@@ -244,13 +244,23 @@ struct Impl : ImplBase {
       gx5 = (ny + 255) / 256;
       g5 = std::max(1, std::min(T * nx, 8192 / std::max(1, gx5)));
       if (const char* e = getenv("PDHG_DBG")) p.dbg = atoi(e);   // timing experiments only
+      // short windows (the reference's T = 1 marching default): few time rows per workgroup leave little to
+      // pipeline over t, so occupancy decides.  Measured on C3's grid (bench --config c3w1/c3w4/c3w8): the
+      // single-role x-transform kernel beats the warp-specialised one up to T = 8 at least (T = 1: 0.18 vs
+      // 0.24 ms, T = 8: 0.79 vs 0.84 ms); the row-per-thread dual (146 VGPRs, 3 waves/SIMD) without the
+      // fused residual beats the fused 8-row sweep (200 VGPRs, 2 waves/SIMD) at T = 1 (0.31 vs 0.41 ms),
+      // ties at T = 4 and loses from T = 8 on.
+      int short_t_xt = 16, short_t_dual = 3;
+      if (const char* e = getenv("PDHG_SHORT_T_XT")) short_t_xt = atoi(e);   // tuning overrides (0: never)
+      if (const char* e = getenv("PDHG_SHORT_T")) short_t_dual = atoi(e);
+      const bool short_win = T < short_t_xt, short_dual = T < short_t_dual;
       if (half_real) {
         fast_xt = true;
         ws_xt = true;
         lds_fast_xt = (size_t)(2 * (4096 + 4096 / 16) + 816 + 4096) * sizeof(C);   // + split twiddles
       } else if (sizeof(R) == 4 && plx.pow2 && nxg * (B / 2) == 4096 && nxg >= 512 && pb.bc_x == 0) {
         fast_xt = true;
-        ws_xt = (nxg == 4096);   // the other widths spill registers in the warp-specialised form
+        ws_xt = (nxg == 4096) && !short_win;   // the other widths spill registers in the warp-specialised form
         if (const char* e = getenv("PDHG_XT_WS")) ws_xt = atoi(e) != 0;   // tuning override
         // padded FFT buffer + theta, E, b' (float2 per item) + twiddle seeds (TwLds<nx>)
         lds_fast_xt = ws_xt ? (size_t)(2 * (4096 + 4096 / 16) + 816) * sizeof(C)
@@ -258,7 +268,7 @@ struct Impl : ImplBase {
       }
       if (sizeof(R) == 4 && ny % 256 == 0) {
         fast_dual = true;
-        dual_rx = (nx % 8 == 0) ? 8 : 0;
+        dual_rx = (nx % 8 == 0 && !short_dual) ? 8 : 0;
         if (const char* e = getenv("PDHG_DUAL_RX")) {   // tuning override: 0 = row-per-thread kernel
           const int v = atoi(e);
           if (v == 0 || ((v == 4 || v == 8 || v == 16) && nx % v == 0)) dual_rx = v;
@@ -336,7 +346,7 @@ struct Impl : ImplBase {
     p.xl0 = xslab ? 8 : 0;
     p.xl1 = xslab ? 8 + xs_nloc : nx;
     if (xslab) {
-      if (!(is2d && sizeof(R) == 4 && fast_rows && fast_dual && dual_rx == 8 && pb.bc_x == 0 && pb.bc_y == 0))
+      if (!(is2d && sizeof(R) == 4 && fast_rows && fast_dual && pb.bc_x == 0 && pb.bc_y == 0))
         return fail(PDHG_ERR_UNSUPPORTED, "x-slab decomposition needs ndim 2, fp32, bc (0,0) and a power-of-two ny "
                                           "in [256, 8192] (fast row and dual kernels)");
       if (p.nb % xs_P) return fail(PDHG_ERR_UNSUPPORTED, "%d column blocks do not split over %d ranks", p.nb, xs_P);

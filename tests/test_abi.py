@@ -92,3 +92,33 @@ def test_null_context_calls(lib):
     L = lib.load()
     assert L.pdhg_update_primal(None, 0.1) == lib.PDHG_ERR_ARG
     assert L.pdhg_destroy(None) == lib.PDHG_OK
+
+
+def test_xslab_create_validates_before_device(lib):
+    """pdhg_create_xslab checks the decomposition (rank range, precision, ndim, bc, row split) before it
+    touches a device."""
+    L = lib.load()
+    xs = np.linspace(0, 2, 64, endpoint=False)
+    ys = np.linspace(0, 2, 256, endpoint=False)
+
+    def prob(**kw):
+        p = lib.pdhg_problem()
+        p.egno, p.ndim, p.nx, p.ny, p.T, p.precision, p.rho_alp_iters = 1, 2, 64, 256, 1, 4, 1
+        p.dx, p.dy, p.dt, p.C, p.pow_, p.Ct, p.c_on_rho = 2 / 64, 2 / 256, 0.025, 1.0, 1.0, 1.0, 70.0
+        p.xs, p.ys = lib.dptr(xs), lib.dptr(ys)
+        for k, v in kw.items():
+            setattr(p, k, v)
+        return p
+
+    h = ctypes.c_void_p()
+    for (rank, nranks, kw, code) in [(2, 2, {}, lib.PDHG_ERR_ARG), (0, 0, {}, lib.PDHG_ERR_ARG),
+                                     (0, 2, {"precision": 8}, lib.PDHG_ERR_UNSUPPORTED),
+                                     (0, 2, {"ndim": 1, "ny": 1}, lib.PDHG_ERR_UNSUPPORTED),
+                                     (0, 2, {"bc_x": 1}, lib.PDHG_ERR_UNSUPPORTED),
+                                     (0, 3, {}, lib.PDHG_ERR_UNSUPPORTED),      # 64 rows / 3
+                                     (0, 16, {}, lib.PDHG_ERR_UNSUPPORTED)]:    # 4-row slabs
+        p = prob(**kw)
+        assert L.pdhg_create_xslab(ctypes.byref(p), rank, nranks, 0, ctypes.byref(h)) == code, (rank, nranks, kw)
+        assert L.pdhg_last_error().decode()
+    # phase calls on a non-slab / null context fail with a status, not a crash
+    assert L.pdhg_xslab_residual(None) == lib.PDHG_ERR_ARG

@@ -33,6 +33,7 @@ UNSTABLE_IDS = ["e{}d{}_{}x{}_T{}_eps{}".format(*c) for c in UNSTABLE]
 
 def _ctx(P, fuse, monkeypatch):
     monkeypatch.setenv("PDHG_FUSE_RES", "1" if fuse else "0")
+    monkeypatch.setenv("PDHG_SHORT_T", "0")   # these windows are short: keep the 8-row (fusable) dual
     ctx = device_ctx(P, "fp32")
     assert ctx.path_info("fused_residual") == (1 if fuse else 0)
     return ctx
