@@ -8,17 +8,22 @@ namespace pdhg {
 // Fixed-order reduction of nrows partial rows (ns sums each) into out[0..ns).
 // Each thread reads whole partial rows (one pass over the rows for all ns sums), then every sum is
 // reduced across the wave (shuffles, fixed order) and across the waves (LDS, fixed order).  Call with
-// blockDim.x a multiple of 64, at most 1024; out is visible to every thread on return.
+// blockDim.x a multiple of 64, at most 1024 (the finalize kernels run one 1024-thread block, so 16
+// waves keep row loads in flight); out is visible to every thread on return.
 __device__ void reduce_partials(const double* __restrict__ partials, int nrows, int ns, double* out) {
   __shared__ double red[kNumSums][16];
   double acc[kNumSums];
 #pragma unroll
   for (int s = 0; s < kNumSums; ++s) acc[s] = 0.0;
-  for (int r = threadIdx.x; r < nrows; r += blockDim.x) {
-    const double* row = partials + (size_t)r * kNumSums;
+  for (int r = threadIdx.x; r < nrows; r += blockDim.x) {   // rows are kNumSums doubles, 16-B aligned
+    const double2* row = reinterpret_cast<const double2*>(partials + (size_t)r * kNumSums);
 #pragma unroll
-    for (int s = 0; s < kNumSums; ++s)
-      if (s < ns) acc[s] += row[s];
+    for (int s2 = 0; s2 < kNumSums / 2; ++s2)
+      if (2 * s2 < ns) {
+        const double2 v = row[s2];
+        acc[2 * s2] += v.x;
+        acc[2 * s2 + 1] += v.y;   // entries >= ns are never written out
+      }
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
 #pragma unroll
@@ -39,7 +44,7 @@ __device__ void reduce_partials(const double* __restrict__ partials, int nrows, 
 
 // After the primal update: err1 sums (utils_pdhg_solver.py:58).  row0_sq = sum phi_0^2
 // (row 0 never changes: utils_precond.py:139/177).
-__global__ void __launch_bounds__(256) k_finalize_primal(const double* partials, int nrows, double row0_sq, Ctrl* ctrl) {
+__global__ void __launch_bounds__(1024) k_finalize_primal(const double* partials, int nrows, double row0_sq, Ctrl* ctrl) {
   if (ctrl->done) return;
   __shared__ double out[3];
   reduce_partials(partials, nrows, 3, out);
@@ -54,7 +59,7 @@ __global__ void __launch_bounds__(256) k_finalize_primal(const double* partials,
 // After dual sub-iteration `sub`: err = sum (drho)^2/sum rho'^2 + sum_a sum (dalp)^2/sum alp'^2
 // (update_fns_in_pdhg.py:162-164); early exit flag when err < eps (:176).  n_dead reference
 // arrays that are not stored (egno 3's y controls, identically zero) contribute 0/0 = NaN.
-__global__ void __launch_bounds__(256) k_finalize_dual(const double* partials, int nrows, int na, int n_dead,
+__global__ void __launch_bounds__(1024) k_finalize_dual(const double* partials, int nrows, int na, int n_dead,
                                                        double eps, int sub, Ctrl* ctrl) {
   if (ctrl->done || ctrl->inner_done) return;
   __shared__ double out[kNumSums];
@@ -105,7 +110,7 @@ __global__ void __launch_bounds__(256) k_outer_sums(KP<R> p, size_t n) {
 
 // End of an outer iteration: err1, err2 (utils_pdhg_solver.py:58-68), stop tests (:74-80).
 // outer_rows > 0: reduce k_outer_sums partials first (k > 1); else use the sub-iteration-0 sums.
-__global__ void __launch_bounds__(256) k_finalize_outer(const double* partials, int outer_rows, int na, double eps,
+__global__ void __launch_bounds__(1024) k_finalize_outer(const double* partials, int outer_rows, int na, double eps,
                                                         int flip, int stop_conv, int stop_nan, Ctrl* ctrl) {
   if (ctrl->done) return;
   __shared__ double out[kNumSums];
@@ -164,7 +169,7 @@ namespace pdhg {
 
 // Fold a partial-sum table into one row of kNumSums doubles (the vector the ranks all-reduce);
 // add0 is added to sums 1 and 2 (the fixed phi row 0 in the primal sums, first slab only).
-__global__ void __launch_bounds__(256) k_reduce_vec(const double* partials, int nrows, int ns, double add0,
+__global__ void __launch_bounds__(1024) k_reduce_vec(const double* partials, int nrows, int ns, double add0,
                                                     double* out) {
   __shared__ double o[kNumSums];
   reduce_partials(partials, nrows, ns, o);

@@ -773,10 +773,10 @@ struct Impl : ImplBase {
         if (rc) return rc;
       }
       if (sums_out)
-        hipLaunchKernelGGL(k_reduce_vec, dim3(1), dim3(256), 0, stream, p.partials, upd_rows, 3,
+        hipLaunchKernelGGL(k_reduce_vec, dim3(1), dim3(1024), 0, stream, p.partials, upd_rows, 3,
                            kp.j0 == 0 ? row0_sq : 0.0, sums_out);
       else
-        hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(256), 0, stream, p.partials, upd_rows, row0_sq, p.ctrl);
+        hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, p.partials, upd_rows, row0_sq, p.ctrl);
     } else {
       int rc;
       {
@@ -810,7 +810,7 @@ struct Impl : ImplBase {
         });
         if (rc) return rc;
       }
-      hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(256), 0, stream, p.partials, gx4, row0_sq, p.ctrl);
+      hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, p.partials, gx4, row0_sq, p.ctrl);
     }
     HIP_TRY(hipGetLastError());
     return PDHG_OK;
@@ -874,7 +874,7 @@ struct Impl : ImplBase {
         }
       }
       const int nrows_d = (pb.ndim == 2 && fast_dual) ? gxd * gyd * gzd : gx5 * g5;
-      hipLaunchKernelGGL(k_finalize_dual, dim3(1), dim3(256), 0, stream, p.partials, nrows_d, na, n_dead, eps, s,
+      hipLaunchKernelGGL(k_finalize_dual, dim3(1), dim3(1024), 0, stream, p.partials, nrows_d, na, n_dead, eps, s,
                          p.ctrl);
     }
     HIP_TRY(hipGetLastError());
@@ -888,7 +888,7 @@ struct Impl : ImplBase {
       hipLaunchKernelGGL((k_outer_sums<R>), dim3(g_outer), dim3(256), 0, stream, p, (size_t)pb.T * plane());
       rows = g_outer;
     }
-    hipLaunchKernelGGL(k_finalize_outer, dim3(1), dim3(256), 0, stream, p.partials, rows, na, eps, k > 1 ? 1 : 0,
+    hipLaunchKernelGGL(k_finalize_outer, dim3(1), dim3(1024), 0, stream, p.partials, rows, na, eps, k > 1 ? 1 : 0,
                        stop_conv, stop_nan, p.ctrl);
     HIP_TRY(hipGetLastError());
     return PDHG_OK;
@@ -1032,7 +1032,7 @@ struct Impl : ImplBase {
   }
   int slab_backward(R tau, double* sums) { return launch_primal(tau, 2 | 4, 2, sums); }
   int slab_primal_finalize(const double* sums) {
-    hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(256), 0, stream, sums, 1, 0.0, kp.ctrl);
+    hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, sums, 1, 0.0, kp.ctrl);
     HIP_TRY(hipGetLastError());
     return PDHG_OK;
   }
@@ -1072,25 +1072,25 @@ struct Impl : ImplBase {
       }
       nrows_d = gx5 * g5;
     }
-    hipLaunchKernelGGL(k_reduce_vec, dim3(1), dim3(256), 0, stream, p.partials, nrows_d, 3 + 3 * na, 0.0, sums);
+    hipLaunchKernelGGL(k_reduce_vec, dim3(1), dim3(1024), 0, stream, p.partials, nrows_d, 3 + 3 * na, 0.0, sums);
     HIP_TRY(hipGetLastError());
     return PDHG_OK;
   }
   int slab_dual_finalize(double eps, int sub, const double* sums) {
-    hipLaunchKernelGGL(k_finalize_dual, dim3(1), dim3(256), 0, stream, sums, 1, na, n_dead, eps, sub, kp.ctrl);
+    hipLaunchKernelGGL(k_finalize_dual, dim3(1), dim3(1024), 0, stream, sums, 1, na, n_dead, eps, sub, kp.ctrl);
     HIP_TRY(hipGetLastError());
     return PDHG_OK;
   }
   int slab_outer(int k, double* sums) {
     if (k > 1) {
       hipLaunchKernelGGL((k_outer_sums<R>), dim3(g_outer), dim3(256), 0, stream, kp, (size_t)pb.T * plane());
-      hipLaunchKernelGGL(k_reduce_vec, dim3(1), dim3(256), 0, stream, kp.partials, g_outer, kNumSums, 0.0, sums);
+      hipLaunchKernelGGL(k_reduce_vec, dim3(1), dim3(1024), 0, stream, kp.partials, g_outer, kNumSums, 0.0, sums);
     }
     HIP_TRY(hipGetLastError());
     return PDHG_OK;
   }
   int slab_outer_finalize(double eps, int k, const double* sums) {
-    hipLaunchKernelGGL(k_finalize_outer, dim3(1), dim3(256), 0, stream, sums, k > 1 ? 1 : 0, na, eps, k > 1 ? 1 : 0,
+    hipLaunchKernelGGL(k_finalize_outer, dim3(1), dim3(1024), 0, stream, sums, k > 1 ? 1 : 0, na, eps, k > 1 ? 1 : 0,
                        stop_conv, stop_nan, kp.ctrl);
     HIP_TRY(hipGetLastError());
     return PDHG_OK;
@@ -1359,7 +1359,7 @@ struct Impl : ImplBase {
       if ((rc = launch_outer(eps, k))) return rc;
     } else if (k > 1) {
       // no primal in this pairing: still move the state to the current buffer set
-      hipLaunchKernelGGL(k_finalize_outer, dim3(1), dim3(256), 0, stream, kp.partials, 0, na, -1.0, 1, 0, 0, kp.ctrl);
+      hipLaunchKernelGGL(k_finalize_outer, dim3(1), dim3(1024), 0, stream, kp.partials, 0, na, -1.0, 1, 0, 0, kp.ctrl);
     }
     if ((rc = read_ctrl(h))) return rc;
     if (inner_used) *inner_used = h.inner_count;

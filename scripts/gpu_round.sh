@@ -1,11 +1,10 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-timeout -k 10 300 python -u -m pytest tests/test_gpu_xslab.py tests/test_gpu_fused.py tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_part.log 2>&1 || exit 1
-for cfg in c3w1 c3w4 c3w8 c3; do
+timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_all.log 2>&1 || exit 1
+for cfg in c3w1 c3; do
   echo "== $cfg"
   timeout -k 10 200 python bench.py --no-pmc --no-cpu-baseline --config $cfg --steps 20 --warmup 3 2>/dev/null | python -c "
 import json,sys
 d=json.loads(sys.stdin.read().strip().splitlines()[-1])
 print('it/s %.2f ms %.4f' % (d['value'], d['ms_per_step']), {k: round(v['avg_ms'],4) for k,v in d['kernels'].items()})" || exit 1
 done
-timeout -k 10 300 python bench.py --no-pmc --no-cpu-baseline --rho-alp-iters 10 --steps 5 --warmup 2 > gpurun_out/bench_c3_k10.json 2>/dev/null || exit 1
