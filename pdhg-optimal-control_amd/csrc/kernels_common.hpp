@@ -214,6 +214,10 @@ __device__ __forceinline__ double slab_pivot(const KP<R>& p, int k, double dd, d
 //   data = 0 (once per context):  out = [G, S2],  G = prod_k g_k,  S2 = sum_k P'_k P_k
 //   data = 1 (every iteration):   out = [D, S1],  D = b0 of the last local row,  S1 = sum_k P'_k b0_k
 // (P'_k = prod g_{j0..k-1}, P_k = P'_k g_k; b0 = the zero-carry forward sweep stored in work).
+// The products only decrease (0 < g <= 1); once P'_k < kSlabDrop the remaining terms of S1 are below that
+// relative weight and the row sweep stops (the high-frequency modes decay within a few rows), the same
+// bound as the neighbour exchange's short-range classification (LONG_RANGE_DELTA = 2^-40).
+constexpr double kSlabDrop = 9.094947017729282e-13;   // 2^-40
 template <typename R>
 __global__ void __launch_bounds__(256) k_slab_sums(KP<R> p, int data, R* __restrict__ out) {
   if (data && p.ctrl->done) return;
@@ -222,18 +226,18 @@ __global__ void __launch_bounds__(256) k_slab_sums(KP<R> p, int data, R* __restr
   if (m >= M) return;
   double dd, h;
   slab_mode(p, m, dd, h);
-  double P = 1.0, s = 0.0, b0 = 0.0;
+  double P = 1.0, s = 0.0;
   for (int k = 0; k < p.T; ++k) {
+    if (data && P < kSlabDrop) break;
     const double g = slab_pivot(p, k, dd, h);
     if (data) {
-      b0 = (double)p.work[(size_t)k * M + m];
-      s += P * b0;
+      s += P * (double)p.work[(size_t)k * M + m];
     } else {
       s += P * P * g;
     }
     P *= g;
   }
-  out[m] = data ? (R)b0 : (R)P;
+  out[m] = data ? p.work[(size_t)(p.T - 1) * M + m] : (R)P;
   out[M + m] = (R)s;
 }
 
@@ -266,6 +270,7 @@ __global__ void __launch_bounds__(256) k_slab_fix(KP<R> p, const R* __restrict__
     double P = 1.0;
     for (int k = 0; k < p.T; ++k) {
       P *= slab_pivot(p, k, dd, h);
+      if (P < kSlabDrop) break;   // decreasing: the carry's weight on the remaining rows is below 2^-40
       R* w = p.work + (size_t)k * M + m;
       *w = (R)((double)*w + P * c_own);
     }
@@ -318,6 +323,7 @@ __global__ void __launch_bounds__(256) k_slab_fix_nb(KP<R> p, const R* __restric
     double P = 1.0;
     for (int k = 0; k < p.T; ++k) {
       P *= slab_pivot(p, k, dd, h);
+      if (P < kSlabDrop) break;   // decreasing: the carry's weight on the remaining rows is below 2^-40
       R* w = p.work + (size_t)k * M + m;
       *w = (R)((double)*w + P * c_own);
     }
