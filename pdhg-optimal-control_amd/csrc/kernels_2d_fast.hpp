@@ -279,7 +279,7 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
   if constexpr (TWL) fill_twlds<C, N>(twl, twy);
   const int nx = p.nx;
   const int ngx = nx / RW;
-  const int ntask = ngx * p.T;
+  const int ntask = ngx * p.row_cnt;   // time rows [row_base, row_base + row_cnt) (t-slab: halo row apart)
   const size_t plane = (size_t)nx * N;
   const int B = p.B;
   const int CS4 = RW * B / 4;
@@ -290,7 +290,7 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
   float4 e0[GPT], e1[GPT];     // next task's edge-row terms (row x0, row x0+RW-1)
   float ev = 0.f;              // next task's strip-edge term number tid
   auto load_rows = [&](int task) {
-    const int j = task / ngx, x0 = (task - j * ngx) * RW;
+    const int jt = task / ngx, j = p.row_base + jt, x0 = (task - jt * ngx) * RW;
     if (tid < NEY) ev = p.ey[((size_t)j * nx + x0) * NSTRIP * 2 + tid];   // first: waited for alone
     const float* R0 = p.res + (size_t)j * plane + (size_t)x0 * N;
 #pragma unroll
@@ -301,7 +301,7 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
     }
   };
   auto load_edges = [&](int task) {
-    const int j = task / ngx, tile = task - j * ngx;
+    const int jt = task / ngx, j = p.row_base + jt, tile = task - jt * ngx;
     const float* E = p.ex + ((size_t)j * ngx + tile) * 2 * N;
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
@@ -318,13 +318,23 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
   }
   __syncthreads();
   for (; task < ntask; task += gridDim.x, buf ^= 1) {
-    const int j = task / ngx, x0 = (task - j * ngx) * RW;
+    const int jt = task / ngx, j = p.row_base + jt, x0 = (task - jt * ngx) * RW;
+    // t-slab, last row: the dual formed it with rho_{j+1} = 0; the next slab's rho row 0 (the halo) adds rho/dt
+    const bool hal = p.rho_halo != nullptr && j == p.T - 1;
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
       const int y = 4 * (tid + gi * NT);
       float4 v[RW];
 #pragma unroll
       for (int r = 0; r < RW; ++r) v[r] = rows[gi][r];
+      if (hal) {
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+          const float4 hv = ld4(p.rho_halo + (size_t)(x0 + r) * N + y);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) f4set(v[r], e, f4(v[r], e) + f4(hv, e) * p.inv_dt);
+        }
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         f4set(v[0], e, f4(v[0], e) + f4(e0[gi], e));

@@ -227,9 +227,14 @@ __global__ void __launch_bounds__(RX * 64, FR ? 2 : 3) k_dual_lds_2d(KP<float> p
         __syncthreads();
       }
     }
-    if constexpr (FR) {   // the window's last row: rho_T = 0, + c/dt (update_fns_in_pdhg.py:80, 95)
+    if constexpr (FR) {
+      // the launch's last row: inside the window (t-slab halo launch of row 0) rho'_{j1} comes from memory;
+      // at the window's end rho_T = 0 and + c/dt (update_fns_in_pdhg.py:80, 95); at a t-slab's end rho_T is
+      // the next slab's row 0, added by k_res_fwdy_fused_2d from the halo
       __syncthreads();
-      finish_res(j1 - 1, (j1 - 1 - j0) & 1, z4(), p.c_over_dt);
+      const bool inner = j1 < p.T;
+      const float4 rnx = inner ? ld4(rd + (size_t)j1 * plane + rxc + y) : z4();
+      finish_res(j1 - 1, (j1 - 1 - j0) & 1, rnx, (!inner && p.last_slab) ? p.c_over_dt : 0.f);
     }
   }
   block_reduce_store<NS>(s, p.partials, ((zbase + (int)blockIdx.z) * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x);

@@ -308,7 +308,7 @@ struct Impl : ImplBase {
       // residual row j needs rho'_{j+1}), so only grids with enough (x, y) tiles to fill the chip
       // (PDHG_FUSE_RES=1 forces it for any eligible size, =0 turns it off)
       if (sizeof(R) == 4 && fast_dual && dual_rx == 8 && fast_rows && RWf == 8 && pb.bc_x == 0 && pb.bc_y == 0 &&
-          pb.egno != 3 && !two_sets && !slab && !xslab) {
+          pb.egno != 3 && !two_sets && !xslab) {
         fuse_res = gxd * gyd >= 1024;
         if (const char* e = getenv("PDHG_FUSE_RES")) fuse_res = atoi(e) != 0;
         if (fuse_res) {
@@ -586,13 +586,15 @@ struct Impl : ImplBase {
   int launch_residual(KP<R> p, int lo, int hi) {
     if (hi <= lo) return PDHG_OK;
     int rc = PDHG_OK;
-    if (fuse_res && res_valid && lo == 0 && hi == pb.T) {
+    if (fuse_res && res_valid && (slab || (lo == 0 && hi == pb.T))) {
       ProfScope ps(this, "residual");
+      p.row_base = lo;
+      p.row_cnt = hi - lo;
       rc = with_fast_rows([&](auto Nc, auto RWc, auto NTc) {
         constexpr int N_ = decltype(Nc)::value, RW_ = decltype(RWc)::value, NT_ = decltype(NTc)::value;
         int r2;
         if constexpr (sizeof(R) == 4 && RW_ == 8 && N_ % 256 == 0 && (N_ / 4) % NT_ == 0) {
-          const dim3 g(std::min((pb.nx / RW_) * pb.T, n_cu));   // persistent, one workgroup per CU (LDS)
+          const dim3 g(std::min((pb.nx / RW_) * (hi - lo), n_cu));   // persistent, one workgroup per CU (LDS)
           auto go = [&](auto ntc) {
             constexpr int NTF = decltype(ntc)::value;
             int r3;
@@ -822,7 +824,7 @@ struct Impl : ImplBase {
     if constexpr (std::is_same<R, float>::value) {
       const dim3 g(gxd, gyd, gz);
       if constexpr (EGNO != 3) {
-        if (fuse_res && p.inplace && lo == 0 && hi == pb.T && gz == 1) {
+        if (fuse_res && p.inplace && gz == 1 && (slab || (lo == 0 && hi == pb.T))) {
           hipLaunchKernelGGL((k_dual_lds_2d<EGNO, 8, true>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase);
           res_valid = true;
           return;

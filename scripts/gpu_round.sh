@@ -1,10 +1,4 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_all.log 2>&1 || exit 1
-for cfg in c3w1 c3; do
-  echo "== $cfg"
-  timeout -k 10 200 python bench.py --no-pmc --no-cpu-baseline --config $cfg --steps 20 --warmup 3 2>/dev/null | python -c "
-import json,sys
-d=json.loads(sys.stdin.read().strip().splitlines()[-1])
-print('it/s %.2f ms %.4f' % (d['value'], d['ms_per_step']), {k: round(v['avg_ms'],4) for k,v in d['kernels'].items()})" || exit 1
-done
+timeout -k 10 400 python -u -m pytest tests/test_gpu_slab.py tests/test_gpu_fused.py -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_slab.log 2>&1 || exit 1
+timeout -k 10 300 python scripts/slab_local_bench.py tslab c3 8 3 > gpurun_out/slab8.json 2> gpurun_out/slab8.err || exit 1

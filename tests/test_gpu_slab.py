@@ -75,3 +75,49 @@ def test_slab_rejects_unsupported(native):
     P = make_problem(1, 2, 48, 40, 4, 0.0)
     with pytest.raises(N.PDHGError):      # nx = 48: no fast x-transform kernel
         SlabContext(0, 2, 4, 1, 48, 40, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"])
+
+
+FUSED_CASES = [
+    # (egno, nx, ny, T, P): the fused residual (k_dual_lds_2d FR + k_res_fwdy_fused_2d) inside t-slabs
+    (1, 512, 256, 6, 2),
+    (2, 512, 256, 7, 3),
+    (2, 4096, 256, 6, 2),      # warp-specialised x transform
+    (1, 512, 256, 3, 3),       # one-row slabs: the halo launch is the whole slab
+    (2, 512, 256, 19, 2),      # residual tiles of 8 rows + remainder rows
+]
+
+
+@pytest.mark.parametrize("egno,nx,ny,T,nr", FUSED_CASES,
+                         ids=[f"e{c[0]}_{c[1]}x{c[2]}_T{c[3]}_P{c[4]}" for c in FUSED_CASES])
+def test_slabs_fused_residual(native, egno, nx, ny, T, nr, monkeypatch):
+    """The dual sweep forms the next residual inside every slab (two launches: the rows without the phi_bar
+    halo, then row 0 with rho'_1 read back); the slab's last row gets the next slab's rho/dt from the halo
+    in k_res_fwdy_fused_2d.  Must match the fused single context."""
+    import torch
+    from pdhg_amd.context import PDHGContext
+    from pdhg_amd.slab import LocalComm, SlabRunner, join_state, slab_bounds, split_state
+    monkeypatch.setenv("PDHG_FUSE_RES", "1")
+    monkeypatch.setenv("PDHG_SHORT_T", "0")
+    P = make_problem(egno, 2, nx, ny, T, 0.0)
+    tau, sigma, n = 0.1 / 1.5, 0.1 * 1.5, 6
+    ref = PDHGContext(egno, 2, nx, ny, T, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"], precision="fp32")
+    assert ref.path_info("fused_residual") == 1
+    ref.set_state(P["phi"], P["rho"], P["alp"])
+    st_ref = ref.iterate(n, tau, sigma, -1.0, 1)
+    phi_r, rho_r, alp_r = ref.get_state()
+    slabs = _slabs(P, nr, 1)
+    for s in slabs:
+        assert s.path_info("fused_residual") == 1
+    for s, part in zip(slabs, split_state(P["phi"], P["rho"], P["alp"], slab_bounds(T, nr))):
+        s.set_state(*part)
+    st = SlabRunner(slabs, LocalComm(nr)).iterate(n, tau, sigma, -1.0, 1)
+    torch.cuda.synchronize()
+    phi_s, rho_s, alp_s = join_state([s.get_state() for s in slabs])
+    assert st["iters"] == st_ref["iters_run"] == n
+    assert rel(phi_s, phi_r) < 2e-5
+    assert rel(rho_s, rho_r) < 2e-4
+    assert rel(np.stack(alp_s), np.stack(alp_r)) < 2e-4
+    assert abs(st["err1"] - st_ref["err1"]) <= 1e-3 * st_ref["err1"]
+    for s in slabs:
+        s.close()
+    ref.close()
