@@ -205,6 +205,19 @@ int pdhg_slab_plane_out(pdhg_ctx* ctx, int which, void* dst); /* 0 rho row 0, 1 
                                                                  3 [D, S1] of the long-range modes */
 int pdhg_slab_plane_in(pdhg_ctx* ctx, int which, const void* src); /* 0 rho halo, 1 phi_bar row 0 */
 int pdhg_slab_status(pdhg_ctx* ctx, pdhg_stats* st);
+/* Partitioned carry exchange (pdhg_amd.slab default): the column blocks are split into nparts parts so the
+ * neighbour planes of part q travel while part q+1 sweeps forward and part q-1 sweeps backward:
+ *   per part: forward_part -> carry_out_part(DS) -> [D -> next slab, S1 -> previous slab, modes part_modes]
+ *   plane_out(3) -> [allgather long-range modes]
+ *   per part: [wait for its planes] -> fixup_nb_part -> backward_part;   then update(tau, sums).
+ * forward_part(q, n) over all q equals slab_forward; backward_part over all q + update equals slab_backward. */
+int pdhg_slab_part_modes(pdhg_ctx* ctx, int part, int nparts, unsigned long long* m0, unsigned long long* m1);
+int pdhg_slab_forward_part(pdhg_ctx* ctx, double tau, int part, int nparts);
+int pdhg_slab_carry_out_part(pdhg_ctx* ctx, void* dst, int part, int nparts);   /* [D, S1] planes, modes of part */
+int pdhg_slab_fixup_nb_part(pdhg_ctx* ctx, const void* D_left, const void* S1_right, const void* all_long,
+                            const void* all_GS, int rank, int nranks, int part, int nparts);
+int pdhg_slab_backward_part(pdhg_ctx* ctx, double tau, int part, int nparts);
+int pdhg_slab_update(pdhg_ctx* ctx, double tau, double* sums);            /* inverse y + update + sums */
 
 /* ---------------- x-slab decomposition (multi-GPU for T = 1 marching windows) -----------
  * New capability (the reference has no distributed path).  The reference's default marches windows of

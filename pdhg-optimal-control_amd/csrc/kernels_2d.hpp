@@ -145,7 +145,7 @@ __global__ void __launch_bounds__(512) k_precond_xt_2d(KP<R> p, F plx, const cpl
   R* sth = reinterpret_cast<R*>(Bf + NC);
   R* sE = sth + M;
   R* sbp = sE + M;
-  const int b = blockIdx.x;
+  const int b = blockIdx.x + p.b0;
   R* wb = p.work + (size_t)b * M;
   const size_t kstride = (size_t)p.nb * M;
   const R ae = p.ae;

@@ -556,7 +556,7 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
   C* sE = sth + NI;
   C* sbp = sE + NI;
   const int T = p.T, tid = threadIdx.x;
-  const int b = blockIdx.x;
+  const int b = blockIdx.x + p.b0;
   constexpr int M = N * B;
   float* wb = p.work + (size_t)b * M;
   const size_t kstride = (size_t)p.nb * M;
@@ -731,7 +731,7 @@ __global__ void __launch_bounds__(512) k_precond_xt_ws_2d(KP<float> p, const flo
   const int T = p.T, tid = threadIdx.x;
   const bool fftg = tid < NTF;                 // wave-uniform role
   const int tt = fftg ? 0 : tid - NTF;         // Thomas-group thread
-  const int b = blockIdx.x;
+  const int b = blockIdx.x + p.b0;
   constexpr int M = N * B;
   float* wb = p.work + (size_t)b * M;
   const size_t kstride = (size_t)p.nb * M;

@@ -219,11 +219,11 @@ __device__ __forceinline__ double slab_pivot(const KP<R>& p, int k, double dd, d
 // bound as the neighbour exchange's short-range classification (LONG_RANGE_DELTA = 2^-40).
 constexpr double kSlabDrop = 9.094947017729282e-13;   // 2^-40
 template <typename R>
-__global__ void __launch_bounds__(256) k_slab_sums(KP<R> p, int data, R* __restrict__ out) {
+__global__ void __launch_bounds__(256) k_slab_sums(KP<R> p, int data, R* __restrict__ out, size_t m0, size_t m1) {
   if (data && p.ctrl->done) return;
   const size_t M = (size_t)p.nb * p.nx * p.B;
-  const size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= M) return;
+  const size_t m = m0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;   // modes [m0, m1)
+  if (m >= m1) return;
   double dd, h;
   slab_mode(p, m, dd, h);
   double P = 1.0, s = 0.0;
@@ -289,11 +289,12 @@ template <typename R>
 __global__ void __launch_bounds__(256) k_slab_fix_nb(KP<R> p, const R* __restrict__ ownDS, const R* __restrict__ D_left,
                                                      const R* __restrict__ S1_right, const R* __restrict__ allLong,
                                                      const int* __restrict__ pos, int K, const R* __restrict__ allGS,
-                                                     int rank, int nranks, R* __restrict__ carry_y) {
+                                                     int rank, int nranks, R* __restrict__ carry_y, size_t m0,
+                                                     size_t m1) {
   if (p.ctrl->done) return;
   const size_t M = (size_t)p.nb * p.nx * p.B;
-  const size_t m = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= M) return;
+  const size_t m = m0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;   // modes [m0, m1)
+  if (m >= m1) return;
   double c_own = 0.0, y = 0.0;
   const int q = pos[m];
   if (q >= 0) {

@@ -53,6 +53,9 @@ struct KP {
   // x-slab decomposition (pdhg_create_xslab): rows [xl0, xl1) are this rank's own rows; the others are
   // ghost / padding rows, which the dual neither stores nor sums (all rows otherwise: 0, nx)
   int xl0, xl1;
+  // x transform on a column-block range (t-slab: the carry exchange of one part overlaps the other's sweep):
+  // workgroup b handles block b0 + b
+  int b0;
 };
 
 // neighbour index along an axis of length n with boundary condition bc

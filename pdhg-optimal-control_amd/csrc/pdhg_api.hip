@@ -676,13 +676,14 @@ struct Impl : ImplBase {
   // ---------------- launches ----------------
   // x transform + Thomas in t + inverse x transform of the spectral blocks in p.work (p.nx-point lines,
   // p.nb blocks); p.xt_phase selects the sweeps (t-slab)
-  int launch_precond(const KP<R>& p) {
+  int launch_precond(const KP<R>& p, int nblk = -1) {   // nblk: blocks [p.b0, p.b0 + nblk) (default: all)
     int rc = PDHG_OK;
+    if (nblk < 0) nblk = p.nb - p.b0;
     if (fast_xt) {
       ProfScope ps(this, "precond");
       rc = PDHG_OK;
       if constexpr (sizeof(R) == 4) {
-        const dim3 g(p.nb);
+        const dim3 g(nblk);
         auto go = [&](auto kern) -> int {
           int r2;
           if ((r2 = ensure_lds(kern, lds_fast_xt))) return r2;
@@ -709,7 +710,7 @@ struct Impl : ImplBase {
       if (rc) return rc;
     } else {
       ProfScope ps(this, "precond");
-      dim3 g(p.nb);
+      dim3 g(nblk);
       if (p.xt_phase != 0) return fail(PDHG_ERR_UNSUPPORTED, "t-slab sweeps need the fp32 power-of-two x kernels");
       rc = with_xt_fft([&](auto f) {
         using F = decltype(f);
@@ -966,7 +967,8 @@ struct Impl : ImplBase {
   // ... -> slab_outer -> [allreduce] -> slab_outer_finalize.  With one slab this is iterate().
   int need_slab() const { return slab ? PDHG_OK : fail(PDHG_ERR_STATE, "not a t-slab context"); }
   int slab_G(R* out) {   // [G, S2] (iteration-invariant)
-    hipLaunchKernelGGL((k_slab_sums<R>), dim3((unsigned)((Mspec + 255) / 256)), dim3(256), 0, stream, kp, 0, out);
+    hipLaunchKernelGGL((k_slab_sums<R>), dim3((unsigned)((Mspec + 255) / 256)), dim3(256), 0, stream, kp, 0, out,
+                       (size_t)0, Mspec);
     HIP_TRY(hipGetLastError());
     return PDHG_OK;
   }
@@ -979,13 +981,54 @@ struct Impl : ImplBase {
     if ((parts & 2) && (rc = launch_residual(kp, split, T))) return rc;
     return PDHG_OK;
   }
-  int slab_forward(R tau) {   // zero-carry forward sweep + this slab's [D, S1] (after both residual parts)
-    int rc = launch_primal(tau, 2, 1);
+  int slab_forward(R tau) { return slab_forward_part(tau, 0, 1); }
+  // part `part` of `nparts` of the column blocks: blocks [b0, b1), spectral modes [m0, m1)
+  void part_range(int part, int nparts, int& b0, int& b1, size_t& m0, size_t& m1) const {
+    b0 = (int)((long long)kp.nb * part / nparts);
+    b1 = (int)((long long)kp.nb * (part + 1) / nparts);
+    const size_t Mb = (size_t)pb.nx * kp.B;
+    m0 = b0 * Mb;
+    m1 = b1 * Mb;
+  }
+  // zero-carry forward sweep + [D, S1] of one part of the column blocks (after both residual parts)
+  int slab_forward_part(R tau, int part, int nparts) {
+    int b0, b1;
+    size_t m0, m1;
+    part_range(part, nparts, b0, b1, m0, m1);
+    if (b1 <= b0) return PDHG_OK;
+    KP<R> p = kp;
+    p.tau = tau;
+    p.xt_phase = 1;
+    p.b0 = b0;
+    int rc = launch_precond(p, b1 - b0);
     if (rc) return rc;
-    hipLaunchKernelGGL((k_slab_sums<R>), dim3((unsigned)((Mspec + 255) / 256)), dim3(256), 0, stream, kp, 1, dsbuf);
+    hipLaunchKernelGGL((k_slab_sums<R>), dim3((unsigned)((m1 - m0 + 255) / 256)), dim3(256), 0, stream, kp, 1, dsbuf,
+                       m0, m1);
     HIP_TRY(hipGetLastError());
     return PDHG_OK;
   }
+  int slab_carry_out_part(void* dst, int part, int nparts) {   // [D, S1] modes [m0, m1) into dst (2 planes)
+    int b0, b1;
+    size_t m0, m1;
+    part_range(part, nparts, b0, b1, m0, m1);
+    if (m1 <= m0) return PDHG_OK;
+    R* d = static_cast<R*>(dst);
+    HIP_TRY(hipMemcpyAsync(d + m0, dsbuf + m0, (m1 - m0) * sizeof(R), hipMemcpyDeviceToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(d + Mspec + m0, dsbuf + Mspec + m0, (m1 - m0) * sizeof(R), hipMemcpyDeviceToDevice, stream));
+    return PDHG_OK;
+  }
+  int slab_backward_part(R tau, int part, int nparts) {   // carry-corrected backward sweep of one part
+    int b0, b1;
+    size_t m0, m1;
+    part_range(part, nparts, b0, b1, m0, m1);
+    if (b1 <= b0) return PDHG_OK;
+    KP<R> p = kp;
+    p.tau = tau;
+    p.xt_phase = 2;
+    p.b0 = b0;
+    return launch_precond(p, b1 - b0);
+  }
+  int slab_update(R tau, double* sums) { return launch_primal(tau, 4, 0, sums); }   // after every part
   // classify the modes once from everybody's [G, S2]: long-range where some slab's gain G >= delta
   int slab_long_modes(const R* allGS, int nranks, double delta, int* K_out) {
     R* gmax = nullptr;
@@ -1019,10 +1062,15 @@ struct Impl : ImplBase {
     *K_out = long_K;
     return PDHG_OK;
   }
-  int slab_fixup_nb(const R* D_left, const R* S1_right, const R* allLong, const R* allGS, int rank, int nranks) {
+  int slab_fixup_nb(const R* D_left, const R* S1_right, const R* allLong, const R* allGS, int rank, int nranks,
+                    int part = 0, int nparts = 1) {
     if (long_K < 0) return fail(PDHG_ERR_STATE, "pdhg_slab_long_modes has not been called");
-    hipLaunchKernelGGL((k_slab_fix_nb<R>), dim3((unsigned)((Mspec + 255) / 256)), dim3(256), 0, stream, kp, dsbuf,
-                       D_left, S1_right, allLong, long_pos, long_K, allGS, rank, nranks, carry_y);
+    int b0, b1;
+    size_t m0, m1;
+    part_range(part, nparts, b0, b1, m0, m1);
+    if (m1 <= m0) return PDHG_OK;
+    hipLaunchKernelGGL((k_slab_fix_nb<R>), dim3((unsigned)((m1 - m0 + 255) / 256)), dim3(256), 0, stream, kp, dsbuf,
+                       D_left, S1_right, allLong, long_pos, long_K, allGS, rank, nranks, carry_y, m0, m1);
     HIP_TRY(hipGetLastError());
     return PDHG_OK;
   }
@@ -1813,6 +1861,44 @@ int pdhg_xslab_precond(pdhg_ctx* ctx) {
 int pdhg_xslab_update(pdhg_ctx* ctx, double tau, double* sums) {
   if (!sums) return fail(PDHG_ERR_ARG, "null sums");
   return xslab_dispatch(ctx, [&](auto& im) { return im.xs_update((float)tau, sums); });
+}
+
+int pdhg_slab_part_modes(pdhg_ctx* ctx, int part, int nparts, unsigned long long* m0, unsigned long long* m1) {
+  if (!m0 || !m1 || nparts < 1 || part < 0 || part >= nparts) return fail(PDHG_ERR_ARG, "part %d of %d", part, nparts);
+  return slab_dispatch(ctx, [&](auto& im) {
+    int b0, b1;
+    size_t a, b;
+    im.part_range(part, nparts, b0, b1, a, b);
+    *m0 = a;
+    *m1 = b;
+    return (int)PDHG_OK;
+  });
+}
+int pdhg_slab_forward_part(pdhg_ctx* ctx, double tau, int part, int nparts) {
+  if (nparts < 1 || part < 0 || part >= nparts) return fail(PDHG_ERR_ARG, "part %d of %d", part, nparts);
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_forward_part((float)tau, part, nparts); });
+}
+int pdhg_slab_carry_out_part(pdhg_ctx* ctx, void* dst, int part, int nparts) {
+  if (!dst || nparts < 1 || part < 0 || part >= nparts) return fail(PDHG_ERR_ARG, "null plane or part %d of %d", part, nparts);
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_carry_out_part(dst, part, nparts); });
+}
+int pdhg_slab_fixup_nb_part(pdhg_ctx* ctx, const void* D_left, const void* S1_right, const void* all_long,
+                            const void* all_GS, int rank, int nranks, int part, int nparts) {
+  if (!D_left || !S1_right || !all_GS || rank < 0 || rank >= nranks || nparts < 1 || part < 0 || part >= nparts)
+    return fail(PDHG_ERR_ARG, "null plane, rank %d of %d or part %d of %d", rank, nranks, part, nparts);
+  return slab_dispatch(ctx, [&](auto& im) {
+    return im.slab_fixup_nb(static_cast<const float*>(D_left), static_cast<const float*>(S1_right),
+                            static_cast<const float*>(all_long), static_cast<const float*>(all_GS), rank, nranks,
+                            part, nparts);
+  });
+}
+int pdhg_slab_backward_part(pdhg_ctx* ctx, double tau, int part, int nparts) {
+  if (nparts < 1 || part < 0 || part >= nparts) return fail(PDHG_ERR_ARG, "part %d of %d", part, nparts);
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_backward_part((float)tau, part, nparts); });
+}
+int pdhg_slab_update(pdhg_ctx* ctx, double tau, double* sums) {
+  if (!sums) return fail(PDHG_ERR_ARG, "null sums");
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_update((float)tau, sums); });
 }
 
 }  // extern "C"

@@ -29,7 +29,8 @@ EXPORTS = (
     "pdhg_create_slab", "pdhg_set_stream", "pdhg_slab_plane_size", "pdhg_slab_begin", "pdhg_slab_carry_gain",
     "pdhg_slab_residual", "pdhg_slab_forward", "pdhg_slab_fixup", "pdhg_slab_long_modes", "pdhg_slab_fixup_nb", "pdhg_slab_backward", "pdhg_slab_primal_finalize", "pdhg_slab_dual",
     "pdhg_slab_dual_finalize", "pdhg_slab_outer", "pdhg_slab_outer_finalize", "pdhg_slab_plane_out",
-    "pdhg_slab_plane_in", "pdhg_slab_status",
+    "pdhg_slab_plane_in", "pdhg_slab_status", "pdhg_slab_part_modes", "pdhg_slab_forward_part",
+    "pdhg_slab_carry_out_part", "pdhg_slab_fixup_nb_part", "pdhg_slab_backward_part", "pdhg_slab_update",
     # x-slab decomposition (multi-GPU for T = 1 windows)
     "pdhg_create_xslab", "pdhg_xslab_layout", "pdhg_xslab_sizes", "pdhg_xslab_halo_out", "pdhg_xslab_halo_in",
     "pdhg_xslab_residual", "pdhg_xslab_wire", "pdhg_xslab_precond", "pdhg_xslab_update",
@@ -133,6 +134,14 @@ def load():
         "pdhg_slab_plane_out": ([P, ctypes.c_int, P], ctypes.c_int),
         "pdhg_slab_plane_in": ([P, ctypes.c_int, P], ctypes.c_int),
         "pdhg_slab_status": ([P, ctypes.POINTER(pdhg_stats)], ctypes.c_int),
+        "pdhg_slab_part_modes": ([P, ctypes.c_int, ctypes.c_int] + [ctypes.POINTER(ctypes.c_ulonglong)] * 2,
+                                 ctypes.c_int),
+        "pdhg_slab_forward_part": ([P, ctypes.c_double, ctypes.c_int, ctypes.c_int], ctypes.c_int),
+        "pdhg_slab_carry_out_part": ([P, P, ctypes.c_int, ctypes.c_int], ctypes.c_int),
+        "pdhg_slab_fixup_nb_part": ([P, P, P, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int],
+                                    ctypes.c_int),
+        "pdhg_slab_backward_part": ([P, ctypes.c_double, ctypes.c_int, ctypes.c_int], ctypes.c_int),
+        "pdhg_slab_update": ([P, ctypes.c_double, P], ctypes.c_int),
         "pdhg_create_xslab": ([ctypes.POINTER(pdhg_problem), ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                ctypes.POINTER(P)], ctypes.c_int),
         "pdhg_xslab_layout": ([P] + [ctypes.POINTER(ctypes.c_int)] * 4, ctypes.c_int),

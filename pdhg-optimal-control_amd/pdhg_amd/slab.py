@@ -133,6 +133,28 @@ class SlabContext(PhaseOps, PDHGContext):
     def plane_out(self, which, dst):
         N.check(self._lib.pdhg_slab_plane_out(self._h, int(which), _ptr(dst)))
 
+    # partitioned carry exchange (column-block parts)
+    def part_modes(self, part, nparts):
+        a, b = ctypes.c_ulonglong(), ctypes.c_ulonglong()
+        N.check(self._lib.pdhg_slab_part_modes(self._h, int(part), int(nparts), ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+    def forward_part(self, tau, part, nparts):
+        N.check(self._lib.pdhg_slab_forward_part(self._h, float(tau), int(part), int(nparts)))
+
+    def carry_out_part(self, dst, part, nparts):
+        N.check(self._lib.pdhg_slab_carry_out_part(self._h, _ptr(dst), int(part), int(nparts)))
+
+    def fixup_nb_part(self, D_left, S1_right, allLong, allGS, part, nparts):
+        N.check(self._lib.pdhg_slab_fixup_nb_part(self._h, _ptr(D_left), _ptr(S1_right), _ptr(allLong), _ptr(allGS),
+                                                  self.rank, self.nranks, int(part), int(nparts)))
+
+    def backward_part(self, tau, part, nparts):
+        N.check(self._lib.pdhg_slab_backward_part(self._h, float(tau), int(part), int(nparts)))
+
+    def update(self, tau, sums):
+        N.check(self._lib.pdhg_slab_update(self._h, float(tau), _ptr(sums)))
+
     def plane_in(self, which, src):
         N.check(self._lib.pdhg_slab_plane_in(self._h, int(which), _ptr(src)))
 
@@ -270,10 +292,11 @@ class SlabRunner:
     """Drives the slabs of this process through outer iterations (pdhg_iterate's loop, split at
     every point where slabs exchange data)."""
 
-    def __init__(self, slabs, comm, overlap=True, exchange="neighbour", delta=LONG_RANGE_DELTA):
+    def __init__(self, slabs, comm, overlap=True, exchange="neighbour", delta=LONG_RANGE_DELTA, parts=2):
         """overlap: halos on a second stream while the interior rows compute.  exchange: "neighbour"
         (D / S1 planes to the adjacent slabs + an allgather of the long-range modes only) or
-        "allgather" (every slab's full [D, S1] planes)."""
+        "allgather" (every slab's full [D, S1] planes).  parts (neighbour exchange with overlap): the column
+        blocks are swept in `parts` parts so each part's carry planes travel while the next part sweeps."""
         import torch
         if exchange not in ("neighbour", "allgather"):
             raise ValueError("exchange must be 'neighbour' or 'allgather'")
@@ -281,6 +304,7 @@ class SlabRunner:
         self.slabs, self.comm = list(slabs), comm
         self.exchange = exchange
         self.side = torch.cuda.Stream() if overlap else None   # halo stream
+        self.parts = int(parts) if (exchange == "neighbour" and overlap) else 1
         dev = torch.device("cuda", torch.cuda.current_device())
         sp, spec = self.slabs[0].plane_sizes()
         f32, f64 = torch.float32, torch.float64
@@ -296,6 +320,7 @@ class SlabRunner:
             s.carry_gain(b["GS"])
         self.allGS = comm.allgather([b["GS"] for b in self.b])   # iteration-invariant
         self.n_long = None
+        self.part_modes = [self.slabs[0].part_modes(q, self.parts) for q in range(self.parts)]
         if exchange == "neighbour":
             Ks = [s.long_modes(self.allGS[i], delta) for i, s in enumerate(self.slabs)]
             self.n_long = Ks[0]
@@ -338,6 +363,9 @@ class SlabRunner:
                 s.plane_in(RHO_HALO, b["rho_recv"])
             s.residual(EDGE)
         # primal: zero-carry forward sweeps, ONE allgather of [D, S1], carry folds, backward sweeps + update
+        if self.exchange == "neighbour" and self.parts > 1:
+            self._primal_parts(tau)
+            return self._after_primal(sigma, eps, k)
         self._each("forward", tau)
         for s, b in zip(S, B):
             s.plane_out(CARRY_DS, b["DS"])
@@ -358,6 +386,38 @@ class SlabRunner:
             for i, s in enumerate(S):
                 s.fixup(allDS[i], self.allGS[i])
                 s.backward(tau, B[i]["sums"])
+        self._after_primal(sigma, eps, k)
+
+    def _primal_parts(self, tau):
+        """Forward sweep, carry exchange and backward sweep in column-block parts: part q's D / S1 planes
+        go to the neighbours on the side stream while part q+1 sweeps forward (and part q-1 backward)."""
+        torch = self.torch
+        S, B, C = self.slabs, self.b, self.comm
+        spec = B[0]["Dl"].numel()
+        done = []
+        for q in range(self.parts):
+            lo, hi = self.part_modes[q]
+            for s, b in zip(S, B):
+                s.forward_part(tau, q, self.parts)
+                s.carry_out_part(b["DS"], q, self.parts)
+            self._halo(C.shift_both, [b["DS"][lo:hi] for b in B], [b["Dl"][lo:hi] for b in B],
+                       [b["DS"][spec + lo:spec + hi] for b in B], [b["S1r"][lo:hi] for b in B])
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+            done.append(ev)
+        for s, b in zip(S, B):
+            s.plane_out(CARRY_LONG, b["LONG"])
+        allLong = C.allgather([b["LONG"] for b in B])
+        for q in range(self.parts):
+            torch.cuda.current_stream().wait_event(done[q])
+            for i, s in enumerate(S):
+                s.fixup_nb_part(B[i]["Dl"], B[i]["S1r"], allLong[i], self.allGS[i], q, self.parts)
+                s.backward_part(tau, q, self.parts)
+        for s, b in zip(S, B):
+            s.update(tau, b["sums"])
+
+    def _after_primal(self, sigma, eps, k):
+        S, B, C = self.slabs, self.b, self.comm
         # phi_bar halo (row T of slab r -> row 0 of slab r+1: the dual's phi_bar_j), overlapped with the
         # primal sums all-reduce and the dual of the rows that do not read it
         for s, b in zip(S, B):
