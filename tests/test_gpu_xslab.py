@@ -23,6 +23,9 @@ CASES = [
     (2, 8192, 256, 1, 2, 1, 0.0),    # half-real x blocks (C4's nx)
     (1, 256, 256, 2, 2, 1, 0.0),     # generic x kernel (runtime plan)
     (2, 384, 256, 1, 2, 1, 0.0),     # non-power-of-two nx (radix-3 plan), 192-row slabs
+    (1, 512, 256, 1, 2, 3, 0.0),     # T = 1 with two buffer sets: the row-per-thread dual's live-row mask
+    (2, 512, 256, 2, 4, 1, 0.0),     # T = 2: short-window kernels (single-role x transform, row-per-thread dual)
+    (2, 512, 256, 8, 2, 1, 0.0),     # T = 8: 8-row LDS dual, single-role x transform
 ]
 
 
