@@ -68,6 +68,121 @@ __global__ void __launch_bounds__(1024) k_res_fwdx_1d(KP<R> p, F plx, const cplx
   }
 }
 
+// ---- four-step DHT of row pairs for nx = 65536 = 256 x 256 (fp32; C1, BASELINE configs[1]) ----
+// x = 256 n1 + n2, k = k1 + 256 k2:  X[k] = sum_n2 W_256^{n2 k2} W_65536^{n2 k1} sum_n1 W_256^{n1 k1} z[256 n1 + n2].
+// A line that does not fit in LDS is split over 16 + 9 workgroups per row pair instead of one workgroup
+// per pair (T = 400 rows gave 200 workgroups for 256 CUs).
+// Stage 1 (grid 16 x pairs): 16 columns n2 per workgroup, 256-point FFTs over n1 in LDS, times
+// W_65536^{n2 k1}, to Y[pair][k1][n2] (global scratch).  MODE 0: z = residual rows j, j+1
+// (update_fns_in_pdhg.py:72-81); MODE 1: z = spectrum rows j, j+1 of work (the inverse DHT).
+constexpr int kFsN1 = 256, kFsL = 16;
+template <int MODE, int EGNO>
+__global__ void __launch_bounds__(256) k_fs1_1d(KP<float> p, const float2* __restrict__ tw256,
+                                                const float2* __restrict__ twN, float2* __restrict__ Y) {
+  using C = float2;
+  if (p.ctrl->done) return;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  C* A = reinterpret_cast<C*>(smem_raw);
+  C* Bf = A + kFsN1 * kFsL;
+  const int nx = p.nx, tile = blockIdx.x, pair = blockIdx.y;
+  const int j = 2 * pair;
+  const bool has2 = (j + 1) < p.T;
+  const int cur = p.ctrl->cur;
+  for (int i = threadIdx.x; i < kFsN1 * kFsL; i += blockDim.x) {
+    const int n1 = i >> 4, l = i & (kFsL - 1);
+    const int x = kFsN1 * n1 + kFsL * tile + l;
+    float r0, r1 = 0.f;
+    if constexpr (MODE == 0) {
+      r0 = cont_residual_1d<float, EGNO>(p, p.rho[cur], p.alp[cur][0], p.alp[cur][1], j, x);
+      if (has2) r1 = cont_residual_1d<float, EGNO>(p, p.rho[cur], p.alp[cur][0], p.alp[cur][1], j + 1, x);
+    } else {
+      r0 = p.work[(size_t)j * nx + x];
+      if (has2) r1 = p.work[(size_t)(j + 1) * nx + x];
+    }
+    A[i] = make_float2(r0, r1);   // line l (column n2), element n1
+  }
+  __syncthreads();
+  const C* Z = lds_fft_fixed<C, kFsN1, kFsL>(A, Bf, tw256);
+  C* Yp = Y + (size_t)pair * nx;
+  for (int i = threadIdx.x; i < kFsN1 * kFsL; i += blockDim.x) {
+    const int k1 = i >> 4, l = i & (kFsL - 1);
+    const int n2 = kFsL * tile + l;
+    Yp[(size_t)k1 * kFsN1 + n2] = cmul(Z[i], twN[(n2 * k1) & (nx - 1)]);
+  }
+}
+
+// Stage 2 (grid 9 x pairs): rows k1 = 16 g + l (k1 <= 128) and their Hartley partners (256 - k1) mod 256,
+// 256-point FFTs over n2, then the Hartley unpack of the two packed real lines: H[k] = (Z_k + Z_{N-k})/2 ...
+// (hartley_pair).  MODE 0: the DHT rows go to work (spectral rows j, j+1); MODE 1: they are the inverse
+// transform -- phi' = phi + tau/nx U, phi_bar = 2 phi' - phi and the err1 sums (k_invx_update_1d).
+template <int MODE>
+__global__ void __launch_bounds__(256) k_fs2_1d(KP<float> p, const float2* __restrict__ tw256,
+                                                const float2* __restrict__ Y) {
+  using C = float2;
+  double s[3] = {0.0, 0.0, 0.0};
+  const int nx = p.nx, g = blockIdx.x, pair = blockIdx.y;
+  const int row = blockIdx.y * gridDim.x + blockIdx.x;
+  if (p.ctrl->done) {
+    block_reduce_store<3>(s, p.partials, row);
+    return;
+  }
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  C* A = reinterpret_cast<C*>(smem_raw);     // rows k1 (lines l)
+  C* Ab = A + kFsN1 * kFsL;
+  C* Bm = Ab + kFsN1 * kFsL;                  // partner rows (256 - k1) mod 256
+  C* Bb = Bm + kFsN1 * kFsL;
+  const int j = 2 * pair;
+  const bool has2 = (j + 1) < p.T;
+  const C* Yp = Y + (size_t)pair * nx;
+  for (int i = threadIdx.x; i < kFsN1 * kFsL; i += blockDim.x) {
+    const int l = i >> 8, n2 = i & (kFsN1 - 1);   // consecutive threads read consecutive n2
+    const int k1 = kFsL * g + l;
+    const int k1b = (kFsN1 - k1) & (kFsN1 - 1);
+    const bool ok = k1 <= kFsN1 / 2;
+    A[n2 * kFsL + l] = ok ? Yp[(size_t)k1 * kFsN1 + n2] : make_float2(0.f, 0.f);
+    Bm[n2 * kFsL + l] = ok ? Yp[(size_t)k1b * kFsN1 + n2] : make_float2(0.f, 0.f);
+  }
+  __syncthreads();
+  const C* ZA = lds_fft_fixed<C, kFsN1, kFsL>(A, Ab, tw256);
+  const C* ZB = lds_fft_fixed<C, kFsN1, kFsL>(Bm, Bb, tw256);
+  const float scale = p.tau * p.inv_n;
+  for (int i = threadIdx.x; i < kFsN1 * kFsL; i += blockDim.x) {
+    const int k2 = i >> 4, l = i & (kFsL - 1);   // consecutive threads: consecutive k1 (64-B segments)
+    const int k1 = kFsL * g + l;
+    if (k1 > kFsN1 / 2) continue;
+    const bool self = (k1 == 0) || (k1 == kFsN1 / 2);   // the partner row is the row itself
+    const int k2m = (k1 == 0) ? ((kFsN1 - k2) & (kFsN1 - 1)) : (kFsN1 - 1 - k2);
+    const C z = ZA[k2 * kFsL + l], w = ZB[k2m * kFsL + l];   // Z_k, Z_{N-k}
+    const int k = k1 + kFsN1 * k2, km = (nx - k) & (nx - 1);
+    // DHT pair at k (from Z_k, Z_{N-k}) and at N-k (roles swapped); a self-paired row writes k only
+    const float ha = 0.5f * ((z.x + w.x) - (z.y - w.y)), hb = 0.5f * ((z.y + w.y) - (w.x - z.x));
+    const float ma = 0.5f * ((w.x + z.x) - (w.y - z.y)), mb = 0.5f * ((w.y + z.y) - (z.x - w.x));
+    const int nout = self ? 1 : 2;
+    for (int o = 0; o < nout; ++o) {
+      const int kk = o ? km : k;
+      const float va = o ? ma : ha, vb = o ? mb : hb;
+      if constexpr (MODE == 0) {
+        p.work[(size_t)j * nx + kk] = va;
+        if (has2) p.work[(size_t)(j + 1) * nx + kk] = vb;
+      } else {
+        for (int r = 0; r < 2; ++r) {
+          if (r == 1 && !has2) break;
+          const size_t idx = (size_t)(j + 1 + r) * nx + kk;
+          const float old = p.phi[idx];
+          const float nw = old + scale * (r ? vb : va);
+          p.phi[idx] = nw;
+          p.phibar[idx] = 2.f * nw - old;
+          const double d = (double)nw - (double)old;
+          s[0] += d * d;
+          s[1] += (double)old * (double)old;
+          s[2] += (double)nw * (double)nw;
+        }
+      }
+    }
+  }
+  if constexpr (MODE == 1) block_reduce_store<3>(s, p.partials, row);
+}
+
 // grid: ceil(nx/256); one thread per mode, sequential in t.
 // (C - lam)^pow u - Ct Dtt u = v with u_0 = 0, Neumann at t = T  (utils_precond.py:105-140)
 template <typename R>

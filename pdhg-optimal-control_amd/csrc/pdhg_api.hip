@@ -115,6 +115,8 @@ struct Impl : ImplBase {
   // fast row kernels (fp32, power-of-two ny): RW rows per workgroup, NTf threads
   bool fast_rows = false;
   bool glb_line = false;          // 1-D line FFTs over global scratch (nx beyond LDS)
+  bool fourstep = false;          // fp32 1-D nx = 65536: four-step DHT over 16 + 9 workgroups per row pair
+  C* tw256 = nullptr;             // W_256 table of the four-step stages
   bool half_real = false;         // 2-D nx = 8192: one real column per x-transform block
   int nt1d = 256;                 // 1-D residual / update block size (1024 on the global-scratch path)
   bool fast_xt = false;
@@ -328,14 +330,17 @@ struct Impl : ImplBase {
         glb_line = true;
         lds_res = 0;
         nt1d = 1024;
+        // four-step DHT over 16 + 9 workgroups per row pair: parity-clean but measured slower at C1 (1.56 vs
+        // 1.41 ms per iteration: 64-B input segments, one workgroup per CU in stage 2), so opt-in only
+        if (const char* e = getenv("PDHG_FOURSTEP")) fourstep = sizeof(R) == 4 && nx == 65536 && atoi(e) != 0;
       }
       g4 = 1;
       gx5 = (nx + 255) / 256;
       g5 = std::max(1, std::min(T, 8192 / std::max(1, gx5)));
     }
     g_outer = 2048;
-    partial_rows = std::max<size_t>(
-        {(size_t)gx4 * g4, (size_t)gx5 * g5, (size_t)g_outer, (size_t)g_fast_upd, (size_t)gxd * gyd * (gzd + 1), 1});
+    partial_rows = std::max<size_t>({(size_t)gx4 * g4, (size_t)gx5 * g5, (size_t)g_outer, (size_t)g_fast_upd,
+                                     (size_t)gxd * gyd * (gzd + 1), fourstep ? (size_t)9 * ((T + 1) / 2) : 1, 1});
     p.slab = slab ? 1 : 0;
     p.j0 = slab ? slab_j0 : 0;
     p.Tg = slab ? slab_Tg : T;
@@ -471,6 +476,11 @@ struct Impl : ImplBase {
       auto t = twiddles<R>(nxg);
       if ((rc = alloc(&twx, nxg))) return rc;
       HIP_TRY(hipMemcpy(twx, t.data(), nxg * sizeof(C), hipMemcpyHostToDevice));
+    }
+    if (fourstep) {
+      auto t = twiddles<R>(256);
+      if ((rc = alloc(&tw256, 256))) return rc;
+      HIP_TRY(hipMemcpy(tw256, t.data(), 256 * sizeof(C), hipMemcpyHostToDevice));
     }
     if (is2d) {
       auto t = twiddles<R>(ny);
@@ -782,6 +792,9 @@ struct Impl : ImplBase {
         hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, p.partials, upd_rows, row0_sq, p.ctrl);
     } else {
       int rc;
+      if constexpr (sizeof(R) == 4) {
+        if (fourstep) return launch_fourstep_1d(p);
+      }
       {
         ProfScope ps(this, "residual");
         rc = with_line_fft(plx, [&](auto f) {
@@ -816,6 +829,42 @@ struct Impl : ImplBase {
       hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, p.partials, gx4, row0_sq, p.ctrl);
     }
     HIP_TRY(hipGetLastError());
+    return PDHG_OK;
+  }
+
+  // 1-D primal with the four-step DHT (nx = 65536, fp32): residual + DHT, Thomas, inverse DHT + update
+  int launch_fourstep_1d(const KP<R>& p) {
+    if constexpr (sizeof(R) == 4) {
+      const int npairs = (pb.T + 1) / 2;
+      const size_t lds1 = (size_t)2 * 256 * 16 * sizeof(C), lds2 = 2 * lds1;
+      float2* Y = reinterpret_cast<float2*>(p.gscr);
+      int rc;
+      {
+        ProfScope ps(this, "residual");
+        if (pb.egno == 1) {
+          if ((rc = ensure_lds(k_fs1_1d<0, 1>, lds1))) return rc;
+          hipLaunchKernelGGL((k_fs1_1d<0, 1>), dim3(16, npairs), dim3(256), lds1, stream, p, tw256, twx, Y);
+        } else {
+          if ((rc = ensure_lds(k_fs1_1d<0, 2>, lds1))) return rc;
+          hipLaunchKernelGGL((k_fs1_1d<0, 2>), dim3(16, npairs), dim3(256), lds1, stream, p, tw256, twx, Y);
+        }
+        if ((rc = ensure_lds(k_fs2_1d<0>, lds2))) return rc;
+        hipLaunchKernelGGL((k_fs2_1d<0>), dim3(9, npairs), dim3(256), lds2, stream, p, tw256, Y);
+      }
+      {
+        ProfScope ps(this, "precond");
+        hipLaunchKernelGGL((k_thomas_1d<R>), dim3((pb.nx + 255) / 256), dim3(256), 0, stream, p);
+      }
+      {
+        ProfScope ps(this, "update");
+        if ((rc = ensure_lds(k_fs1_1d<1, 1>, lds1))) return rc;
+        hipLaunchKernelGGL((k_fs1_1d<1, 1>), dim3(16, npairs), dim3(256), lds1, stream, p, tw256, twx, Y);
+        if ((rc = ensure_lds(k_fs2_1d<1>, lds2))) return rc;
+        hipLaunchKernelGGL((k_fs2_1d<1>), dim3(9, npairs), dim3(256), lds2, stream, p, tw256, Y);
+      }
+      hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, p.partials, 9 * npairs, row0_sq, p.ctrl);
+      HIP_TRY(hipGetLastError());
+    }
     return PDHG_OK;
   }
 

@@ -334,3 +334,23 @@ def test_half_real_x_transform_fp32(native, case):
     assert rel(phi_d, phi_o) < 1e-5
     assert rel(rho_d, rho_o) < 2e-4
     ctx.close()
+
+
+@pytest.mark.parametrize("prec", ["fp32"])
+def test_fourstep_1d_opt_in(native, prec, monkeypatch):
+    """C1's line length through the opt-in four-step DHT (PDHG_FOURSTEP=1: 256-point FFT stages split over
+    16 + 9 workgroups per row pair) vs the oracle, same fp32 bounds as the default path."""
+    monkeypatch.setenv("PDHG_FOURSTEP", "1")
+    P = make_problem(2, 1, 65536, 1, 3, 0.0)
+    ctx = device_ctx(P, prec)
+    ctx.set_state(P["phi"], P["rho"], P["alp"])
+    ctx.update_primal(TAU)
+    phi_o = _oracle_primal(P, P["phi"], P["rho"], P["alp"])
+    assert rel(ctx.get_state()[0], phi_o) < 1e-6
+    phi_o, rho_o, _, e1_o, _ = _oracle_iterate(P, 10)
+    ctx.set_state(P["phi"], P["rho"], P["alp"])
+    st = ctx.iterate(10, TAU, SIGMA, -1.0, 1)
+    phi_d, rho_d, _ = ctx.get_state()
+    assert rel(phi_d, phi_o) < 1e-5 and rel(rho_d, rho_o) < 2e-4
+    assert abs(st["err1"] - e1_o) <= 1e-2 * e1_o
+    ctx.close()
