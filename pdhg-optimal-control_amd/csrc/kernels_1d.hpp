@@ -77,7 +77,7 @@ __global__ void __launch_bounds__(1024) k_res_fwdx_1d(KP<R> p, F plx, const cplx
 // (update_fns_in_pdhg.py:72-81); MODE 1: z = spectrum rows j, j+1 of work (the inverse DHT).
 constexpr int kFsN1 = 256, kFsL = 16;
 template <int MODE, int EGNO>
-__global__ void __launch_bounds__(256) k_fs1_1d(KP<float> p, const float2* __restrict__ tw256,
+__global__ void __launch_bounds__(1024) k_fs1_1d(KP<float> p, const float2* __restrict__ tw256,
                                                 const float2* __restrict__ twN, float2* __restrict__ Y) {
   using C = float2;
   if (p.ctrl->done) return;
@@ -116,7 +116,7 @@ __global__ void __launch_bounds__(256) k_fs1_1d(KP<float> p, const float2* __res
 // (hartley_pair).  MODE 0: the DHT rows go to work (spectral rows j, j+1); MODE 1: they are the inverse
 // transform -- phi' = phi + tau/nx U, phi_bar = 2 phi' - phi and the err1 sums (k_invx_update_1d).
 template <int MODE>
-__global__ void __launch_bounds__(256) k_fs2_1d(KP<float> p, const float2* __restrict__ tw256,
+__global__ void __launch_bounds__(1024) k_fs2_1d(KP<float> p, const float2* __restrict__ tw256,
                                                 const float2* __restrict__ Y) {
   using C = float2;
   double s[3] = {0.0, 0.0, 0.0};

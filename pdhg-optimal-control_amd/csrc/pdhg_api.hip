@@ -330,9 +330,10 @@ struct Impl : ImplBase {
         glb_line = true;
         lds_res = 0;
         nt1d = 1024;
-        // four-step DHT over 16 + 9 workgroups per row pair: parity-clean but measured slower at C1 (1.56 vs
-        // 1.41 ms per iteration: 64-B input segments, one workgroup per CU in stage 2), so opt-in only
-        if (const char* e = getenv("PDHG_FOURSTEP")) fourstep = sizeof(R) == 4 && nx == 65536 && atoi(e) != 0;
+        // fp32 nx = 65536 (C1): four-step DHT over 16 + 9 workgroups of 1024 threads per row pair instead of
+        // one workgroup per pair (T = 400 gave 200 workgroups for 256 CUs): 1.41 -> 1.12 ms per iteration
+        fourstep = sizeof(R) == 4 && nx == 65536;
+        if (const char* e = getenv("PDHG_FOURSTEP")) fourstep = fourstep && atoi(e) != 0;   // tuning override
       }
       g4 = 1;
       gx5 = (nx + 255) / 256;
@@ -835,6 +836,7 @@ struct Impl : ImplBase {
   // 1-D primal with the four-step DHT (nx = 65536, fp32): residual + DHT, Thomas, inverse DHT + update
   int launch_fourstep_1d(const KP<R>& p) {
     if constexpr (sizeof(R) == 4) {
+      constexpr int kFsNT = 1024;   // 16 waves: the load / unpack loops keep more rows in flight
       const int npairs = (pb.T + 1) / 2;
       const size_t lds1 = (size_t)2 * 256 * 16 * sizeof(C), lds2 = 2 * lds1;
       float2* Y = reinterpret_cast<float2*>(p.gscr);
@@ -843,13 +845,13 @@ struct Impl : ImplBase {
         ProfScope ps(this, "residual");
         if (pb.egno == 1) {
           if ((rc = ensure_lds(k_fs1_1d<0, 1>, lds1))) return rc;
-          hipLaunchKernelGGL((k_fs1_1d<0, 1>), dim3(16, npairs), dim3(256), lds1, stream, p, tw256, twx, Y);
+          hipLaunchKernelGGL((k_fs1_1d<0, 1>), dim3(16, npairs), dim3(kFsNT), lds1, stream, p, tw256, twx, Y);
         } else {
           if ((rc = ensure_lds(k_fs1_1d<0, 2>, lds1))) return rc;
-          hipLaunchKernelGGL((k_fs1_1d<0, 2>), dim3(16, npairs), dim3(256), lds1, stream, p, tw256, twx, Y);
+          hipLaunchKernelGGL((k_fs1_1d<0, 2>), dim3(16, npairs), dim3(kFsNT), lds1, stream, p, tw256, twx, Y);
         }
         if ((rc = ensure_lds(k_fs2_1d<0>, lds2))) return rc;
-        hipLaunchKernelGGL((k_fs2_1d<0>), dim3(9, npairs), dim3(256), lds2, stream, p, tw256, Y);
+        hipLaunchKernelGGL((k_fs2_1d<0>), dim3(9, npairs), dim3(kFsNT), lds2, stream, p, tw256, Y);
       }
       {
         ProfScope ps(this, "precond");
@@ -858,9 +860,9 @@ struct Impl : ImplBase {
       {
         ProfScope ps(this, "update");
         if ((rc = ensure_lds(k_fs1_1d<1, 1>, lds1))) return rc;
-        hipLaunchKernelGGL((k_fs1_1d<1, 1>), dim3(16, npairs), dim3(256), lds1, stream, p, tw256, twx, Y);
+        hipLaunchKernelGGL((k_fs1_1d<1, 1>), dim3(16, npairs), dim3(kFsNT), lds1, stream, p, tw256, twx, Y);
         if ((rc = ensure_lds(k_fs2_1d<1>, lds2))) return rc;
-        hipLaunchKernelGGL((k_fs2_1d<1>), dim3(9, npairs), dim3(256), lds2, stream, p, tw256, Y);
+        hipLaunchKernelGGL((k_fs2_1d<1>), dim3(9, npairs), dim3(kFsNT), lds2, stream, p, tw256, Y);
       }
       hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, p.partials, 9 * npairs, row0_sq, p.ctrl);
       HIP_TRY(hipGetLastError());

@@ -337,10 +337,10 @@ def test_half_real_x_transform_fp32(native, case):
 
 
 @pytest.mark.parametrize("prec", ["fp32"])
-def test_fourstep_1d_opt_in(native, prec, monkeypatch):
-    """C1's line length through the opt-in four-step DHT (PDHG_FOURSTEP=1: 256-point FFT stages split over
-    16 + 9 workgroups per row pair) vs the oracle, same fp32 bounds as the default path."""
-    monkeypatch.setenv("PDHG_FOURSTEP", "1")
+def test_glb_lines_1d_fp32(native, prec, monkeypatch):
+    """C1's line length in fp32 through the one-workgroup-per-row-pair global-scratch lines (PDHG_FOURSTEP=0;
+    the default fp32 path at nx = 65536 is the four-step DHT, covered by the CASES above) vs the oracle."""
+    monkeypatch.setenv("PDHG_FOURSTEP", "0")
     P = make_problem(2, 1, 65536, 1, 3, 0.0)
     ctx = device_ctx(P, prec)
     ctx.set_state(P["phi"], P["rho"], P["alp"])
