@@ -204,8 +204,12 @@ __global__ void __launch_bounds__(256) k_thomas_1d(KP<R> p) {
   const R em = exp(-th);
   R E = expm1((R)-2 * th);
   R bp = (R)0;
+  // each row's load is issued one step ahead (the rows are independent addresses; without the explicit
+  // prefetch the store to row k keeps the load of row k+1 behind it)
+  R hn = w[0];
   for (int k = 0; k < T; ++k) {
-    const R h = w[(size_t)k * nx];
+    const R h = hn;
+    if (k + 1 < T) hn = w[(size_t)(k + 1) * nx];
     if (k < T - 1) {
       const R E2 = expm1((R)-2 * th * (R)(k + 2));
       const R g = (th > (R)0) ? em * E / E2 : (R)(k + 1) / (R)(k + 2);
@@ -225,10 +229,13 @@ __global__ void __launch_bounds__(256) k_thomas_1d(KP<R> p) {
     }
   }
   E = expm1((R)-2 * th * (R)T);
+  R wn = (T >= 2) ? w[(size_t)(T - 2) * nx] : (R)0;
   for (int k = T - 2; k >= 0; --k) {
+    const R wk = wn;
+    if (k > 0) wn = w[(size_t)(k - 1) * nx];
     const R E1 = expm1((R)-2 * th * (R)(k + 1));
     const R g = (th > (R)0) ? em * E1 / E : (R)(k + 1) / (R)(k + 2);
-    bp = w[(size_t)k * nx] + g * bp;
+    bp = wk + g * bp;
     E = E1;
     w[(size_t)k * nx] = bp;
   }
