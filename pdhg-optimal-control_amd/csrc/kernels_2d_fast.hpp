@@ -689,6 +689,66 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
   }
 }
 
+// ---- x-transform for a one-row window (T = 1, the reference's marching default; fp32, nx = N) ----
+// With T = 1 the t-solve is one division per mode (the Neumann row: u = ae (dd + 1), utils_precond.py:164-169),
+// so no carries are kept: forward DHT_x of the block's NL packed lines in LDS, scale every item, write it
+// back as the packed lines, inverse DHT_x (same transform), store.  LDS = the padded lines + twiddle seeds
+// (41 KiB at N = 4096), two workgroups per CU.
+template <int N, int NL, int NT>
+__global__ void __launch_bounds__(NT, 2) k_precond_x_t1_2d(KP<float> p, const float2* __restrict__ twx) {
+  using C = float2;
+  constexpr int IT = N * NL / NT;
+  constexpr int B = 2 * NL;
+  constexpr int LINE = Pad<N>::LINE;
+  constexpr int lnl = (NL == 1) ? 0 : (NL == 2) ? 1 : (NL == 4) ? 2 : 3;
+  if (p.ctrl->done) return;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  C* A = reinterpret_cast<C*>(smem_raw);
+  C* twl = A + NL * LINE;
+  fill_twlds<C, N>(twl, twx);
+  const int tid = threadIdx.x;
+  const int b = blockIdx.x + p.b0;
+  constexpr int M = N * B;
+  C* wb = reinterpret_cast<C*>(p.work + (size_t)b * M);
+  C v[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) v[i] = wb[tid + i * NT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int item = tid + i * NT;
+    A[(item & (NL - 1)) * LINE + pix(item >> lnl)] = v[i];
+  }
+  lds_sync();
+  lds_fft_inplace_tl<C, N, NL, NT>(A, twl);
+  const float inv_ae = 1.f / p.ae;
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int item = tid + i * NT;
+    const int kx = item >> lnl, l = item & (NL - 1);
+    float ha, hb;
+    hartley_padded<C, float>(A + l * LINE, N, kx, ha, hb);
+    const float lx = p.lamx[kx];
+    const float dd0 = (p.C - lx - p.lamy[b * B + 2 * l]) * inv_ae, dd1 = (p.C - lx - p.lamy[b * B + 2 * l + 1]) * inv_ae;
+    v[i] = make_float2(ha * inv_ae / (dd0 + 1.f), hb * inv_ae / (dd1 + 1.f));
+  }
+  lds_sync();   // every item has read its Hartley pair
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int item = tid + i * NT;
+    A[(item & (NL - 1)) * LINE + pix(item >> lnl)] = v[i];
+  }
+  lds_sync();
+  lds_fft_inplace_tl<C, N, NL, NT>(A, twl);
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int item = tid + i * NT;
+    const int kx = item >> lnl, l = item & (NL - 1);
+    float ha, hb;
+    hartley_padded<C, float>(A + l * LINE, N, kx, ha, hb);
+    wb[item] = make_float2(ha, hb);
+  }
+}
+
 // ---- x-transform + Thomas, warp-specialised (fp32, nx = N a power of two, N*NL = 4096) ----
 // Waves 0-3 (the FFT group, 256 threads) run the three Stockham passes on buffer X while waves 4-7
 // (the Thomas group, 256 threads x 16 items) unpack buffer Y -- the previous t-row's transform --,

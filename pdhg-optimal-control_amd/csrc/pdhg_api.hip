@@ -116,6 +116,7 @@ struct Impl : ImplBase {
   bool fast_rows = false;
   bool glb_line = false;          // 1-D line FFTs over global scratch (nx beyond LDS)
   bool fourstep = false;          // fp32 1-D nx = 65536: four-step DHT over 16 + 9 workgroups per row pair
+  bool t1_xt = true;              // T = 1 windows: carry-free x transform (k_precond_x_t1_2d; env PDHG_T1_XT=0 off)
   C* tw256 = nullptr;             // W_256 table of the four-step stages
   bool half_real = false;         // 2-D nx = 8192: one real column per x-transform block
   int nt1d = 256;                 // 1-D residual / update block size (1024 on the global-scratch path)
@@ -246,6 +247,7 @@ struct Impl : ImplBase {
       gx5 = (ny + 255) / 256;
       g5 = std::max(1, std::min(T * nx, 8192 / std::max(1, gx5)));
       if (const char* e = getenv("PDHG_DBG")) p.dbg = atoi(e);   // timing experiments only
+      if (const char* e = getenv("PDHG_T1_XT")) t1_xt = atoi(e) != 0;   // tuning override
       // short windows (the reference's T = 1 marching default): few time rows per workgroup leave little to
       // pipeline over t, so occupancy decides.  Measured on C3's grid (bench --config c3w1/c3w4/c3w8): the
       // single-role x-transform kernel beats the warp-specialised one up to T = 8 at least (T = 1: 0.18 vs
@@ -690,6 +692,29 @@ struct Impl : ImplBase {
   int launch_precond(const KP<R>& p, int nblk = -1) {   // nblk: blocks [p.b0, p.b0 + nblk) (default: all)
     int rc = PDHG_OK;
     if (nblk < 0) nblk = p.nb - p.b0;
+    if constexpr (sizeof(R) == 4) {
+      // one-row window: no t carries (k_precond_x_t1_2d), two workgroups per CU
+      if (fast_xt && !half_real && p.T == 1 && !p.slab && p.xt_phase == 0 && t1_xt) {
+        ProfScope ps(this, "precond");
+        const size_t lds = (size_t)((p.B / 2) * (p.nx + p.nx / 16) + twlds_size(p.nx)) * sizeof(C);
+        auto go = [&](auto kern) -> int {
+          int r2;
+          if ((r2 = ensure_lds(kern, lds))) return r2;
+          hipLaunchKernelGGL(kern, dim3(nblk), dim3(512), lds, stream, p, twx);
+          return (int)PDHG_OK;
+        };
+        switch (p.nx) {
+          case 4096: rc = go(k_precond_x_t1_2d<4096, 1, 512>); break;
+          case 2048: rc = go(k_precond_x_t1_2d<2048, 2, 512>); break;
+          case 1024: rc = go(k_precond_x_t1_2d<1024, 4, 512>); break;
+          case 512: rc = go(k_precond_x_t1_2d<512, 8, 512>); break;
+          default: rc = fail(PDHG_ERR_UNSUPPORTED, "no one-row x kernel for nx=%d", p.nx);
+        }
+        if (rc) return rc;
+        HIP_TRY(hipGetLastError());
+        return PDHG_OK;
+      }
+    }
     if (fast_xt) {
       ProfScope ps(this, "precond");
       rc = PDHG_OK;

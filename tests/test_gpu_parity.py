@@ -354,3 +354,26 @@ def test_glb_lines_1d_fp32(native, prec, monkeypatch):
     assert rel(phi_d, phi_o) < 1e-5 and rel(rho_d, rho_o) < 2e-4
     assert abs(st["err1"] - e1_o) <= 1e-2 * e1_o
     ctx.close()
+
+
+T1_FAST = [(1, 2, 4096, 256, 1, 0.0), (2, 2, 1024, 512, 1, 0.0), (1, 2, 512, 256, 1, 0.0)]
+
+
+@pytest.mark.parametrize("case", T1_FAST, ids=["e{}d{}_{}x{}_T{}_eps{}".format(*c) for c in T1_FAST])
+def test_t1_x_transform_fp32(native, case):
+    """One-row windows (the marching default) through the carry-free x transform k_precond_x_t1_2d vs the
+    oracle: primal U and 10 iterations, fp32 bounds of test_fp32_from_reference_init."""
+    P = make_problem(*case, seeded=False)
+    phi_o = _oracle_primal(P, P["phi"], P["rho"], P["alp"])
+    ctx = device_ctx(P, "fp32")
+    assert ctx.path_info("fast_xt") == 1
+    ctx.set_state(P["phi"], P["rho"], P["alp"])
+    ctx.update_primal(TAU)
+    assert rel(ctx.get_state()[0], phi_o) < 1e-6
+    phi_o, rho_o, _, e1_o, _ = _oracle_iterate(P, 10)
+    ctx.set_state(P["phi"], P["rho"], P["alp"])
+    st = ctx.iterate(10, TAU, SIGMA, -1.0, 1)
+    phi_d, rho_d, _ = ctx.get_state()
+    assert rel(phi_d, phi_o) < 1e-5 and rel(rho_d, rho_o) < 1e-5
+    assert abs(st["err1"] - e1_o) <= 1e-3 * e1_o
+    ctx.close()
