@@ -52,9 +52,10 @@ def grid(ndim, nx, ny):
     return x1, np.linspace(0.0, 2.0, num=ny, endpoint=False)
 
 
-def cpu_baseline(cfg, T_sample, threads):
+def cpu_baseline(cfg, T_sample, threads, reps_min=3):
     """The float64 oracle (restatement of the reference, labelled 'port') on a bounded sample:
-    the full nx x ny plane with T_sample unknown rows; extrapolated linearly to the full T."""
+    the full nx x ny plane with T_sample unknown rows, one warm-up iteration then reps_min timed
+    iterations (median); extrapolated linearly in T to the full window."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     os.environ["ORACLE_FFT_WORKERS"] = str(threads)
     import pdhg_oracle as O
@@ -82,21 +83,22 @@ def cpu_baseline(cfg, T_sample, threads):
         phi, rho, alp = phi_n, rho_n, alp_n
 
     one()                      # warm-up
-    reps, t0 = 0, time.perf_counter()
-    while True:
+    times = []
+    t_all = time.perf_counter()
+    while len(times) < reps_min or (time.perf_counter() - t_all < 8.0 and len(times) < 50):
+        t0 = time.perf_counter()
         one()
-        reps += 1
-        el = time.perf_counter() - t0
-        if el > 8.0 or reps >= 5:
-            break
-    per_it = el / reps
+        times.append(time.perf_counter() - t0)
+    per_it = float(np.median(times))
     pts_per_s = T_sample * np.prod(nsp) / per_it
     full_pts = T * np.prod(nsp)
     return {"value": float(pts_per_s / full_pts), "unit": "it/s", "cores": threads, "kind": "port",
             "sample": "float64 NumPy/SciPy oracle (restatement of the JAX reference, which cannot run here), "
-                      "{} x {} plane with T'={} of T={} rows, {} iterations in {:.1f}s, it/s extrapolated "
-                      "linearly in T; scipy.fft workers={}, NumPy elementwise single-threaded".format(
-                          nx, ny, T_sample, T, reps, el, threads)}
+                      "{} x {} plane with T'={} of T={} rows: {} timed iterations after 1 warm-up, median "
+                      "{:.2f} s (min {:.2f}, max {:.2f}), it/s extrapolated linearly in T; scipy.fft workers={}, "
+                      "NumPy elementwise single-threaded".format(nx, ny, T_sample, T, len(times), per_it,
+                                                                min(times), max(times), threads),
+            "reps": len(times)}
 
 
 def pmc_traffic(args):
@@ -118,7 +120,7 @@ def pmc_traffic(args):
         d = tempfile.mkdtemp(prefix="pdhg_pmc_", dir="/tmp")
         cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "run", "--",
                sys.executable, os.path.abspath(__file__), "--config", args.config, "--steps", "2", "--warmup", "1",
-               "--rho-alp-iters", str(args.rho_alp_iters), "--no-cpu-baseline", "--no-pmc"]
+               "--rho-alp-iters", str(args.rho_alp_iters), "--no-cpu-baseline", "--no-pmc", "--no-probe"]
         try:
             subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=600,
                            env=dict(os.environ, TMPDIR="/tmp"))
@@ -131,8 +133,8 @@ def pmc_traffic(args):
                         for r in csv.DictReader(fh):
                             if r["Counter_Name"] != ctr:
                                 continue
-                            for cls, sym in KERNEL_SYMBOL.items():
-                                if sym in r["Kernel_Name"]:
+                            for cls, syms in KERNEL_SYMBOL.items():
+                                if any(sym in r["Kernel_Name"] for sym in syms):
                                     vals.setdefault((cls, ctr), {}).setdefault(r["Kernel_Name"], []).append(
                                         float(r["Counter_Value"]) * 1024.0)
         shutil.rmtree(d, ignore_errors=True)
@@ -148,36 +150,89 @@ def pmc_traffic(args):
     return (out, None) if out else (None, "no PMC rows matched")
 
 
-KERNEL_SYMBOL = {"dual": "k_dual_", "residual": "k_res_fwd", "precond": "k_precond_xt", "update": "k_inv"}
+# kernel-name substrings of the four classes (precond: k_precond_xt_* and the one-row k_precond_x_t1_2d,
+# 1-D k_thomas_1d; the 1-D four-step kernels k_fs1/k_fs2 serve both residual and update and are not attributed)
+KERNEL_SYMBOL = {"dual": ("k_dual_",), "residual": ("k_res_fwd",), "precond": ("k_precond_x", "k_thomas_1d"),
+                 "update": ("k_inv",)}
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """--gpus N > 1 without a launcher: start N rank processes (torch.distributed.run, one per GPU) as a
+    child process group before this process touches the GPU, and return their exit code."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node={}".format(n),
+           "--master-addr", "127.0.0.1", "--master-port={}".format(_free_port()), os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC (RCCL on this host)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    proc = subprocess.Popen(cmd, env=env, start_new_session=True)
+    try:
+        return proc.wait()
+    except KeyboardInterrupt:
+        os.killpg(proc.pid, 15)
+        return proc.wait()
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks); > 1 without WORLD_SIZE in the environment launches the ranks itself")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--rho-alp-iters", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-T", type=int, default=2)
+    ap.add_argument("--cpu-sample-T", type=int, default=1)
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
+    ap.add_argument("--no-probe", action="store_true", help="skip the non-finite probe and the finite segment")
     ap.add_argument("--decomp", default="tslab", choices=["tslab", "xslab"],
                     help="multi-GPU decomposition of the window (xslab also at N = 1: one slab through its phases)")
+    ap.add_argument("--selftest", action="store_true",
+                    help="launcher / process-group check only: no GPU work, prints the world size")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit("bench: --gpus {} but WORLD_SIZE={}".format(args.gpus, world))
     dist = None
+    backend = os.environ.get("PDHG_DIST_BACKEND", "gloo" if args.selftest else "nccl")
     if world > 1:
         import torch
         import torch.distributed as tdist
-        # device = local rank (modulo the visible GPUs: PDHG_DIST_BACKEND=gloo rehearses the multi-rank
-        # path with several ranks on one GPU; the driver's runs use one GPU per rank over RCCL)
-        dev = local_rank % max(1, torch.cuda.device_count())
-        torch.cuda.set_device(dev)
-        tdist.init_process_group(os.environ.get("PDHG_DIST_BACKEND", "nccl"))
+        if not args.selftest:
+            # device = local rank (modulo the visible GPUs: PDHG_DIST_BACKEND=gloo rehearses the multi-rank
+            # path with several ranks on one GPU; the driver's runs use one GPU per rank over RCCL)
+            dev = local_rank % max(1, torch.cuda.device_count())
+            torch.cuda.set_device(dev)
+        tdist.init_process_group(backend)
         dist = tdist
+        if tdist.get_world_size() != world:
+            raise SystemExit("bench: process group has {} ranks, WORLD_SIZE={}".format(tdist.get_world_size(), world))
+    if args.selftest:
+        if dist is not None:
+            import torch
+            t = torch.ones(1)
+            dist.all_reduce(t)
+            ranks_seen = int(t.item())
+            dist.destroy_process_group()
+        else:
+            ranks_seen = 1
+        if rank == 0:
+            print(json.dumps({"selftest": True, "n_gpus": world, "ranks_seen": ranks_seen, "backend": backend}),
+                  flush=True)
+        return
 
     pmc, pmc_err = None, "disabled"
     if world == 1 and not args.no_pmc and args.decomp == "tslab":
@@ -208,14 +263,14 @@ def main():
         g = np.sin(np.pi * xs)
     else:
         g = np.sin(np.pi * xs)[:, None] + np.sin(np.pi * ys)[None, :]
-    if xslab:
-        ctx.init_global_state(g)
-    else:
-        ctx.init_state(g)
-    # epsl = 0.1 on a 4096^2 grid is outside the reference algorithm's stability range (explicit
-    # sigma*epsl*Lap in the dual; its fp64 restatement diverges already at 256^2): keep executing
-    # exactly the requested iterations after the state goes non-finite, and report it.
-    ctx.set_stop_rules(converge=True, nan=False)
+
+    def init():
+        """The reference initial state (phi = g, rho = 70, alp = 0; utils_pdhg_solver.py:123-137)."""
+        if xslab:
+            ctx.init_global_state(g)
+        else:
+            ctx.init_state(g)
+
     tau, sigma = 0.1 / 1.5, 0.1 * 1.5
     eps = 1e-6
 
@@ -225,7 +280,8 @@ def main():
 
         def run(n):
             s = xrunner.iterate(n, tau, sigma, eps, k)
-            return {"iters_run": s["iters"], "status": s["status"], "nan_seen": s["nan_seen"]}
+            return {"iters_run": s["iters"], "status": s["status"], "nan_seen": s["nan_seen"],
+                    "first_nan_iter": s.get("first_nan_iter", 0)}
 
         def sync():
             torch.cuda.synchronize()
@@ -235,7 +291,8 @@ def main():
 
         def run(n):
             s = runner.iterate(n, tau, sigma, eps, k)
-            return {"iters_run": s["iters"], "status": s["status"], "nan_seen": s["nan_seen"]}
+            return {"iters_run": s["iters"], "status": s["status"], "nan_seen": s["nan_seen"],
+                    "first_nan_iter": s.get("first_nan_iter", 0)}
 
         def sync():
             torch.cuda.synchronize()
@@ -246,49 +303,91 @@ def main():
         def sync():
             ctx.synchronize()
 
-    if args.warmup > 0:
-        run(args.warmup)
-    sync()
-
     def barrier():
         if dist is not None:
             dist.barrier()
 
-    ctx.profile_enable(True)
-    barrier()
-    sync()
-    t0 = time.perf_counter()
-    st = run(args.steps)
-    sync()
-    barrier()
-    el = time.perf_counter() - t0
-    iters = st["iters_run"]
-    if dist is not None:
+    def max_over_ranks(x):
+        if dist is None:
+            return x
         import torch
-        t = torch.tensor([el, float(iters)], dtype=torch.float64, device="cuda")
-        tmax = t.clone()
-        dist.all_reduce(tmax[0:1], op=dist.ReduceOp.MAX)
-        el_max, iters_total = float(tmax[0]), iters          # one window: every rank ran the same iterations
-    else:
-        el_max, iters_total = el, iters
+        t = torch.tensor([x], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t[0])
 
-    # per-kernel live timing (HIP events on the context's stream)
-    kern = {}
-    for cls in ("residual", "precond", "update", "dual"):
-        ms, n = ctx.profile_query(cls)
-        if n:
-            kern[cls] = {"avg_ms": ms / n, "launches": n, "bytes_per_launch": ctx.algorithmic_bytes(k, cls)}
+    # epsl = 0.1 on a 4096^2 grid is outside the reference algorithm's stability range (explicit
+    # sigma*epsl*Lap in the dual; its fp64 restatement diverges already at 256^2).  Probe: from the
+    # reference initial state, the first iteration whose phi' or rho' holds a NaN (NaN stop on).
+    first_nonfinite = None
+    probe_n = 0
+    if not args.no_probe:
+        init()
+        ctx.set_stop_rules(converge=True, nan=True)
+        probe_n = max(args.warmup + args.steps, 20)
+        st = run(probe_n)
+        sync()
+        if st["status"] == 2 or st["nan_seen"]:
+            first_nonfinite = int(st.get("first_nan_iter") or st["iters_run"])
+    # the timed runs execute exactly the requested iterations (NaN stop off), each from the reference state
+    ctx.set_stop_rules(converge=True, nan=False)
+
+    def timed(n):
+        init()
+        sync()
+        ctx.profile_enable(True)
+        barrier()
+        sync()
+        t0 = time.perf_counter()
+        st = run(n)
+        sync()
+        barrier()
+        el = time.perf_counter() - t0
+        kern = {}
+        for cls in ("residual", "precond", "update", "dual"):
+            ms, nl = ctx.profile_query(cls)
+            if nl:
+                kern[cls] = {"avg_ms": ms / nl, "launches": nl, "bytes_per_launch": ctx.algorithmic_bytes(k, cls)}
+        ctx.profile_enable(False)
+        return st, el, kern
+
+    # finite segment: iterations 1..F from the reference state, all before the first non-finite one
+    finite = None
+    if not args.no_probe:
+        F = 10 if first_nonfinite is None else min(10, first_nonfinite - 1)
+        if F >= 1:
+            st_f, el_f, kern_f = timed(F)
+            el_f = max_over_ranks(el_f)
+            finite = {"iters": F, "ms_per_step": el_f / F * 1e3, "value": F / el_f, "nonfinite": bool(st_f["nan_seen"]),
+                      "kernels_avg_ms": {c: d["avg_ms"] for c, d in kern_f.items()}}
+
+    if args.warmup > 0:
+        init()
+        run(args.warmup)
+    sync()
+    if runner is not None:
+        runner.timing = True
+    st, el, kern = timed(args.steps)
+    exch = runner.exchange_times() if runner is not None else None
+    if runner is not None:
+        runner.timing = False
+    el_max = max_over_ranks(el)
+    iters = st["iters_run"]
+    iters_total = iters          # one window: every rank ran the same iterations
+
     if world > 1 or xslab:   # slabs: sweeps and halo/interior row parts are separate launches -> per iteration
         for cls, d in kern.items():
             per = max(iters, 1) * (k if cls == "dual" else 1)
             d["avg_ms"] = d["avg_ms"] * d["launches"] / per
             d["launches"] = per
-    ctx.profile_enable(False)
     dom = max(kern, key=lambda c: kern[c]["avg_ms"] * kern[c]["launches"])
     d = kern[dom]
     achieved = d["bytes_per_launch"] / (d["avg_ms"] * 1e-3) / 1e9
+    # per-rank dominant-kernel time (slabs differ by one row at most): the slowest rank bounds the step
+    dom_ms_max = max_over_ranks(d["avg_ms"])
     it_bytes = ctx.algorithmic_bytes(k, "iteration") * world   # whole window (slabs are equal-ish)
     ms_per_step = el_max / max(iters, 1) * 1e3
+    if exch is not None:
+        exch = {c: max_over_ranks(v) / max(iters, 1) for c, v in sorted(exch.items())}
 
     if rank != 0:
         if dist is not None:
@@ -306,22 +405,33 @@ def main():
         "scaling": "strong" if world > 1 else "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (reference initial state phi=g, rho=70, alp=0)",
+        "data": "synthetic (reference initial state phi=g, rho=70, alp=0; every timed run starts from it)",
         "config": {"workload": "egno{} ndim{} epsl{} nx={} ny={} nt={}: one PDHG window of T={} rows, "
                                "rho_alp_iters={}".format(egno, ndim, epsl, nx, ny, nt, T, k),
                    "parallelism": ("x-slab x{} (halo-row allgathers, two all-to-all spectrum transposes per "
                                    "iteration)".format(world) if xslab else
                                    "t-slab x{} (RCCL point-to-point halos and carries, overlapped)".format(world))
                    if (world > 1 or xslab) else "single GPU",
-                   "iters_executed": iters, "stop_status": st["status"], "state_nonfinite": bool(st["nan_seen"])},
-        **({"slab_exchange": {"carries": runner.exchange, "long_range_modes": runner.n_long,
-                              "halo_overlap": runner.side is not None}} if runner is not None else {}),
+                   "iters_executed": iters, "stop_status": st["status"], "state_nonfinite": bool(st["nan_seen"]),
+                   "first_nonfinite_iter": first_nonfinite,
+                   "nonfinite_probe_iters": probe_n},
         "hbm_gbps_iteration": it_bytes / (ms_per_step * 1e-3) / 1e9,
         "iteration_bytes": it_bytes,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": None},
         "kernels": kern,
     }
+    if finite is not None:
+        out["finite_segment"] = finite
+    if world > 1:
+        out["world"] = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
+                        "dominant_kernel_ms_max_over_ranks": dom_ms_max}
+    if runner is not None:
+        from pdhg_amd.slab import slab_bounds
+        out["slab"] = {"rows_per_slab": [j1 - j0 for j0, j1 in slab_bounds(T, world)],
+                       "carries": runner.exchange, "carry_parts": runner.parts, "long_range_modes": runner.n_long,
+                       "halo_overlap": runner.side is not None,
+                       "exchange_ms_per_iter_max_over_ranks": exch}
     if pmc and dom in pmc:
         out["roofline"]["traffic"] = pmc[dom]["bytes"]
         out["roofline"]["traffic_detail"] = pmc[dom]

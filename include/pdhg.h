@@ -74,7 +74,7 @@ typedef struct pdhg_stats {
   double err_inner;  /* last dual sub-iteration error (update_fns_in_pdhg.py:162-164)        */
   double rho_min, rho_max; /* not computed (NaN) unless requested; reserved                 */
   int nan_seen;      /* a NaN appeared in phi' or rho' during this call                        */
-  int reserved1;
+  int first_nan_iter; /* iteration of this call (1-based) whose phi' or rho' first held a NaN; 0: none */
 } pdhg_stats;
 
 typedef struct pdhg_ctx pdhg_ctx;

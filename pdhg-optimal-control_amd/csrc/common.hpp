@@ -37,6 +37,7 @@ struct Ctrl {
   int cur;           // which rho/alp buffer set holds the state (0/1)
   int primal_valid;  // primal sums of the current outer iteration are valid
   int nan_seen;      // a NaN appeared in phi' or rho' (recorded even when the NaN stop is off)
+  int first_nan;     // iteration (1-based, since the last reset) at which nan_seen was first set; 0: none
   double err1, err2, err_inner;
   double s_dphi, s_phi_old, s_phi_new;   // finalized primal sums
   double dual_sums[kNumSums];            // finalized sums of the last dual sub-iteration

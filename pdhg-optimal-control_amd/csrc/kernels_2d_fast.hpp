@@ -693,9 +693,10 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
 // With T = 1 the t-solve is one division per mode (the Neumann row: u = ae (dd + 1), utils_precond.py:164-169),
 // so no carries are kept: forward DHT_x of the block's NL packed lines in LDS, scale every item, write it
 // back as the packed lines, inverse DHT_x (same transform), store.  LDS = the padded lines + twiddle seeds
-// (41 KiB at N = 4096), two workgroups per CU.
+// (41 KiB at N = 4096), two workgroups per CU: HIP's second __launch_bounds__ argument is the minimum waves
+// per SIMD, and a 512-thread workgroup puts 2 waves on each SIMD, so 4 guarantees two workgroups (<= 128 VGPRs).
 template <int N, int NL, int NT>
-__global__ void __launch_bounds__(NT, 2) k_precond_x_t1_2d(KP<float> p, const float2* __restrict__ twx) {
+__global__ void __launch_bounds__(NT, 4) k_precond_x_t1_2d(KP<float> p, const float2* __restrict__ twx) {
   using C = float2;
   constexpr int IT = N * NL / NT;
   constexpr int B = 2 * NL;

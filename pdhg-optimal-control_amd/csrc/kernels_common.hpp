@@ -134,6 +134,7 @@ __global__ void __launch_bounds__(1024) k_finalize_outer(const double* partials,
       if (stop_conv) ctrl->done = 1;
     } else if (ctrl->s_phi_new != ctrl->s_phi_new || rho_new_sq != rho_new_sq) {
       if (stop_nan) ctrl->done = 2;
+      if (!ctrl->nan_seen) ctrl->first_nan = ctrl->iters;
       ctrl->nan_seen = 1;
     }
     if (flip) ctrl->cur = 1 - ctrl->cur;

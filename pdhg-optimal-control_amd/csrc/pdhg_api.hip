@@ -1030,6 +1030,7 @@ struct Impl : ImplBase {
       st->rho_min = NAN;
       st->rho_max = NAN;
       st->nan_seen = h.nan_seen;
+      st->first_nan_iter = h.first_nan;
     }
     primal_done = false;
     return PDHG_OK;
@@ -1328,6 +1329,7 @@ struct Impl : ImplBase {
     st->rho_min = NAN;
     st->rho_max = NAN;
     st->nan_seen = h.nan_seen;
+    st->first_nan_iter = h.first_nan;
     return PDHG_OK;
   }
 
@@ -1704,6 +1706,15 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
     else if (k == "fast_rows") *value = im.fast_rows ? 1 : 0;
     else if (k == "fast_dual") *value = im.fast_dual ? im.dual_rx : -1;
     else if (k == "fast_xt") *value = im.fast_xt ? (im.ws_xt ? 2 : 1) : 0;
+    else if (k == "half_real") *value = im.half_real ? 1 : 0;
+    else if (k == "fourstep") *value = im.fourstep ? 1 : 0;
+    else if (k == "glb_line") *value = im.glb_line ? 1 : 0;
+    else if (k == "rows_rw") *value = im.fast_rows ? im.RWf : 0;   // rows per fast row-kernel workgroup
+    // threads of the fast row kernels as launched (ny = 4096: 512 instead of 1024 per half_nt)
+    else if (k == "res_threads") *value = im.fast_rows ? ((im.NTf == 1024 && im.RWf == 8 && (im.half_nt & 1) &&
+                                                           im.fuse_res) ? 512 : im.NTf) : 0;
+    else if (k == "upd_threads") *value = im.fast_rows ? ((im.NTf == 1024 && im.RWf == 8 && (im.half_nt & 2))
+                                                              ? 512 : im.NTf) : 0;
     else return fail(PDHG_ERR_ARG, "unknown path key %s", key);
     return (int)PDHG_OK;
   });

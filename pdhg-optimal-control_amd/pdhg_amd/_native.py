@@ -64,7 +64,7 @@ class pdhg_stats(ctypes.Structure):
         ("iters_run", ctypes.c_int), ("status", ctypes.c_int), ("inner_last", ctypes.c_int),
         ("inner_total", ctypes.c_int), ("err1", ctypes.c_double), ("err2", ctypes.c_double),
         ("err_inner", ctypes.c_double), ("rho_min", ctypes.c_double), ("rho_max", ctypes.c_double),
-        ("nan_seen", ctypes.c_int), ("reserved1", ctypes.c_int),
+        ("nan_seen", ctypes.c_int), ("first_nan_iter", ctypes.c_int),
     ]
 
 

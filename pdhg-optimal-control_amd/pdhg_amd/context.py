@@ -118,7 +118,7 @@ class PDHGContext:
                                        int(rho_alp_iters), ctypes.byref(st)))
         return {"iters_run": st.iters_run, "status": st.status, "inner_last": st.inner_last,
                 "inner_total": st.inner_total, "err1": st.err1, "err2": st.err2, "err_inner": st.err_inner,
-                "nan_seen": st.nan_seen}
+                "nan_seen": st.nan_seen, "first_nan_iter": st.first_nan_iter}
 
     def set_stop_rules(self, converge=True, nan=True):
         N.check(self._lib.pdhg_set_stop_rules(self._h, 1 if converge else 0, 1 if nan else 0))

@@ -77,7 +77,8 @@ class PhaseOps:
         st = N.pdhg_stats()
         N.check(self._lib.pdhg_slab_status(self._h, ctypes.byref(st)))
         return {"iters": st.iters_run, "status": st.status, "err1": st.err1, "err2": st.err2,
-                "inner_last": st.inner_last, "inner_total": st.inner_total, "nan_seen": st.nan_seen}
+                "inner_last": st.inner_last, "inner_total": st.inner_total, "nan_seen": st.nan_seen,
+                "first_nan_iter": st.first_nan_iter}
 
 
 class SlabContext(PhaseOps, PDHGContext):
@@ -303,6 +304,8 @@ class SlabRunner:
         self.torch = torch
         self.slabs, self.comm = list(slabs), comm
         self.exchange = exchange
+        self.timing = False      # record HIP events around every exchange (exchange_times())
+        self._tev = {}
         self.side = torch.cuda.Stream() if overlap else None   # halo stream
         self.parts = int(parts) if (exchange == "neighbour" and overlap) else 1
         dev = torch.device("cuda", torch.cuda.current_device())
@@ -333,16 +336,38 @@ class SlabRunner:
         for s in self.slabs:
             getattr(s, name)(*args)
 
-    def _halo(self, shift, *planes):
+    def _timed(self, cat, fn, stream=None):
+        """fn() bracketed by timing events on `stream` (default: the current stream) when timing is on."""
+        if not self.timing:
+            return fn()
+        torch = self.torch
+        stream = stream or torch.cuda.current_stream()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        r = fn()
+        b.record(stream)
+        self._tev.setdefault(cat, []).append((a, b))
+        return r
+
+    def exchange_times(self, reset=True):
+        """{category: total ms} of the exchanges since timing was switched on (halo_rho, halo_phibar,
+        carry_planes, carry_long, allreduce); side-stream exchanges overlap the kernels of the main stream."""
+        self.torch.cuda.synchronize()
+        out = {c: sum(a.elapsed_time(b) for a, b in evs) for c, evs in self._tev.items()}
+        if reset:
+            self._tev = {}
+        return out
+
+    def _halo(self, shift, *planes, cat="halo"):
         """Run a halo shift on the side stream after everything enqueued so far on the main stream;
         returns at once (join with _join before the halo plane is used)."""
         torch = self.torch
         if self.side is None:
-            shift(*planes)
+            self._timed(cat, lambda: shift(*planes))
             return
         self.side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(self.side):
-            shift(*planes)
+            self._timed(cat, lambda: shift(*planes), self.side)
 
     def _join(self):
         if self.side is not None:
@@ -354,7 +379,7 @@ class SlabRunner:
         # with the residual of the rows that do not read it
         for s, b in zip(S, B):
             s.plane_out(RHO_ROW0, b["rho_send"])
-        self._halo(C.shift_up, [b["rho_send"] for b in B], [b["rho_recv"] for b in B])
+        self._halo(C.shift_up, [b["rho_send"] for b in B], [b["rho_recv"] for b in B], cat="halo_rho")
         for s in S:
             s.residual(INTERIOR)
         self._join()
@@ -375,14 +400,14 @@ class SlabRunner:
             for s, b in zip(S, B):
                 s.plane_out(CARRY_LONG, b["LONG"])
             self._halo(C.shift_both, [b["DS"][:spec] for b in B], [b["Dl"] for b in B],
-                       [b["DS"][spec:] for b in B], [b["S1r"] for b in B])
-            allLong = C.allgather([b["LONG"] for b in B])
+                       [b["DS"][spec:] for b in B], [b["S1r"] for b in B], cat="carry_planes")
+            allLong = self._timed("carry_long", lambda: C.allgather([b["LONG"] for b in B]))
             self._join()
             for i, s in enumerate(S):
                 s.fixup_nb(B[i]["Dl"], B[i]["S1r"], allLong[i], self.allGS[i])
                 s.backward(tau, B[i]["sums"])
         else:
-            allDS = C.allgather([b["DS"] for b in B])
+            allDS = self._timed("carry_planes", lambda: C.allgather([b["DS"] for b in B]))
             for i, s in enumerate(S):
                 s.fixup(allDS[i], self.allGS[i])
                 s.backward(tau, B[i]["sums"])
@@ -401,13 +426,13 @@ class SlabRunner:
                 s.forward_part(tau, q, self.parts)
                 s.carry_out_part(b["DS"], q, self.parts)
             self._halo(C.shift_both, [b["DS"][lo:hi] for b in B], [b["Dl"][lo:hi] for b in B],
-                       [b["DS"][spec + lo:spec + hi] for b in B], [b["S1r"][lo:hi] for b in B])
+                       [b["DS"][spec + lo:spec + hi] for b in B], [b["S1r"][lo:hi] for b in B], cat="carry_planes")
             ev = torch.cuda.Event()
             ev.record(self.side)
             done.append(ev)
         for s, b in zip(S, B):
             s.plane_out(CARRY_LONG, b["LONG"])
-        allLong = C.allgather([b["LONG"] for b in B])
+        allLong = self._timed("carry_long", lambda: C.allgather([b["LONG"] for b in B]))
         for q in range(self.parts):
             torch.cuda.current_stream().wait_event(done[q])
             for i, s in enumerate(S):
@@ -422,8 +447,8 @@ class SlabRunner:
         # primal sums all-reduce and the dual of the rows that do not read it
         for s, b in zip(S, B):
             s.plane_out(PHIBAR_LAST, b["pb_send"])
-        self._halo(C.shift_down, [b["pb_send"] for b in B], [b["pb_recv"] for b in B])
-        C.allreduce([b["sums"] for b in B])
+        self._halo(C.shift_down, [b["pb_send"] for b in B], [b["pb_recv"] for b in B], cat="halo_phibar")
+        self._timed("allreduce", lambda: C.allreduce([b["sums"] for b in B]))
         for s, b in zip(S, B):
             s.primal_finalize(b["sums"])
         # dual sub-iterations (device-side early exit once the global inner error is below eps)
@@ -436,13 +461,13 @@ class SlabRunner:
                     if s.rank > 0:
                         s.plane_in(PHIBAR_ROW0, b["pb_recv"])
                     s.dual(sigma, k, sub, b["sums"], EDGE)
-            C.allreduce([b["sums"] for b in B])
+            self._timed("allreduce", lambda: C.allreduce([b["sums"] for b in B]))
             for s, b in zip(S, B):
                 s.dual_finalize(eps, sub, b["sums"])
         for s, b in zip(S, B):
             s.outer(k, b["sums"])
         if k > 1:
-            C.allreduce([b["sums"] for b in B])
+            self._timed("allreduce", lambda: C.allreduce([b["sums"] for b in B]))
         for s, b in zip(S, B):
             s.outer_finalize(eps, k, b["sums"])
 

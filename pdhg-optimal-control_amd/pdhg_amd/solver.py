@@ -58,5 +58,6 @@ def load_solution(dir, filename):
 
 
 def load_middle_solution(dir, filename):
-    """solver.py:28-33 — returns [max_iters, phi_all, rho_all, alp_all, errs_all]."""
+    """solver.py:28-33 — returns [max_iters, phi_all, rho_all, alp_all, errs_all] (+ [phi_end, stepsz_param]
+    when written by pdhg_amd.utils_pdhg_solver.PDHG_multi_step, which needs them to resume)."""
     return _load(os.path.join(dir, "{}.npz".format(filename)))

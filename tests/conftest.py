@@ -4,6 +4,8 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# the oracle's FFT threads: the GPU box shows the whole machine's CPUs but gives a job a 16-CPU share
+os.environ.setdefault("ORACLE_FFT_WORKERS", str(min(16, os.cpu_count() or 1)))
 for p in (os.path.join(ROOT, "pdhg-optimal-control_amd"), os.path.join(ROOT, "oracle"), ROOT,
           os.path.join(ROOT, "tests", "golden")):
     if p not in sys.path:

@@ -1,0 +1,196 @@
+"""The kernel instantiations every BASELINE config runs, against the float64 oracle (pytest -m gpu).
+
+Each case below selects, and asserts through ``pdhg_path_info``, the size-specialised kernels of one
+bench config (BASELINE.json configs[1..4]) at the window length the config uses where that matters
+(closed-form Thomas pivots at T = 200 / 400, utils_precond.py:10-35, :142-178):
+
+  c3_ws_T200         C3's x transform k_precond_xt_ws_2d<4096,1,false>, pivots over T = 200
+  c3_fr_4096x256     the same x transform under the fused-residual dual (update_fns_in_pdhg.py:72-96,
+                     150-165) and the 8-row fast kernels at nx = 4096
+  c3_rows_ny4096     C3's row kernels: k_res_fwdy_fused_2d<2,4096,8,512>, k_invy_update_fast_2d<4096,8,512>
+  c2_x2048           C2's x transform at nx = 2048, T = 100 (fused residual on, as at 2048^2)
+  c2_rows_ny2048     C2's ny = 2048 row kernels, T = 100
+  c4_halfreal_x8192  C4's half-real nx = 8192 warp-specialised x transform (no fused residual, as at 8192^2)
+  c4_rows_ny8192     C4's ny = 8192 four-row kernels
+  c1_exact           C1 itself: egno 1, 1-D, nx = 65536, T = 400 (four-step DHT, 1-D Thomas)
+
+The fp64 oracle needs 20 s - 6 min per iteration at these sizes, so tests/golden/make_config_fixtures.py
+ran it once (from the float32-rounded initial state the device holds) and kept the oracle state at 8192
+sampled points per array, the full-array norms, the last iteration's err1/err2 and the oracle's own
+sensitivity to one float32 rounding of its initial values.  The device runs the same iterations in fp32
+and is compared on those points.
+
+Bounds (relative L2 over the sampled points; the larger of the fixed bound and K_SENS x the oracle's
+sensitivity for that quantity):
+  fixed: phi after the first primal update 1e-6, phi after the run 1e-5 (the north-star bound), rho 1e-5
+  and each live alp array 1e-4 from the reference state; from the seeded rough state the primal update
+  U itself 5e-4 and rho / alp 2e-4 / 1e-3 (test_gpu_parity's fp32 bounds for that state); err1 1e-3.
+  sensitivity: with epsl = 0.1 the reference's explicit sigma*epsl*Lap(phi_bar) dual term amplifies a
+  float32 rounding of phi_bar by ~sigma*epsl*8/dx^2 = 5e5 at dx = 2/4096, so after one iteration the
+  oracle itself moves rho by ~5e-5 under such a perturbation (and by 14 % after two); the controls follow
+  one-sided differences of phi_bar whose float32 precision is ulp(phi)/(dx*|grad phi|) (~1e-3 at C1).
+  K_SENS = 10: the device rounds every intermediate, the perturbation rounds only the inputs.
+Runs with epsl = 0.1 therefore stop after one iteration; test_one_step_eps below checks a further
+iteration (the fused residual formed by the first dual sweep) from the device's own state.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from _problems import device_ctx, make_problem, oracle_fns, rel
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+TAU, SIGMA = 0.1 / 1.5, 0.1 * 1.5
+K_SENS = 10.0
+
+# name: (environment for the context, expected pdhg_path_info values)
+CASES = {
+    "c3_ws_T200": ({}, {"fast_xt": 2, "half_real": 0}),
+    "c3_fr_4096x256": ({"PDHG_FUSE_RES": "1"}, {"fast_xt": 2, "fused_residual": 1, "rows_rw": 8, "fast_dual": 8}),
+    "c3_rows_ny4096": ({"PDHG_FUSE_RES": "1"}, {"fused_residual": 1, "rows_rw": 8, "res_threads": 512,
+                                                "upd_threads": 512, "fast_dual": 8}),
+    "c2_x2048": ({"PDHG_FUSE_RES": "1"}, {"fast_xt": 1, "fused_residual": 1, "rows_rw": 8}),
+    "c2_rows_ny2048": ({"PDHG_FUSE_RES": "1"}, {"fused_residual": 1, "rows_rw": 8, "res_threads": 512,
+                                                "upd_threads": 512}),
+    "c4_halfreal_x8192": ({"PDHG_FUSE_RES": "0"}, {"fast_xt": 2, "half_real": 1, "fused_residual": 0}),
+    "c4_rows_ny8192": ({}, {"rows_rw": 4, "fused_residual": 0, "res_threads": 1024, "upd_threads": 1024}),
+    "c1_exact": ({}, {"fourstep": 1, "glb_line": 1}),
+}
+
+
+def _fixture(name):
+    path = os.path.join(HERE, "golden", "cfg_{}.npz".format(name))
+    if not os.path.exists(path):
+        pytest.fail("missing fixture {} (python tests/golden/make_config_fixtures.py {})".format(path, name))
+    return np.load(path)
+
+
+def _live(ndim, egno, alp):
+    if ndim == 1 or egno == 3:
+        return [a[..., 0] for a in alp]
+    return [a[..., 0 if i < 2 else 1] for i, a in enumerate(alp)]
+
+
+def _f32_state(P):
+    f = lambda a: np.asarray(a, dtype=np.float32).astype(np.float64)  # noqa: E731
+    return f(P["phi"]), f(P["rho"]), tuple(f(a) for a in P["alp"])
+
+
+def _norm_dev(x, ref_norm):
+    return abs(np.linalg.norm(x) / float(ref_norm) - 1)
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_config_instantiation(native, name, monkeypatch):
+    env, expect = CASES[name]
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    F = _fixture(name)
+    egno, ndim, nx, ny, T = (int(v) for v in F["meta"])
+    failures = []
+    for tag in [str(t) for t in F["runs"]]:
+        g = lambda k: F[tag + "__" + k]  # noqa: E731
+        epsl, n, seeded = float(g("epsl")), int(g("iters")), bool(int(g("seeded")))
+        ip, ir = g("idx_phi"), g("idx_rho")
+        sens = g("sens")
+        tol = {"phi1": max(1e-6, K_SENS * sens[0]), "phi": max(1e-5, K_SENS * sens[1]),
+               "rho": max(2e-4 if seeded else 1e-5, K_SENS * sens[2]), "U1": 5e-4,
+               # err1 = ||phi' - phi|| / ||phi||: a difference of iterates, 100x more sensitive than phi
+               "err1": max(1e-3, 100 * K_SENS * sens[1])}
+        for a in range(len(sens) - 3):
+            tol["alp{}".format(a)] = max(1e-3 if seeded else 1e-4, K_SENS * sens[3 + a])
+        P = make_problem(egno, ndim, nx, ny, T, epsl, seeded=seeded)
+        phi0, rho0, alp0 = _f32_state(P)
+        ctx = device_ctx(P, "fp32")
+        try:
+            for key, val in expect.items():
+                assert ctx.path_info(key) == val, (name, key, ctx.path_info(key), val)
+            ctx.set_state(phi0, rho0, alp0)
+            ctx.update_primal(TAU)
+            phi1 = ctx.get_state()[0]
+            m = {"phi1": rel(phi1.reshape(-1)[ip], g("phi1")), "phi1_norm": _norm_dev(phi1, g("phi1_norm"))}
+            if seeded:   # the primal update itself (zero from the reference state)
+                m["U1"] = rel((phi1.reshape(-1)[ip] - phi0.reshape(-1)[ip]) / TAU, g("U1"))
+            del phi1
+            ctx.set_state(phi0, rho0, alp0)
+            st = ctx.iterate(n, TAU, SIGMA, -1.0, 1)
+            phi, rho, alp = ctx.get_state()
+            m["phi"], m["phi_norm"] = rel(phi.reshape(-1)[ip], g("phi")), _norm_dev(phi, g("phi_norm"))
+            m["rho"], m["rho_norm"] = rel(rho.reshape(-1)[ir], g("rho")), _norm_dev(rho, g("rho_norm"))
+            for a, arr in enumerate(_live(ndim, egno, alp)):
+                ref = g("alp{}".format(a))
+                if np.linalg.norm(ref) > 0:
+                    m["alp{}".format(a)] = rel(arr.reshape(-1)[ir], ref)
+                    m["alp{}_norm".format(a)] = _norm_dev(arr, g("alp{}_norm".format(a)))
+            e1_o = float(g("err")[0])
+            m["err1"] = abs(st["err1"] - e1_o) / e1_o if e1_o > 0 else abs(st["err1"])
+        finally:
+            ctx.close()
+        print("CFG {} {}: {} | sens {}".format(name, tag, " ".join("{}={:.2e}".format(k, v) for k, v in m.items()),
+                                               " ".join("{:.1e}".format(v) for v in sens)), flush=True)
+        if not (st["iters_run"] == n and st["status"] == 0 and not st["nan_seen"]):
+            failures.append((tag, "run", st))
+        for k, v in m.items():
+            bound = tol[k[:-5] if k.endswith("_norm") else k]
+            if not v <= bound:
+                failures.append((tag, k, v, bound))
+    assert not failures, failures
+
+
+# one further iteration from the device's own state (epsl = 0.1, seeded rough state): the fused residual
+# formed by the first dual sweep feeds the second primal update.  Short windows with the C3/C4 kernels
+# forced (PDHG_XT_WS=1 selects the warp-specialised x transform below T = 16), so the oracle runs here.
+ONE_STEP = {
+    # name: (egno, nx, ny, T, env, expected path)
+    "ws_fr_4096x256": (2, 4096, 256, 4, {"PDHG_XT_WS": "1", "PDHG_FUSE_RES": "1"},
+                       {"fast_xt": 2, "fused_residual": 1}),
+    "rows_ny4096_fr": (2, 64, 4096, 4, {"PDHG_FUSE_RES": "1"}, {"fused_residual": 1, "res_threads": 512}),
+    "halfreal_x8192": (2, 8192, 16, 4, {}, {"fast_xt": 2, "half_real": 1}),
+    "rows_ny8192": (2, 64, 8192, 4, {}, {"rows_rw": 4}),
+}
+
+
+@pytest.mark.parametrize("name", list(ONE_STEP))
+def test_one_step_eps(native, name, monkeypatch):
+    """Device iteration 2 vs one oracle iteration from the device's iteration-1 state (float32 values, so the
+    oracle starts from exactly the device's state).  Bounds: the larger of the seeded-state bounds (phi 1e-5,
+    rho 2e-4, alp 1e-3) and K_SENS x the oracle's sensitivity to one float32 rounding of that state."""
+    egno, nx, ny, T, env, expect = ONE_STEP[name]
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    P = make_problem(egno, 2, nx, ny, T, 0.1, seeded=True)
+    ctx = device_ctx(P, "fp32")
+    try:
+        for key, val in expect.items():
+            assert ctx.path_info(key) == val, (name, key, ctx.path_info(key), val)
+        ctx.set_state(*_f32_state(P))
+        st1 = ctx.iterate(1, TAU, SIGMA, -1.0, 1)
+        s1 = ctx.get_state()
+        st2 = ctx.iterate(1, TAU, SIGMA, -1.0, 1)
+        s2 = ctx.get_state()
+    finally:
+        ctx.close()
+    assert st1["status"] == 0 and st2["status"] == 0
+    primal, dual = oracle_fns(P)
+
+    def step(phi, rho, alp):
+        phi_n = primal(phi, rho, 70.0, alp, TAU, P["dt"], P["dsp"], P["fns"], P["fv"], 0.1, P["x_arr"], None)
+        rho_n, alp_n = dual(2 * phi_n - phi, rho, 70.0, alp, SIGMA, P["dt"], P["dsp"], 0.1, P["fns"], P["x_arr"],
+                            None, 2, -1.0)
+        return phi_n, rho_n, alp_n
+    o = step(*s1)
+    rng = np.random.default_rng(11)
+    pert = lambda a: a * (1.0 + rng.uniform(-1.0, 1.0, a.shape) * 2.0 ** -24)  # noqa: E731
+    p = step(pert(s1[0]), pert(s1[1]), tuple(pert(a) for a in s1[2]))
+    live_o, live_p, live_d = (_live(2, egno, x[2]) for x in (o, p, s2))
+    m = {"phi": (rel(s2[0], o[0]), max(1e-5, K_SENS * rel(p[0], o[0]))),
+         "rho": (rel(s2[1], o[1]), max(2e-4, K_SENS * rel(p[1], o[1])))}
+    for a in range(4):
+        if np.linalg.norm(live_o[a]) > 0:
+            m["alp{}".format(a)] = (rel(live_d[a], live_o[a]), max(1e-3, K_SENS * rel(live_p[a], live_o[a])))
+    print("ONESTEP {}: {}".format(name, " ".join("{}={:.2e}(<{:.1e})".format(k, v, b) for k, (v, b) in m.items())),
+          flush=True)
+    assert all(v <= b for v, b in m.values()), m

@@ -356,7 +356,7 @@ def test_glb_lines_1d_fp32(native, prec, monkeypatch):
     ctx.close()
 
 
-T1_FAST = [(1, 2, 4096, 256, 1, 0.0), (2, 2, 1024, 512, 1, 0.0), (1, 2, 512, 256, 1, 0.0)]
+T1_FAST = [(1, 2, 4096, 256, 1, 0.0), (2, 2, 2048, 256, 1, 0.0), (2, 2, 1024, 512, 1, 0.0), (1, 2, 512, 256, 1, 0.0)]
 
 
 @pytest.mark.parametrize("case", T1_FAST, ids=["e{}d{}_{}x{}_T{}_eps{}".format(*c) for c in T1_FAST])

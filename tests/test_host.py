@@ -113,3 +113,41 @@ def test_update_fns_tagged_for_device_loop():
     assert fp._pdhg_native is fd._pdhg_native and fp._pdhg_native["rho_alp_iters"] == 10
     assert S._native_tag(fp, fd) is not None
     assert S._native_tag(fp, lambda *a: None) is None
+
+
+def test_resume_from_middle_matches_straight_run(tmp_path, monkeypatch):
+    """Resuming PDHG_multi_step from the middle results after 2 of 4 windows gives the straight run's result
+    (the end row of the last finished window is saved for the next window's phi0)."""
+    nx, nt = 12, 5
+    x, fns, g, fv = _setup(nx, nt)
+    primal, dual = O.make_update_fns(1, 0, rho_alp_iters=10)
+    kw = dict(time_step_per_PDHG=2, stepsz_param=0.1, n_ctrl=1, fv=fv, N_maxiter=3000, print_freq=400, eps=1e-6,
+              verbose=False)
+    real_save = S.save
+
+    def save_and_snapshot(d, prefix, results):
+        real_save(d, prefix, results)
+        if len(results[1]) == 2:
+            real_save(d, "after2", results)
+    monkeypatch.setattr(S, "save", save_and_snapshot)
+    res_s, errs_s = S.PDHG_multi_step(primal, dual, fns, g, x, 1, nt, (nx,), 0.25, (2.0 / nx,), 70.0,
+                                      save_middle_dir=str(tmp_path), save_middle_prefix="mid", **kw)
+    res_r, errs_r = S.PDHG_multi_step(primal, dual, fns, g, x, 1, nt, (nx,), 0.25, (2.0 / nx,), 70.0,
+                                      load_middle_dir=str(tmp_path), load_middle_prefix="after2", **kw)
+    assert res_r[0][0] == res_s[0][0]
+    for a, b in zip(res_r[0][1:], res_s[0][1:]):
+        assert a.shape == b.shape and np.array_equal(a, b)
+    assert len(errs_r) == len(errs_s)
+
+
+def test_resume_without_end_row_raises(tmp_path):
+    """Middle results in the reference's 5-entry form hold no end row: resuming mid-run is refused."""
+    nx, nt = 8, 5
+    x, fns, g, fv = _setup(nx, nt)
+    primal, dual = O.make_update_fns(1, 0, rho_alp_iters=1)
+    phi = np.zeros((1, nx))
+    solver.save(str(tmp_path), "old", [3, [phi], [np.zeros((1, nx))], [np.zeros((2, 1, nx, 1))], [np.zeros((1, 2))]])
+    with pytest.raises(ValueError, match="end row"):
+        S.PDHG_multi_step(primal, dual, fns, g, x, 1, nt, (nx,), 0.25, (2.0 / nx,), 70.0, time_step_per_PDHG=2,
+                          stepsz_param=0.1, n_ctrl=1, fv=fv, N_maxiter=10, print_freq=5, eps=1e-6, verbose=False,
+                          load_middle_dir=str(tmp_path), load_middle_prefix="old")
