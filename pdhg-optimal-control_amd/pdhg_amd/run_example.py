@@ -6,9 +6,12 @@ Same flags, grid (egno 3: centred grid, bc (1, 0), n_ctrl 1), initial value J(x)
 marching (PDHG_multi_step with the NaN step-size back-off) and result layout
 (results = [(iters, phi, rho, alp)], errs_all).  The PDHG iterations of every window run on the GPU
 through libpdhg.so (make_update_fns tags the callables for the device loop).  Results are saved as an
-npz tree (pdhg_amd.solver) instead of a pickle.  The plotting / TensorBoard / trajectory flags are
-accepted for command-line compatibility and ignored (out of scope: DESIGN.md section 8).
-Extra flags: --precision {fp32,fp64}, --rho_alp_iters (the reference fixes 10), --out (root dir).
+npz tree (pdhg_amd.solver) instead of a pickle.  --plot writes the reference's figures (phi, each alp
+component, their sum; matplotlib, PNG) under plots/<stamp>/eg<egno>_<ndim>d, and with --plot_traj_num_1d > 0
+simulates the controlled trajectories from the solved alp (pdhg_amd.trajectories, run_example.py:342-393)
+and saves them as traj_<prefix>.npz (+ figures).  --tfboard is accepted and ignored (no TensorBoard).
+Extra flags: --precision {fp32,fp64}, --rho_alp_iters (the reference fixes 10), --out (root dir),
+--load_middle / --load_middle_timestamp (resume from middle results, run_example.py:246-248).
 """
 import argparse
 import os
@@ -16,7 +19,7 @@ import time
 
 import numpy as np
 
-from . import set_fns, solver, utils_pdhg_solver, utils_precond
+from . import set_fns, solver, trajectories, utils_pdhg_solver, utils_precond
 
 
 def build_parser():
@@ -38,7 +41,9 @@ def build_parser():
     A("--save_middle", type=int, default=0)
     A("--load", type=int, default=0)
     A("--load_timestamp", default="")
-    # plotting (:423-425) -- accepted, ignored
+    A("--load_middle", type=int, default=0)
+    A("--load_middle_timestamp", default="")
+    # plotting (:423-425)
     A("--tfboard", type=int, default=0)
     A("--plot", type=int, default=0)
     A("--plot_traj_num_1d", type=int, default=0)
@@ -74,7 +79,8 @@ def make_grid(ndim, egno, nx, ny, nt, x_period, y_period, T):
 
 def solve_HJ(ndim, n_ctrl, egno, epsl, fns_dict, nx, ny, nt, x_period, y_period, T, x_arr, c_on_rho,
              time_step_per_PDHG, stepsz_param, N_maxiter, print_freq, eps, bc, C=1.0, pow=1.0, Ct=1.0,
-             rho_alp_iters=10, precision="fp64", save_middle_dir=None, save_middle_prefix=None, verbose=True):
+             rho_alp_iters=10, precision="fp64", save_middle_dir=None, save_middle_prefix=None, load_middle_dir=None,
+             load_middle_prefix=None, verbose=True):
     """run_example.py:157-210 with the device-resident update functions."""
     dt = T / (nt - 1)
     dx, dy = x_period / nx, y_period / ny
@@ -90,7 +96,8 @@ def solve_HJ(ndim, n_ctrl, egno, epsl, fns_dict, nx, ny, nt, x_period, y_period,
                                              time_step_per_PDHG=time_step_per_PDHG, epsl=epsl,
                                              stepsz_param=stepsz_param, fv=fv, n_ctrl=n_ctrl, N_maxiter=N_maxiter,
                                              print_freq=print_freq, eps=eps, save_middle_dir=save_middle_dir,
-                                             save_middle_prefix=save_middle_prefix, verbose=verbose)
+                                             save_middle_prefix=save_middle_prefix, load_middle_dir=load_middle_dir,
+                                             load_middle_prefix=load_middle_prefix, verbose=verbose)
 
 
 def main(argv=None):
@@ -104,11 +111,19 @@ def main(argv=None):
     else:
         n_ctrl, bc = F.ndim, (0 if F.ndim == 1 else (0, 0))
     prefix = "nt{}_nx{}".format(F.nt, F.nx) if F.ndim == 1 else "nt{}_nx{}_ny{}".format(F.nt, F.nx, F.ny)
-    stamp = F.load_timestamp if F.load else time.strftime("%Y%m%d-%H%M%S")
+    if F.load:
+        stamp = F.load_timestamp
+    elif F.load_middle:
+        stamp = F.load_middle_timestamp
+    else:
+        stamp = time.strftime("%Y%m%d-%H%M%S")
+    if (F.load or F.load_middle) and not stamp:
+        raise SystemExit("--load / --load_middle need --load_timestamp / --load_middle_timestamp")
     save_dir = os.path.join(F.out, "check_points", stamp, "eg{}_{}d".format(F.egno, F.ndim))
+    plot_dir = os.path.join(F.out, "plots", stamp, "eg{}_{}d".format(F.egno, F.ndim))
     os.makedirs(save_dir, exist_ok=True)
     fns = set_fns.set_up_example_fns(F.egno, F.ndim, F.numerical_L_ind)
-    x_arr, _ = make_grid(F.ndim, F.egno, F.nx, F.ny, F.nt, F.x_period, F.y_period, F.T)
+    x_arr, t_arr = make_grid(F.ndim, F.egno, F.nx, F.ny, F.nt, F.x_period, F.y_period, F.T)
     if F.load:
         results, errs_all = solver.load_solution(save_dir, prefix)
     else:
@@ -117,13 +132,37 @@ def main(argv=None):
                                      F.print_freq, F.eps, bc, C=F.C, pow=F.pow, Ct=F.Ct,
                                      rho_alp_iters=F.rho_alp_iters, precision=F.precision,
                                      save_middle_dir=save_dir if F.save_middle else None,
-                                     save_middle_prefix=prefix if F.save_middle else None)
+                                     save_middle_prefix=prefix if F.save_middle else None,
+                                     load_middle_dir=save_dir if F.load_middle else None,
+                                     load_middle_prefix=prefix if F.load_middle else None)
         if F.save:
             solver.save(save_dir, prefix, (results, errs_all))
     iters, phi = results[-1][0], results[-1][1]
+    if F.plot:
+        plot_results(F, results, x_arr, t_arr, fns, bc, n_ctrl, plot_dir, prefix)
     print("windows: {}  last window iterations: {}  phi shape: {}  saved: {}".format(
         len(results), iters, np.shape(phi), save_dir if F.save else "-"), flush=True)
     return results, errs_all
+
+
+def plot_results(F, results, x_arr, t_arr, fns, bc, n_ctrl, plot_dir, prefix):
+    """The plot block of run_example.main (:296-393): figures of phi and alp, and the trajectories."""
+    os.makedirs(plot_dir, exist_ok=True)
+    phi, alp = np.asarray(results[-1][1]), np.asarray(results[-1][3])
+    try:
+        from . import plotting
+    except ImportError:            # matplotlib absent: trajectories are still computed and saved
+        plotting = None
+    if plotting is not None:
+        plotting.plot_solution_figs(phi, alp, x_arr, t_arr, F.ndim, F.egno, n_ctrl, plot_dir)
+    if F.plot_traj_num_1d > 0:
+        traj_alp, traj_x = trajectories.run_trajectories(F.egno, F.ndim, alp, fns, F.nt, x_arr, t_arr, F.x_period,
+                                                         F.y_period, F.T, bc, F.epsl, F.plot_traj_num_1d)
+        np.savez(os.path.join(plot_dir, "traj_{}.npz".format(prefix)), traj_x=traj_x, traj_alp=traj_alp,
+                 t=np.asarray(t_arr).reshape(-1))
+        if plotting is not None:
+            plotting.plot_traj_figs(traj_x, traj_alp, np.asarray(t_arr).reshape(-1), F.ndim, F.egno, n_ctrl,
+                                    plot_dir)
 
 
 if __name__ == "__main__":

@@ -6,14 +6,15 @@ the reference's jitted functions runs unchanged.  For speed use the
 device-resident loop in ``utils_pdhg_solver`` instead: per-call use moves the
 whole state over PCIe twice.
 
-Precision: fp32 by default (the bench precision); ``set_precision("fp64")``
-makes the drop-ins match the reference's float64 to roundoff.
+Precision: float64 by default, as the reference (jax_enable_x64, update_fns_in_pdhg.py:10), so a caller
+swapping these in for the reference's functions gets its arithmetic; ``set_precision("fp32")`` (or
+``make_update_fns(..., precision="fp32")``) selects the fp32 fast kernels the benchmark runs.
 """
 import numpy as np
 
 from .context import PDHGContext
 
-_PRECISION = ["fp32"]
+_PRECISION = ["fp64"]
 _CACHE = {}
 _CACHE_MAX = 4
 

@@ -289,6 +289,7 @@ def test_multi_step_window_marching(native):
 def test_dropin_update_functions(native):
     """update_fns_in_pdhg drop-ins (reference signatures) in fp64 vs the oracle."""
     from pdhg_amd import set_fns, update_fns_in_pdhg as U
+    prev = U.get_precision()
     U.set_precision("fp64")
     try:
         P = make_problem(2, 2, 16, 12, 3, 0.1)
@@ -309,7 +310,7 @@ def test_dropin_update_functions(native):
                                              P["fns"], P["x_arr"], None, 2, P["bc"], rho_alp_iters=10, eps=1e-6)
         assert rel(r_d, r_o) < 1e-10
     finally:
-        U.set_precision("fp32")
+        U.set_precision(prev)
         U.clear_cache()
 
 
@@ -377,3 +378,45 @@ def test_t1_x_transform_fp32(native, case):
     assert rel(phi_d, phi_o) < 1e-5 and rel(rho_d, rho_o) < 1e-5
     assert abs(st["err1"] - e1_o) <= 1e-3 * e1_o
     ctx.close()
+
+
+PRECOND_1D = [   # (C, pow, Ct): utils_precond.py:125-134, run_example.py:436-438 flags
+    (2.0, 1.0, 1.0), (1.0, 2.0, 1.0), (1.0, 1.0, 0.0), (1.0, 1.0, 2.0), (0.5, 2.0, 0.0), (3.0, 2.0, 2.0)]
+
+
+@pytest.mark.parametrize("cpc", PRECOND_1D, ids=["C{}_pow{}_Ct{}".format(*c) for c in PRECOND_1D])
+@pytest.mark.parametrize("prec", ["fp64", "fp32"])
+@pytest.mark.parametrize("case", [(1, 1, 256, 1, 8, 0.0), (2, 1, 65536, 1, 6, 0.0)], ids=["e1_256_T8", "e2_65536_T6"])
+def test_precond_1d_parameters(native, case, prec, cpc):
+    """H1_precond_1d with non-default C, pow and Ct (diagonal (C - fv)^pow + Ct * Lap_t, off-diagonals
+    -Ct/dt^2; Ct = 0 decouples the time rows): the primal update and 3 iterations vs the oracle.  fp64
+    <= 1e-10 (x10 at 65536 points, see _big); fp32 from the seeded state: phi' <= 1e-6, U <= 5e-4."""
+    C, pw, Ct = cpc
+    P = make_problem(*case)
+    primal, dual = oracle_fns(P, C=C, pow=pw, Ct=Ct)
+    phi_o = primal(P["phi"], P["rho"], 70.0, P["alp"], TAU, P["dt"], P["dsp"], P["fns"], P["fv"], P["epsl"],
+                   P["x_arr"], None)
+    ctx = device_ctx(P, prec, C=C, pow=pw, Ct=Ct)
+    try:
+        ctx.set_state(P["phi"], P["rho"], P["alp"])
+        ctx.update_primal(TAU)
+        phi_d = ctx.get_state()[0]
+        U_o, U_d = (phi_o - P["phi"]) / TAU, (phi_d - P["phi"]) / TAU
+        if prec == "fp64":
+            assert rel(U_d, U_o) < 1e-10 * _big(P)
+        else:
+            assert rel(phi_d, phi_o) < 1e-6 and rel(U_d, U_o) < 5e-4
+        phi, rho, alp = P["phi"], P["rho"], P["alp"]
+        for _ in range(3):
+            phi_n = primal(phi, rho, 70.0, alp, TAU, P["dt"], P["dsp"], P["fns"], P["fv"], P["epsl"], P["x_arr"], None)
+            rho, alp = dual(2 * phi_n - phi, rho, 70.0, alp, SIGMA, P["dt"], P["dsp"], P["epsl"], P["fns"],
+                            P["x_arr"], None, 1, -1.0)
+            phi = phi_n
+        ctx.set_state(P["phi"], P["rho"], P["alp"])
+        st = ctx.iterate(3, TAU, SIGMA, -1.0, 1)
+        assert st["iters_run"] == 3
+        phi_d, rho_d, _ = ctx.get_state()
+        tol = 1e-10 * _big(P) if prec == "fp64" else 1e-5
+        assert rel(phi_d, phi) < tol and rel(rho_d, rho) < (tol if prec == "fp64" else 2e-4)
+    finally:
+        ctx.close()

@@ -151,3 +151,11 @@ def test_resume_without_end_row_raises(tmp_path):
         S.PDHG_multi_step(primal, dual, fns, g, x, 1, nt, (nx,), 0.25, (2.0 / nx,), 70.0, time_step_per_PDHG=2,
                           stepsz_param=0.1, n_ctrl=1, fv=fv, N_maxiter=10, print_freq=5, eps=1e-6, verbose=False,
                           load_middle_dir=str(tmp_path), load_middle_prefix="old")
+
+
+def test_dropin_default_precision_is_fp64():
+    """The drop-ins compute in float64 unless asked otherwise, as the reference (update_fns_in_pdhg.py:10)."""
+    from pdhg_amd import update_fns_in_pdhg as U
+    assert U.get_precision() == "fp64"
+    fp, fd = S.make_update_fns(1, 0)
+    assert fp._pdhg_native["precision"] is None   # resolved to the module default when the context is made
