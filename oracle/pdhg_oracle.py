@@ -210,12 +210,19 @@ def compute_Dxx_fft_fv(ndim, nspatial, dspatial, bc):
     raise NotImplementedError
 
 
-def _lap_t(T, dt):
-    """dl, du, Lap_t_diag of utils_precond.py:128-130 / :164-166 (Ct factor applied by caller)."""
+def _lap_t(T, dt, cdtype=np.complex128):
+    """dl, du, Lap_t_diag of utils_precond.py:128-130 / :164-166 (Ct factor applied by caller).
+    cdtype: complex128 as the reference; complex64 when the oracle is run in float32 (test calibration)."""
     dl = -np.pad(1 / (dt * dt) * np.ones((T - 1,)), (1, 0))
     du = -np.pad(1 / (dt * dt) * np.ones((T - 1,)), (0, 1))
     diag = -np.array([-2 / (dt * dt)] * (T - 1) + [-1 / (dt * dt)])
-    return dl.astype(np.complex128), du.astype(np.complex128), diag
+    return dl.astype(cdtype), du.astype(cdtype), diag.astype(np.finfo(cdtype).dtype)
+
+
+def _dtypes(a):
+    """(real, complex) dtypes the preconditioner computes in: float64 / complex128 as the reference, or
+    float32 / complex64 for a float32 input (the float32 run of this oracle calibrates fp32 test bounds)."""
+    return (np.float32, np.complex64) if a.dtype == np.float32 else (np.float64, np.complex128)
 
 
 def H1_precond_1d(source_term, fv, dt, bc, C=1.0, pow=1, Ct=1):
@@ -223,22 +230,26 @@ def H1_precond_1d(source_term, fv, dt, bc, C=1.0, pow=1, Ct=1):
     nt, nx = source_term.shape
     if bc != 0:
         raise NotImplementedError
+    rdt, cdt = _dtypes(source_term)
+    fv = np.asarray(fv).astype(cdt)
     v = sfft.fft(source_term[1:, :], axis=1, workers=_WORKERS)
     thomas_b = (np.broadcast_to(-fv, (nt - 1, nx)) + C) ** pow
     if Ct != 0:
-        dl, du, diag = _lap_t(nt - 1, dt)
+        dl, du, diag = _lap_t(nt - 1, dt, cdt)
         dl, du = dl * Ct, du * Ct
         part = tridiagonal_solve(dl, thomas_b + diag[:, None] * Ct, du, v)
     else:
         part = v / thomas_b
     upd = sfft.ifft(part, axis=1, workers=_WORKERS).real
-    return np.concatenate([np.zeros((1, nx)), upd], axis=0)
+    return np.concatenate([np.zeros((1, nx), dtype=rdt), upd], axis=0)
 
 
 def H1_precond_2d(source_term, fv, dt, bc, C=1.0):
     """C u - (Dtt + Dxx + Dyy) u = source, u_0 = 0; utils_precond.py:142-178."""
     nt, nx, ny = source_term.shape
     bc_x, bc_y = bc
+    rdt, cdt = _dtypes(source_term)
+    fv = np.asarray(fv).astype(cdt)
     if bc_x == 0 and bc_y == 0:
         v = sfft.fft2(source_term[1:], axes=(1, 2), workers=_WORKERS)
     elif bc_x == 1 and bc_y == 0:
@@ -246,7 +257,7 @@ def H1_precond_2d(source_term, fv, dt, bc, C=1.0):
         v = sfft.fft(v, axis=2, workers=_WORKERS)
     else:
         raise NotImplementedError
-    dl, du, diag = _lap_t(nt - 1, dt)
+    dl, du, diag = _lap_t(nt - 1, dt, cdt)
     thomas_b = np.broadcast_to(-fv, (nt - 1, nx, ny)) + diag[:, None, None] + C
     part = tridiagonal_solve(dl, thomas_b, du, v)
     if bc_x == 0 and bc_y == 0:
@@ -254,7 +265,7 @@ def H1_precond_2d(source_term, fv, dt, bc, C=1.0):
     else:
         upd = sfft.ifft(part, axis=2, workers=_WORKERS).real
         upd = sfft.idct(upd, axis=1, workers=_WORKERS)
-    return np.concatenate([np.zeros((1, nx, ny)), upd], axis=0)
+    return np.concatenate([np.zeros((1, nx, ny), dtype=rdt), upd], axis=0)
 
 
 # ---------------------------------------------------------------------------

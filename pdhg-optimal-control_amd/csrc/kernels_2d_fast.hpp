@@ -289,17 +289,21 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
   float4 rows[GPT][RW];        // next task's residual rows x0 .. x0+RW-1
   float4 e0[GPT], e1[GPT];     // next task's edge-row terms (row x0, row x0+RW-1)
   float ev = 0.f;              // next task's strip-edge term number tid
-  auto load_rows = [&](int task) {
+  // rows [r0, r1) of a task (NT = 1024: half before the transform, half after, so that only 4 rows of
+  // loads are live across the FFT's registers)
+  auto load_rows = [&](int task, int r0, int r1) {
     const int jt = task / ngx, j = p.row_base + jt, x0 = (task - jt * ngx) * RW;
-    if (tid < NEY) ev = p.ey[((size_t)j * nx + x0) * NSTRIP * 2 + tid];   // first: waited for alone
+    if (r0 == 0 && tid < NEY) ev = p.ey[((size_t)j * nx + x0) * NSTRIP * 2 + tid];   // first: waited for alone
     const float* R0 = p.res + (size_t)j * plane + (size_t)x0 * N;
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
       const int y = 4 * (tid + gi * NT);
 #pragma unroll
-      for (int r = 0; r < RW; ++r) rows[gi][r] = ld4(R0 + (size_t)r * N + y);
+      for (int r = 0; r < RW; ++r)
+        if (r >= r0 && r < r1) rows[gi][r] = ld4(R0 + (size_t)r * N + y);
     }
   };
+  constexpr int RSPLIT = (NT >= 1024) ? RW / 2 : RW;
   auto load_edges = [&](int task) {
     const int jt = task / ngx, j = p.row_base + jt, tile = task - jt * ngx;
     const float* E = p.ex + ((size_t)j * ngx + tile) * 2 * N;
@@ -312,7 +316,7 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
   };
   int task = blockIdx.x, buf = 0;
   if (task < ntask) {
-    load_rows(task);
+    load_rows(task, 0, RW);
     load_edges(task);
     if (tid < NEY) eyl[0][tid] = ev;
   }
@@ -355,15 +359,16 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
         for (int e = 0; e < 4; ++e) Af[2 * e] = f4(v[r], e);
       }
     }
-    const bool more = task + (int)gridDim.x < ntask;
-    if (more) load_rows(task + gridDim.x);
+    // the next task's loads are unconditional (the last task re-loads its own rows): a conditional load
+    // keeps the previous registers live across the transform on the not-taken path (spills at NT = 1024)
+    const int nxt = min(task + (int)gridDim.x, ntask - 1);
+    load_rows(nxt, 0, RSPLIT);
     lds_sync();
     if constexpr (TWL) lds_fft_inplace_tl<C, N, NL, NT>(A, twl);
     else lds_fft_inplace<C, N, NL, NT>(A, twy);
-    if (more) {
-      if (tid < NEY) eyl[buf ^ 1][tid] = ev;   // read one barrier after its last use two tasks ago
-      load_edges(task + gridDim.x);
-    }
+    if (tid < NEY) eyl[buf ^ 1][tid] = ev;   // read one barrier after its last use two tasks ago
+    if constexpr (RSPLIT < RW) load_rows(nxt, RSPLIT, RW);
+    load_edges(nxt);
     float* wk = p.work + (size_t)j * nb * nx * B;
     for (int t = tid; t < nb * CS4; t += NT) {
       const int b = t >> lCS4, part = t & (CS4 - 1);

@@ -19,6 +19,8 @@
 #include "kernels_dual_lds.hpp"
 #include "kernels_common.hpp"
 #include "kernels_xslab.hpp"
+#include "kernels_xt_batch.hpp"
+#include "kernels_thomas_chunk.hpp"
 
 using namespace pdhg;
 
@@ -122,6 +124,10 @@ struct Impl : ImplBase {
   int nt1d = 256;                 // 1-D residual / update block size (1024 on the global-scratch path)
   bool fast_xt = false;
   bool ws_xt = false;             // warp-specialised variant (k_precond_xt_ws_2d)            // fp32 power-of-two nx: k_precond_xt_fast_2d
+  bool batch_xt = false;          // row-batched variant (k_precond_xt_batch_2d: 4 rows per transform, 1024 threads)
+  size_t lds_batch_xt = 0;
+  int xt_rpre = 0;
+  bool thomas_chunk = false;      // 1-D fp32: t-solve in chunks of 32 rows (k_thomas_chunk_1d)
   size_t lds_fast_xt = 0;
   int RWf = 8, NTf = 1024, g_fast_upd = 1;
   size_t lds_fast = 0, lds_fast_tw = 0;
@@ -266,6 +272,13 @@ struct Impl : ImplBase {
         fast_xt = true;
         ws_xt = (nxg == 4096) && !short_win;   // the other widths spill registers in the warp-specialised form
         if (const char* e = getenv("PDHG_XT_WS")) ws_xt = atoi(e) != 0;   // tuning override
+        // row-batched x transform (k_precond_xt_batch_2d): 4 rows per transform, 1024 threads.  Measured at C3
+        // (nx = 4096, T = 200): 16.2 -> 14.5 ms against the warp-specialised kernel; at C2 (nx = 2048,
+        // T = 100) 2.07 -> 1.82 ms against the single-role one.  nx = 1024 / 512 spill in it: not selected.
+        batch_xt = (nxg == 4096 || nxg == 2048) && T >= 4;
+        if (const char* e = getenv("PDHG_XT_BATCH")) batch_xt = atoi(e) != 0;   // tuning override
+        if (const char* e = getenv("PDHG_XT_RPRE")) xt_rpre = atoi(e);           // tuning: rows prefetched across the FFT
+        lds_batch_xt = (size_t)(4 * (4096 + 4096 / 16) + twlds_size(nxg)) * sizeof(C);
         // padded FFT buffer + theta, E, b' (float2 per item) + twiddle seeds (TwLds<nx>)
         lds_fast_xt = ws_xt ? (size_t)(2 * (4096 + 4096 / 16) + 816) * sizeof(C)
                             : (size_t)(4096 + 4096 / 16 + 3 * 4096 + 816) * sizeof(C);
@@ -340,6 +353,9 @@ struct Impl : ImplBase {
       g4 = 1;
       gx5 = (nx + 255) / 256;
       g5 = std::max(1, std::min(T, 8192 / std::max(1, gx5)));
+      // chunked t-solve: one wave per 32-row chunk of 64 modes (T <= 512, Ct != 0)
+      thomas_chunk = sizeof(R) == 4 && pb.Ct != 0.0 && T <= 16 * 32;
+      if (const char* e = getenv("PDHG_THOMAS_CHUNK")) thomas_chunk = thomas_chunk && atoi(e) != 0;   // override
     }
     g_outer = 2048;
     partial_rows = std::max<size_t>({(size_t)gx4 * g4, (size_t)gx5 * g5, (size_t)g_outer, (size_t)g_fast_upd,
@@ -687,6 +703,17 @@ struct Impl : ImplBase {
   }
 
   // ---------------- launches ----------------
+  void launch_thomas_1d(const KP<R>& p) {
+    if constexpr (sizeof(R) == 4) {
+      if (thomas_chunk) {
+        const int P = (pb.T + 31) / 32;
+        hipLaunchKernelGGL((k_thomas_chunk_1d<32>), dim3((pb.nx + 63) / 64), dim3(64 * P), 0, stream, p);
+        return;
+      }
+    }
+    hipLaunchKernelGGL((k_thomas_1d<R>), dim3((pb.nx + 255) / 256), dim3(256), 0, stream, p);
+  }
+
   // x transform + Thomas in t + inverse x transform of the spectral blocks in p.work (p.nx-point lines,
   // p.nb blocks); p.xt_phase selects the sweeps (t-slab)
   int launch_precond(const KP<R>& p, int nblk = -1) {   // nblk: blocks [p.b0, p.b0 + nblk) (default: all)
@@ -726,7 +753,24 @@ struct Impl : ImplBase {
           hipLaunchKernelGGL(kern, g, dim3(512), lds_fast_xt, stream, p, twx);
           return (int)PDHG_OK;
         };
-        if (ws_xt) {
+        if (batch_xt) {
+          auto gob = [&](auto kern) -> int {
+            int r2;
+            if ((r2 = ensure_lds(kern, lds_batch_xt))) return r2;
+            hipLaunchKernelGGL(kern, g, dim3(1024), lds_batch_xt, stream, p, twx);
+            return (int)PDHG_OK;
+          };
+          switch (p.nx) {
+            case 4096:
+              if (xt_rpre == 2) rc = gob(k_precond_xt_batch_2d<4096, 1, 4, 2>);
+              else rc = gob(k_precond_xt_batch_2d<4096, 1>);
+              break;
+            case 2048: rc = gob(k_precond_xt_batch_2d<2048, 2>); break;
+            case 1024: rc = gob(k_precond_xt_batch_2d<1024, 4>); break;
+            case 512: rc = gob(k_precond_xt_batch_2d<512, 8>); break;
+            default: rc = fail(PDHG_ERR_UNSUPPORTED, "no batched x kernel for nx=%d", p.nx);
+          }
+        } else if (ws_xt) {
           switch (p.nx) {
             case 8192: rc = go(k_precond_xt_ws_2d<4096, 1, true>); break;
             case 4096: rc = go(k_precond_xt_ws_2d<4096, 1>); break;
@@ -839,7 +883,7 @@ struct Impl : ImplBase {
       }
       {
         ProfScope ps(this, "precond");
-        hipLaunchKernelGGL((k_thomas_1d<R>), dim3((pb.nx + 255) / 256), dim3(256), 0, stream, p);
+        launch_thomas_1d(p);
       }
       {
         ProfScope ps(this, "update");
@@ -880,7 +924,7 @@ struct Impl : ImplBase {
       }
       {
         ProfScope ps(this, "precond");
-        hipLaunchKernelGGL((k_thomas_1d<R>), dim3((pb.nx + 255) / 256), dim3(256), 0, stream, p);
+        launch_thomas_1d(p);
       }
       {
         ProfScope ps(this, "update");
@@ -1705,10 +1749,11 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
     if (k == "fused_residual") *value = im.fuse_res ? 1 : 0;
     else if (k == "fast_rows") *value = im.fast_rows ? 1 : 0;
     else if (k == "fast_dual") *value = im.fast_dual ? im.dual_rx : -1;
-    else if (k == "fast_xt") *value = im.fast_xt ? (im.ws_xt ? 2 : 1) : 0;
+    else if (k == "fast_xt") *value = im.fast_xt ? (im.batch_xt && !im.half_real ? 3 : im.ws_xt ? 2 : 1) : 0;
     else if (k == "half_real") *value = im.half_real ? 1 : 0;
     else if (k == "fourstep") *value = im.fourstep ? 1 : 0;
     else if (k == "glb_line") *value = im.glb_line ? 1 : 0;
+    else if (k == "thomas_chunk") *value = im.thomas_chunk ? 1 : 0;
     else if (k == "rows_rw") *value = im.fast_rows ? im.RWf : 0;   // rows per fast row-kernel workgroup
     // threads of the fast row kernels as launched (ny = 4096: 512 instead of 1024 per half_nt)
     else if (k == "res_threads") *value = im.fast_rows ? ((im.NTf == 1024 && im.RWf == 8 && (im.half_nt & 1) &&

@@ -14,13 +14,17 @@ Runs ("kind_e<epsl>_n<iterations>"):
   seeded  from the seeded rough parity state of SURVEY.md §8(d) (drives every mask / clip branch; from the
           reference state the first primal update is exactly zero: the terminal c/dt cancels -rho/dt).
 The initial state is rounded to float32 first, so the oracle starts from exactly what the fp32 device
-holds.  Every run also stores the oracle's own sensitivity: the relative change of its result when
-every initial value is perturbed by one float32 rounding (relative 2^-24, seeded uniform).  Two effects
-make it large: with epsl > 0 the reference's explicit sigma*epsl*Lap(phi_bar) dual term amplifies such
-perturbations by ~sigma*epsl*8/dx^2 per iteration (5e5 at dx = 2/4096), and the controls follow the
-one-sided differences of phi_bar, whose relative precision in float32 is ulp(phi)/(dx*|grad phi|) (~1e-3
-at C1's dx = 2/65536).  An fp32 implementation cannot agree with the fp64 oracle better than this, so
-the tests bound each quantity by the larger of a fixed bound and a multiple of it.
+holds.  Every run also stores "e32": how far the same oracle, executed in float32 from the same state
+(pdhg_oracle follows a float32 input through the preconditioner: complex64 FFTs and Thomas), lands from
+its float64 result at the sampled points -- the accuracy the reference algorithm itself reaches in
+float32.  Three effects make it large at these sizes: with epsl > 0 the reference's explicit
+sigma*epsl*Lap(phi_bar) dual term amplifies rounding by ~sigma*epsl*8/dx^2 per iteration (5e5 at
+dx = 2/4096); from a rough state the H1 preconditioner recovers low modes of U from a residual dominated
+by high ones (float32 FFT round-off relative to |R|); and the controls follow one-sided differences of
+phi_bar, whose float32 precision is ulp(phi)/(dx*|grad phi|) (~1e-3 at C1's dx = 2/65536).  The tests bound
+each quantity by the larger of a fixed bound and a multiple of e32.  (The "sens" entries are the older
+calibration of the first fixtures: the float64 oracle's change under one float32 rounding of the initial
+values only; no longer generated.)
 rho_alp_iters = 1, dt = 1/max(T, 40) (tests/_problems.make_problem).
 Run:  python tests/golden/make_config_fixtures.py [name ...]
 """
@@ -43,7 +47,7 @@ NSAMPLE = 8192
 CASES = {
     "c3_ws_T200": (2, 2, 4096, 16, 200, [("ref", 0.1, 1), ("ref", 0.0, 10), ("seeded", 0.1, 1)],
                    "C3 x transform: k_precond_xt_ws_2d<4096> and closed-form pivots at T = 200"),
-    "c3_fr_4096x256": (2, 2, 4096, 256, 64, [("ref", 0.1, 1), ("ref", 0.0, 6), ("seeded", 0.1, 1)],
+    "c3_fr_4096x256": (2, 2, 4096, 256, 32, [("ref", 0.1, 1), ("ref", 0.0, 10), ("seeded", 0.1, 1)],
                        "C3 x transform with the fused-residual dual and 8-row fast kernels (nx = 4096)"),
     "c3_rows_ny4096": (2, 2, 64, 4096, 32, [("ref", 0.1, 1), ("ref", 0.0, 10), ("seeded", 0.1, 1)],
                        "C3 row kernels: ny = 4096 fused residual / update with 512 threads"),
@@ -135,20 +139,37 @@ def generate(name):
         for a, arr in enumerate(live_alp(P, alp)):
             o["alp{}".format(a)] = arr.reshape(-1)[ir]
             o["alp{}_norm".format(a)] = np.linalg.norm(arr)
-        # sensitivity to one float32 rounding of every initial value
-        rng = np.random.default_rng(7)
-
-        def pert(a):
-            return a * (1.0 + rng.uniform(-1.0, 1.0, a.shape) * 2.0 ** -24)
-        s1, sp, sr, sa, _ = iterate(P, pert(P["phi"]), pert(P["rho"]), tuple(pert(a) for a in P["alp"]), n)
-        sens = [rel(s1, phi1), rel(sp, phi), rel(sr, rho)]
-        sens += [rel(x, y) for x, y in zip(live_alp(P, sa), live_alp(P, alp))]
-        o["sens"] = np.array(sens)    # phi1, phi, rho, alp0.. (relative L2, full arrays)
-        print("  {} {} sensitivity {}".format(name, tag, " ".join("{:.2e}".format(v) for v in sens)), flush=True)
         out.update({tag + "__" + k: v for k, v in o.items()})
         del P, phi1, phi, rho, alp
+    for (kind, epsl, n), tag in zip(runs, tags):
+        if tag + "__e32" not in out:
+            out[tag + "__e32"] = float32_run(egno, ndim, nx, ny, T, kind, epsl, n, {k.split("__", 1)[1]: v for k, v in
+                                                                                 out.items() if k.startswith(tag + "__")},
+                                             log="{} {}".format(name, tag))
     out["runs"] = np.array(tags)
     return out
+
+
+def float32_run(egno, ndim, nx, ny, T, kind, epsl, n, o, log=None):
+    """The oracle executed in float32 from the run's initial state, compared with the stored float64 samples:
+    [phi1, U1, phi, rho, alp0.., err1] relative L2 at the sampled points (err1: relative difference)."""
+    P = initial_state(egno, ndim, nx, ny, T, kind, epsl)
+    f = np.float32
+    phi0 = P["phi"].astype(f)
+    P["x_arr"] = P["x_arr"].astype(f)
+    phi1, phi, rho, alp, err = iterate(P, phi0, P["rho"].astype(f), tuple(a.astype(f) for a in P["alp"]), n)
+    assert phi.dtype == np.float32 and rho.dtype == np.float32
+    ip, ir = o["idx_phi"], o["idx_rho"]
+    U1 = (phi1.astype(np.float64) - phi0) / TAU
+    e = [rel(phi1.reshape(-1)[ip], o["phi1"]), rel(U1.reshape(-1)[ip], o["U1"]), rel(phi.reshape(-1)[ip], o["phi"]),
+         rel(rho.reshape(-1)[ir], o["rho"])]
+    for a, arr in enumerate(live_alp(P, alp)):
+        e.append(rel(arr.reshape(-1)[ir], o["alp{}".format(a)]))
+    e1 = float(o["err"][0])
+    e.append(abs(float(err[0]) - e1) / e1 if e1 > 0 else abs(float(err[0])))
+    if log:
+        print("  {} float32 oracle vs float64: {}".format(log, " ".join("{:.2e}".format(v) for v in e)), flush=True)
+    return np.array(e)
 
 
 if __name__ == "__main__":

@@ -390,7 +390,10 @@ PRECOND_1D = [   # (C, pow, Ct): utils_precond.py:125-134, run_example.py:436-43
 def test_precond_1d_parameters(native, case, prec, cpc):
     """H1_precond_1d with non-default C, pow and Ct (diagonal (C - fv)^pow + Ct * Lap_t, off-diagonals
     -Ct/dt^2; Ct = 0 decouples the time rows): the primal update and 3 iterations vs the oracle.  fp64
-    <= 1e-10 (x10 at 65536 points, see _big); fp32 from the seeded state: phi' <= 1e-6, U <= 5e-4."""
+    <= 1e-10 (x10 at 65536 points, see _big); fp32 from the seeded state: phi' <= max(1e-6, 4 e32) and
+    U <= max(5e-4, 4 e32), e32 = distance of the oracle run in float32 from the float64 one (with Ct = 0 at
+    65536 points U = R/(C - lam)^pow recovers the low modes of a residual dominated by high ones: the
+    float32 oracle itself is 1e-5 off in phi' there)."""
     C, pw, Ct = cpc
     P = make_problem(*case)
     primal, dual = oracle_fns(P, C=C, pow=pw, Ct=Ct)
@@ -405,7 +408,14 @@ def test_precond_1d_parameters(native, case, prec, cpc):
         if prec == "fp64":
             assert rel(U_d, U_o) < 1e-10 * _big(P)
         else:
-            assert rel(phi_d, phi_o) < 1e-6 and rel(U_d, U_o) < 5e-4
+            f = np.float32
+            phi0 = P["phi"].astype(f)
+            phi_32 = primal(phi0, P["rho"].astype(f), 70.0, tuple(a.astype(f) for a in P["alp"]), TAU, P["dt"],
+                            P["dsp"], P["fns"], P["fv"], P["epsl"], P["x_arr"].astype(f), None)
+            assert phi_32.dtype == f
+            e32_phi, e32_U = rel(phi_32, phi_o), rel((phi_32 - phi0) / TAU, U_o)
+            assert rel(phi_d, phi_o) < max(1e-6, 4 * e32_phi), (rel(phi_d, phi_o), e32_phi)
+            assert rel(U_d, U_o) < max(5e-4, 4 * e32_U), (rel(U_d, U_o), e32_U)
         phi, rho, alp = P["phi"], P["rho"], P["alp"]
         for _ in range(3):
             phi_n = primal(phi, rho, 70.0, alp, TAU, P["dt"], P["dsp"], P["fns"], P["fv"], P["epsl"], P["x_arr"], None)

@@ -12,12 +12,16 @@ from _problems import make_problem, rel
 pytestmark = pytest.mark.gpu
 
 CASES = [
-    # (egno, nx, ny, T, P, k)   nx = 512: k_precond_xt_fast_2d;  nx = 4096: k_precond_xt_ws_2d
+    # (egno, nx, ny, T, P, k)   the x kernel follows the SLAB's row count (path asserted in the test):
+    # nx = 512: k_precond_xt_fast_2d; nx = 4096: k_precond_xt_batch_2d for slabs of >= 4 rows, else the
+    # single-role k_precond_xt_fast_2d (k_precond_xt_ws_2d: test_ws_slabs below)
     (1, 512, 256, 6, 2, 1),
     (2, 512, 256, 7, 3, 1),
     (1, 512, 256, 5, 5, 3),
-    (2, 4096, 256, 6, 2, 1),
+    (2, 4096, 256, 6, 2, 1),     # 3-row slabs: single-role
     (1, 4096, 256, 4, 3, 2),
+    (2, 4096, 256, 50, 2, 1),    # 25-row slabs (C3's slab length on 8 GPUs): batched x transform
+    (2, 4096, 256, 11, 2, 1),    # 6 + 5 rows: batched x transform with partial last batches
     (2, 8192, 256, 5, 2, 1),    # half-real x blocks (C4's nx)
     (1, 512, 256, 3, 3, 1),     # one-row slabs: the halo row is the whole slab
     (2, 512, 256, 19, 2, 1),    # residual tiles of 8 rows + untiled remainder rows
@@ -48,6 +52,9 @@ def test_slabs_match_single_context(native, egno, nx, ny, T, nr, k, overlap, exc
     phi_r, rho_r, alp_r = ref.get_state()
 
     slabs = _slabs(P, nr, k)
+    for s in slabs:   # the x kernel the slab runs (see CASES)
+        if nx == 4096:
+            assert s.path_info("fast_xt") == (3 if s.T >= 4 else 1), (s.T, s.path_info("fast_xt"))
     for s, part in zip(slabs, split_state(P["phi"], P["rho"], P["alp"], slab_bounds(T, nr))):
         s.set_state(*part)
     runner = SlabRunner(slabs, LocalComm(nr), overlap=overlap, exchange=exchange)
@@ -69,6 +76,33 @@ def test_slabs_match_single_context(native, egno, nx, ny, T, nr, k, overlap, exc
     ref.close()
 
 
+def test_ws_slabs(native, monkeypatch):
+    """The warp-specialised x transform (PDHG_XT_BATCH=0, slabs of >= 16 rows) through the slab phases (forward
+    sweep, carry fix-up, backward sweep from the right carry) against the single context."""
+    import torch
+    from pdhg_amd.context import PDHGContext
+    from pdhg_amd.slab import LocalComm, SlabRunner, join_state, slab_bounds, split_state
+    monkeypatch.setenv("PDHG_XT_BATCH", "0")
+    P = make_problem(2, 2, 4096, 256, 40, 0.0)
+    tau, sigma, n = 0.1 / 1.5, 0.1 * 1.5, 4
+    ref = PDHGContext(2, 2, 4096, 256, 40, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"], precision="fp32")
+    assert ref.path_info("fast_xt") == 2
+    ref.set_state(P["phi"], P["rho"], P["alp"])
+    ref.iterate(n, tau, sigma, -1.0, 1)
+    phi_r, rho_r, _ = ref.get_state()
+    slabs = _slabs(P, 2, 1)
+    assert all(s.path_info("fast_xt") == 2 for s in slabs)
+    for s, part in zip(slabs, split_state(P["phi"], P["rho"], P["alp"], slab_bounds(40, 2))):
+        s.set_state(*part)
+    SlabRunner(slabs, LocalComm(2)).iterate(n, tau, sigma, -1.0, 1)
+    torch.cuda.synchronize()
+    phi_s, rho_s, _ = join_state([s.get_state() for s in slabs])
+    assert rel(phi_s, phi_r) < 2e-5 and rel(rho_s, rho_r) < 2e-4
+    for s in slabs:
+        s.close()
+    ref.close()
+
+
 def test_slab_rejects_unsupported(native):
     from pdhg_amd import _native as N
     from pdhg_amd.slab import SlabContext
@@ -81,7 +115,8 @@ FUSED_CASES = [
     # (egno, nx, ny, T, P): the fused residual (k_dual_lds_2d FR + k_res_fwdy_fused_2d) inside t-slabs
     (1, 512, 256, 6, 2),
     (2, 512, 256, 7, 3),
-    (2, 4096, 256, 6, 2),      # warp-specialised x transform
+    (2, 4096, 256, 6, 2),      # 3-row slabs: single-role x transform
+    (2, 4096, 256, 16, 2),     # 8-row slabs: batched x transform
     (1, 512, 256, 3, 3),       # one-row slabs: the halo launch is the whole slab
     (2, 512, 256, 19, 2),      # residual tiles of 8 rows + remainder rows
 ]

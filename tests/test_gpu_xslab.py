@@ -2,7 +2,7 @@
 rows and the transposed spectrum through LocalComm, must reproduce the single-context iteration
 (pdhg_iterate) of the same window -- same state after n outer iterations within fp32 rounding, same
 error history and stop decisions -- for T = 1 (the reference's marching default) and longer windows,
-every x-transform kernel (generic, single-role, warp-specialised, half-real) and k = 1 / k > 1.
+the x-transform kernels x-slab windows select (one-row, single-role, half-real, generic) and k = 1 / k > 1.
 The single-context path is itself pinned to the oracle by test_gpu_parity.py; one case here also
 checks the x-slab state against the fp64 oracle directly."""
 import numpy as np
@@ -14,12 +14,12 @@ pytestmark = pytest.mark.gpu
 
 CASES = [
     # (egno, nx, ny, T, P, k, epsl)
-    (1, 512, 256, 1, 2, 1, 0.0),     # k_precond_xt_fast_2d, T = 1 (marching default)
+    (1, 512, 256, 1, 2, 1, 0.0),     # T = 1 (marching default): k_precond_x_t1_2d
     (2, 512, 256, 1, 4, 1, 0.1),
     (1, 512, 256, 3, 2, 3, 0.0),     # two buffer sets (rho_alp_iters > 1), T = 3
     (2, 512, 512, 2, 1, 1, 0.0),     # one slab: the halo ring is the slab itself
     (1, 512, 256, 1, 8, 1, 0.0),     # 64-row slabs
-    (2, 4096, 256, 1, 2, 1, 0.0),    # k_precond_xt_ws_2d
+    (2, 4096, 256, 1, 2, 1, 0.0),    # nx = 4096, T = 1: k_precond_x_t1_2d<4096>
     (2, 8192, 256, 1, 2, 1, 0.0),    # half-real x blocks (C4's nx)
     (1, 256, 256, 2, 2, 1, 0.0),     # generic x kernel (runtime plan)
     (2, 384, 256, 1, 2, 1, 0.0),     # non-power-of-two nx (radix-3 plan), 192-row slabs
