@@ -21,6 +21,7 @@
 #include "kernels_xslab.hpp"
 #include "kernels_xt_batch.hpp"
 #include "kernels_thomas_chunk.hpp"
+#include "kernels_fs_wide.hpp"
 
 using namespace pdhg;
 
@@ -128,6 +129,7 @@ struct Impl : ImplBase {
   size_t lds_batch_xt = 0;
   int xt_rpre = 0;
   bool thomas_chunk = false;      // 1-D fp32: t-solve in chunks of 32 rows (k_thomas_chunk_1d)
+  bool fs_wide = true;            // four-step DHT with 64-column / 32-row tiles (k_fs1w_1d / k_fs2w_1d)
   size_t lds_fast_xt = 0;
   int RWf = 8, NTf = 1024, g_fast_upd = 1;
   size_t lds_fast = 0, lds_fast_tw = 0;
@@ -349,6 +351,7 @@ struct Impl : ImplBase {
         // one workgroup per pair (T = 400 gave 200 workgroups for 256 CUs): 1.41 -> 1.12 ms per iteration
         fourstep = sizeof(R) == 4 && nx == 65536;
         if (const char* e = getenv("PDHG_FOURSTEP")) fourstep = fourstep && atoi(e) != 0;   // tuning override
+        if (const char* e = getenv("PDHG_FS_WIDE")) fs_wide = atoi(e) != 0;                 // tuning override
       }
       g4 = 1;
       gx5 = (nx + 255) / 256;
@@ -905,6 +908,7 @@ struct Impl : ImplBase {
   // 1-D primal with the four-step DHT (nx = 65536, fp32): residual + DHT, Thomas, inverse DHT + update
   int launch_fourstep_1d(const KP<R>& p) {
     if constexpr (sizeof(R) == 4) {
+      if (fs_wide) return launch_fourstep_wide_1d(p);
       constexpr int kFsNT = 1024;   // 16 waves: the load / unpack loops keep more rows in flight
       const int npairs = (pb.T + 1) / 2;
       const size_t lds1 = (size_t)2 * 256 * 16 * sizeof(C), lds2 = 2 * lds1;
@@ -934,6 +938,42 @@ struct Impl : ImplBase {
         hipLaunchKernelGGL((k_fs2_1d<1>), dim3(9, npairs), dim3(kFsNT), lds2, stream, p, tw256, Y);
       }
       hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, p.partials, 9 * npairs, row0_sq, p.ctrl);
+      HIP_TRY(hipGetLastError());
+    }
+    return PDHG_OK;
+  }
+
+  // the same with the wide-tile stages (kernels_fs_wide.hpp): 4 + 5 workgroups per row pair
+  int launch_fourstep_wide_1d(const KP<R>& p) {
+    if constexpr (sizeof(R) == 4) {
+      const int npairs = (pb.T + 1) / 2;
+      const size_t lds = (size_t)(64 * kFwLine + twlds_size(256)) * sizeof(C);
+      float2* Y = reinterpret_cast<float2*>(p.gscr);
+      int rc;
+      {
+        ProfScope ps(this, "residual");
+        if (pb.egno == 1) {
+          if ((rc = ensure_lds(k_fs1w_1d<0, 1>, lds))) return rc;
+          hipLaunchKernelGGL((k_fs1w_1d<0, 1>), dim3(4, npairs), dim3(1024), lds, stream, p, tw256, twx, Y);
+        } else {
+          if ((rc = ensure_lds(k_fs1w_1d<0, 2>, lds))) return rc;
+          hipLaunchKernelGGL((k_fs1w_1d<0, 2>), dim3(4, npairs), dim3(1024), lds, stream, p, tw256, twx, Y);
+        }
+        if ((rc = ensure_lds(k_fs2w_1d<0>, lds))) return rc;
+        hipLaunchKernelGGL((k_fs2w_1d<0>), dim3(5, npairs), dim3(1024), lds, stream, p, tw256, Y);
+      }
+      {
+        ProfScope ps(this, "precond");
+        launch_thomas_1d(p);
+      }
+      {
+        ProfScope ps(this, "update");
+        if ((rc = ensure_lds(k_fs1w_1d<1, 1>, lds))) return rc;
+        hipLaunchKernelGGL((k_fs1w_1d<1, 1>), dim3(4, npairs), dim3(1024), lds, stream, p, tw256, twx, Y);
+        if ((rc = ensure_lds(k_fs2w_1d<1>, lds))) return rc;
+        hipLaunchKernelGGL((k_fs2w_1d<1>), dim3(5, npairs), dim3(1024), lds, stream, p, tw256, Y);
+      }
+      hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, p.partials, 5 * npairs, row0_sq, p.ctrl);
       HIP_TRY(hipGetLastError());
     }
     return PDHG_OK;
@@ -1754,6 +1794,7 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
     else if (k == "fourstep") *value = im.fourstep ? 1 : 0;
     else if (k == "glb_line") *value = im.glb_line ? 1 : 0;
     else if (k == "thomas_chunk") *value = im.thomas_chunk ? 1 : 0;
+    else if (k == "fs_wide") *value = (im.fourstep && im.fs_wide) ? 1 : 0;
     else if (k == "rows_rw") *value = im.fast_rows ? im.RWf : 0;   // rows per fast row-kernel workgroup
     // threads of the fast row kernels as launched (ny = 4096: 512 instead of 1024 per half_nt)
     else if (k == "res_threads") *value = im.fast_rows ? ((im.NTf == 1024 && im.RWf == 8 && (im.half_nt & 1) &&

@@ -10,8 +10,11 @@ import sys
 
 
 def short(name):
-    name = re.sub(r"\(.*", "", name)
-    for k in ("k_res_fwdy_fast_2d", "k_invy_update_fast_2d", "k_precond_xt_fast_2d", "k_dual_fast_2d", "k_res_fwdy_2d", "k_precond_xt_2d", "k_invy_update_2d", "k_dual_2d", "k_res_fwdx_1d", "k_thomas_1d",
+    name = re.sub(r"\(.*", "", name).replace("void pdhg::", "")
+    for k in ("k_res_fwdy_fused_2d", "k_res_fwdy_fast_2d", "k_invy_update_fast_2d", "k_precond_xt_batch_2d",
+              "k_precond_xt_ws_2d", "k_precond_xt_fast_2d", "k_precond_x_t1_2d", "k_dual_lds_2d", "k_dual_fast_2d",
+              "k_res_fwdy_2d", "k_precond_xt_2d", "k_invy_update_2d", "k_dual_2d", "k_res_fwdx_1d",
+              "k_thomas_chunk_1d", "k_thomas_1d", "k_fs1_1d<0", "k_fs1_1d<1", "k_fs2_1d<0", "k_fs2_1d<1",
               "k_invx_update_1d", "k_dual_1d", "k_finalize_primal", "k_finalize_dual", "k_finalize_outer",
               "k_outer_sums", "k_bcast_rows", "k_fill"):
         if k in name:

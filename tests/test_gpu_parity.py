@@ -393,7 +393,8 @@ def test_precond_1d_parameters(native, case, prec, cpc):
     <= 1e-10 (x10 at 65536 points, see _big); fp32 from the seeded state: phi' <= max(1e-6, 4 e32) and
     U <= max(5e-4, 4 e32), e32 = distance of the oracle run in float32 from the float64 one (with Ct = 0 at
     65536 points U = R/(C - lam)^pow recovers the low modes of a residual dominated by high ones: the
-    float32 oracle itself is 1e-5 off in phi' there)."""
+    float32 oracle itself is 1e-5 off in phi' there); the 3 iterations likewise against the float32
+    oracle's distance from the float64 one."""
     C, pw, Ct = cpc
     P = make_problem(*case)
     primal, dual = oracle_fns(P, C=C, pow=pw, Ct=Ct)
@@ -426,7 +427,22 @@ def test_precond_1d_parameters(native, case, prec, cpc):
         st = ctx.iterate(3, TAU, SIGMA, -1.0, 1)
         assert st["iters_run"] == 3
         phi_d, rho_d, _ = ctx.get_state()
-        tol = 1e-10 * _big(P) if prec == "fp64" else 1e-5
-        assert rel(phi_d, phi) < tol and rel(rho_d, rho) < (tol if prec == "fp64" else 2e-4)
+        if prec == "fp64":
+            tol = 1e-10 * _big(P)
+            assert rel(phi_d, phi) < tol and rel(rho_d, rho) < tol
+        else:   # the same 3 iterations of the oracle in float32 calibrate the fp32 bound
+            f = np.float32
+            p32, r32, a32 = P["phi"].astype(f), P["rho"].astype(f), tuple(a.astype(f) for a in P["alp"])
+            for _ in range(3):
+                pn = primal(p32, r32, 70.0, a32, TAU, P["dt"], P["dsp"], P["fns"], P["fv"], P["epsl"],
+                            P["x_arr"].astype(f), None)
+                r32, a32 = dual(2 * pn - p32, r32, 70.0, a32, SIGMA, P["dt"], P["dsp"], P["epsl"], P["fns"],
+                                P["x_arr"].astype(f), None, 1, -1.0)
+                p32 = pn
+            e_phi, e_rho = rel(p32, phi), rel(r32, rho)
+            # x8: with Ct = 0 at 65536 points the device's 65536-point four-step DHT (twiddled fp32 passes)
+            # rounds deeper than the oracle's float32 FFT and the decoupled low modes amplify it (measured 3.6-4.4x)
+            assert rel(phi_d, phi) < max(1e-5, 8 * e_phi), (rel(phi_d, phi), e_phi)
+            assert rel(rho_d, rho) < max(2e-4, 8 * e_rho), (rel(rho_d, rho), e_rho)
     finally:
         ctx.close()
