@@ -6,40 +6,53 @@
 namespace pdhg {
 
 // Fixed-order reduction of nrows partial rows (ns sums each) into out[0..ns).
-// Each thread reads whole partial rows (one pass over the rows for all ns sums), then every sum is
-// reduced across the wave (shuffles, fixed order) and across the waves (LDS, fixed order).  Call with
-// blockDim.x a multiple of 64, at most 1024 (the finalize kernels run one 1024-thread block, so 16
-// waves keep row loads in flight); out is visible to every thread on return.
+// The table is read as a flat array of double2: thread i accumulates column pair i % 8 of rows i/8,
+// i/8 + blockDim/8, ... (every load instruction of a wave reads 1 KiB of consecutive rows, 8 of them in
+// flight per thread), then the 8 threads of each column pair are reduced across the wave (shuffles) and
+// across the waves (LDS), both in fixed order.  Call with blockDim.x a multiple of 64, at most 1024 (the
+// finalize kernels run one 1024-thread block); out is visible to every thread on return.
 __device__ void reduce_partials(const double* __restrict__ partials, int nrows, int ns, double* out) {
-  __shared__ double red[kNumSums][16];
-  double acc[kNumSums];
-#pragma unroll
-  for (int s = 0; s < kNumSums; ++s) acc[s] = 0.0;
-  for (int r = threadIdx.x; r < nrows; r += blockDim.x) {   // rows are kNumSums doubles, 16-B aligned
-    const double2* row = reinterpret_cast<const double2*>(partials + (size_t)r * kNumSums);
-#pragma unroll
-    for (int s2 = 0; s2 < kNumSums / 2; ++s2)
-      if (2 * s2 < ns) {
-        const double2 v = row[s2];
-        acc[2 * s2] += v.x;
-        acc[2 * s2 + 1] += v.y;   // entries >= ns are never written out
-      }
+  static_assert(kNumSums == 16, "rows of 8 double2");
+  __shared__ double red[16][kNumSums];
+  const int c = threadIdx.x & 7;
+  const int rstep = blockDim.x >> 3;
+  const double2* P = reinterpret_cast<const double2*>(partials);
+  double ax = 0.0, ay = 0.0;
+  if (2 * c < ns) {   // entries >= ns are never written out
+#pragma unroll 8
+    for (int r = threadIdx.x >> 3; r < nrows; r += rstep) {
+      const double2 v = P[(size_t)r * 8 + c];
+      ax += v.x;
+      ay += v.y;
+    }
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
 #pragma unroll
-  for (int s = 0; s < kNumSums; ++s) {
-    double v = acc[s];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
-    if (lane == 0) red[s][w] = v;
+  for (int o = 32; o >= 8; o >>= 1) {
+    ax += __shfl_down(ax, o, 64);
+    ay += __shfl_down(ay, o, 64);
+  }
+  if (lane < 8) {
+    red[w][2 * lane] = ax;
+    red[w][2 * lane + 1] = ay;
   }
   __syncthreads();
   if ((int)threadIdx.x < ns) {
     double t = 0.0;
-    for (int i = 0; i < nw; ++i) t += red[threadIdx.x][i];
+    for (int i = 0; i < nw; ++i) t += red[i][threadIdx.x];
     out[threadIdx.x] = t;
   }
   __syncthreads();
+}
+
+// First level of a two-level fold for long partial tables: workgroup b reduces rows [b chunk, (b+1) chunk)
+// into row b of out (fixed order, as reduce_partials); the finalize kernels then read gridDim.x rows.
+__global__ void __launch_bounds__(1024) k_fold_partials(const double* __restrict__ partials, int nrows, int ns,
+                                                       int chunk, double* __restrict__ out) {
+  __shared__ double o[kNumSums];
+  const int r0 = blockIdx.x * chunk;
+  reduce_partials(partials + (size_t)r0 * kNumSums, max(0, min(chunk, nrows - r0)), ns, o);
+  if ((int)threadIdx.x < ns) out[(size_t)blockIdx.x * kNumSums + threadIdx.x] = o[threadIdx.x];
 }
 
 // After the primal update: err1 sums (utils_pdhg_solver.py:58).  row0_sq = sum phi_0^2

@@ -1,0 +1,285 @@
+// 65536-point DHT of row pairs as 16 x 4096 (fp32, nx = 65536: C1, BASELINE configs[1]) with a permuted
+// spectrum.
+//
+// Same preconditioner as the four-step kernels (H1_precond_1d, utils_precond.py:105-140: DHT_x of the
+// residual rows, the t-solve per mode, the inverse DHT, phi update), with a split chosen for HBM streaming:
+// x = 4096 n1 + n2, k = k1 + 16 k2.
+//   forward  (decimation in frequency)  A: per column n2, a 16-point DFT over n1 (registers only: every
+//            load / store of a wave is 64 consecutive columns), times W_65536^{n2 k1}, to Y[k1][n2];
+//            B: per chunk k1, a 4096-point FFT over n2 in LDS, then the Hartley unpack of the row pair.
+//   inverse  (decimation in time)       B': per chunk k1 of the spectrum, a 4096-point FFT;
+//            A': per column n2, W_65536^{n2 k1} times the chunk values, a 16-point DFT over k1, the Hartley
+//            unpack, phi' = phi + tau/nx U, phi_bar = 2 phi' - phi and the err1 sums.
+// The spectrum in p.work is stored chunk-major, mode k = k1 + 16 k2 at position k1 4096 + k2: the t-solve is
+// per mode and reads d0 through the same permutation (the host uploads d0 permuted), so no transpose is ever
+// made, and the forward leaves / the inverse takes exactly that order.  The Hartley partner of k is
+// N - k = (16 - k1) + 16 (4095 - k2) (chunk 16 - k1, reversed) for k1 != 0 and chunk 0 reversed mod 4096 for
+// k1 = 0; of x = 4096 n1 + n2 it is 4096 (15 - n1) + 4096 - n2 (column 4096 - n2) for n2 != 0.
+// HBM per iteration: A reads the residual inputs and writes Y (8 B/point), B reads Y and writes the spectrum
+// rows, B' / A' the same the other way round; every access is a whole 128-B line.
+#pragma once
+#include "kernels_fs_wide.hpp"
+
+namespace pdhg {
+
+constexpr int kF16N2 = 4096;
+constexpr int kF16Line = Pad<kF16N2>::LINE;
+
+// Hartley values of rows a, b at k and N - k from Z_k = z, Z_{N-k} = w (fft_lds.hpp header)
+struct HPair {
+  float ha, hb, ma, mb;
+};
+__device__ __forceinline__ HPair hunpack(float2 z, float2 w) {
+  HPair h;
+  h.ha = 0.5f * ((z.x + w.x) - (z.y - w.y));
+  h.hb = 0.5f * ((z.y + w.y) - (w.x - z.x));
+  h.ma = 0.5f * ((w.x + z.x) - (w.y - z.y));
+  h.mb = 0.5f * ((w.y + z.y) - (z.x - w.x));
+  return h;
+}
+
+// Stage A (forward).  grid (4096/256, pairs); block 256: thread = column n2; 16 residual values per row,
+// formed in groups of G rows n1 (a scheduling barrier between groups bounds the loads the compiler hoists).
+// The x -+ 1 neighbours come from the neighbouring lanes (DPP); the values beyond the wave's 64 columns for
+// all 16 rows n1 are fetched by ONE load per array (lane l < 16: column cw - 1 of row n1 = l, lane 16 + l:
+// column cw + 64) and picked per row with readlane.
+template <int EGNO, int G = 16>
+__global__ void __launch_bounds__(256, G == 16 ? 1 : 4) k_f16a_fwd_1d(KP<float> p, const float2* __restrict__ twN,
+                                                     float2* __restrict__ Y) {
+  using C = float2;
+  if (p.ctrl->done) return;
+  const int nx = p.nx, T = p.T;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63, cw = c - lane;   // first column of this wave
+  const int pair = blockIdx.y, j = 2 * pair;
+  const bool has2 = (j + 1) < T;
+  const int cur = p.ctrl->cur;
+  const float* rho = p.rho[cur];
+  const float* a1 = p.alp[cur][0];
+  const float* a2 = p.alp[cur][1];
+  const int j1c = has2 ? j + 1 : j, j2 = min(j + 2, T - 1);
+  const size_t o0 = (size_t)j * nx, o1 = (size_t)j1c * nx;
+  const float* r_j = rho + o0;
+  const float* r_j1 = rho + o1;
+  const float* r_j2 = rho + (size_t)j2 * nx;
+  const int ex = (kF16N2 * (lane & 15) + cw + ((lane & 16) ? 64 : -1)) & (nx - 1);
+  const float e_ax = p.ax[ex], e_r0 = r_j[ex], e_r1 = r_j1[ex];
+  const float e_b10 = a1[o0 + ex], e_b20 = a2[o0 + ex], e_b11 = a1[o1 + ex], e_b21 = a2[o1 + ex];
+  auto edge = [](float v, int l) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l)); };
+  C v[16];
+  int cl = c;   // laundered at every group: the group's addresses are formed there, not hoisted to the top
+#pragma unroll
+  for (int n1 = 0; n1 < 16; ++n1) {
+    if (n1 % G == 0) {
+      if (n1 > 0) __builtin_amdgcn_sched_barrier(0);
+      cl = c;
+      asm volatile("" : "+v"(cl));
+    }
+    const int x = kF16N2 * n1 + cl;
+    const float ac = p.ax[x];
+    const float am = lane_from_prev(ac, edge(e_ax, n1)), ap = lane_from_next(ac, edge(e_ax, 16 + n1));
+    // every load unconditional (rows clamped into [0, T)), the missing row's terms selected away
+    const float c0 = r_j[x], c1 = r_j1[x], c2 = r_j2[x];
+    const float b10 = a1[o0 + x], b20 = a2[o0 + x], b11 = a1[o1 + x], b21 = a2[o1 + x];
+    const float r0 = res1d<EGNO>(p, c0, lane_from_prev(c0, edge(e_r0, n1)), lane_from_next(c0, edge(e_r0, 16 + n1)),
+                                 has2 ? c1 : 0.f, b10, lane_from_prev(b10, edge(e_b10, n1)), b20,
+                                 lane_from_next(b20, edge(e_b20, 16 + n1)), ac, am, ap, j == T - 1);
+    const float r1 = res1d<EGNO>(p, c1, lane_from_prev(c1, edge(e_r1, n1)), lane_from_next(c1, edge(e_r1, 16 + n1)),
+                                 (j + 2 < T) ? c2 : 0.f, b11, lane_from_prev(b11, edge(e_b11, n1)), b21,
+                                 lane_from_next(b21, edge(e_b21, 16 + n1)), ac, am, ap, j + 1 == T - 1);
+    v[n1] = make_float2(r0, has2 ? r1 : 0.f);
+  }
+  dft_any<C, 16>(v);
+  C w[16];
+  twiddles_from3<C, 16>(w, twN, c);   // W_65536^{c k1}
+  C* Yp = Y + (size_t)pair * nx + c;
+  Yp[0] = v[0];
+#pragma unroll
+  for (int k1 = 1; k1 < 16; ++k1) Yp[(size_t)k1 * kF16N2] = cmul(v[k1], w[k1]);
+}
+
+// Stage B (forward).  grid (8, pairs); block 512; LDS 2 lines of 4096 + TwLds<4096>.
+// Workgroup g transforms chunks {g, 16 - g} (g = 0: the self-partnered chunks {0, 8}) and writes the
+// Hartley rows j, j+1 of both to p.work at chunk-major positions.
+__global__ void __launch_bounds__(512) k_f16b_fwd_1d(KP<float> p, const float2* __restrict__ twN,
+                                                     const float2* __restrict__ Y) {
+  using C = float2;
+  constexpr int NT = 512, L = kF16Line;
+  if (p.ctrl->done) return;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  C* A = reinterpret_cast<C*>(smem_raw);
+  C* twl = A + 2 * L;
+  fill_twlds<C, kF16N2>(twl, twN, 16);   // twN holds W_65536: stride 16 gives W_4096
+  const int nx = p.nx, g = blockIdx.x, pair = blockIdx.y, j = 2 * pair;
+  const bool has2 = (j + 1) < p.T;
+  const int ka = g, kb = (g == 0) ? 8 : 16 - g;
+  const C* Yp = Y + (size_t)pair * nx;
+  const int tid = threadIdx.x;
+#pragma unroll 4
+  for (int i = tid; i < 2 * (kF16N2 / 2); i += NT) {   // two complex per 16-B load
+    const int ln = i >> 11, e = 2 * (i & 2047);
+    const float4 q = *reinterpret_cast<const float4*>(Yp + (size_t)(ln ? kb : ka) * kF16N2 + e);
+    C* d = A + ln * L;
+    d[pix(e)] = make_float2(q.x, q.y);
+    d[pix(e + 1)] = make_float2(q.z, q.w);
+  }
+  lds_sync();
+  lds_fft_inplace_tl<C, kF16N2, 2, NT>(A, twl);
+  float* w0 = p.work + (size_t)j * nx;
+  float* w1 = w0 + nx;
+  if (g == 0) {   // chunk 0: partner (4096 - k2) mod 4096; chunk 8: partner 4095 - k2 (one output each)
+#pragma unroll 2
+    for (int i = tid; i < kF16N2; i += NT) {
+      const HPair h0 = hunpack(A[pix(i)], A[pix((kF16N2 - i) & (kF16N2 - 1))]);
+      const HPair h8 = hunpack(A[L + pix(i)], A[L + pix(kF16N2 - 1 - i)]);
+      w0[i] = h0.ha;
+      w0[8 * kF16N2 + i] = h8.ha;
+      if (has2) {
+        w1[i] = h0.hb;
+        w1[8 * kF16N2 + i] = h8.hb;
+      }
+    }
+  } else {        // chunk ka element i pairs with chunk kb element 4095 - i: both outputs
+#pragma unroll 2
+    for (int i = tid; i < kF16N2; i += NT) {
+      const HPair h = hunpack(A[pix(i)], A[L + pix(kF16N2 - 1 - i)]);
+      const int P = ka * kF16N2 + i, Pm = kb * kF16N2 + (kF16N2 - 1 - i);
+      w0[P] = h.ha;
+      w0[Pm] = h.ma;
+      if (has2) {
+        w1[P] = h.hb;
+        w1[Pm] = h.mb;
+      }
+    }
+  }
+}
+
+// Stage B' (inverse).  grid (8, pairs); block 512: chunks {2g, 2g+1} of spectrum rows j, j+1 packed as
+// z = H_j + i H_{j+1}, 4096-point FFT, to Y[k1][n2].
+__global__ void __launch_bounds__(512) k_f16b_inv_1d(KP<float> p, const float2* __restrict__ twN,
+                                                     float2* __restrict__ Y) {
+  using C = float2;
+  constexpr int NT = 512, L = kF16Line;
+  if (p.ctrl->done) return;
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  C* A = reinterpret_cast<C*>(smem_raw);
+  C* twl = A + 2 * L;
+  fill_twlds<C, kF16N2>(twl, twN, 16);
+  const int nx = p.nx, g = blockIdx.x, pair = blockIdx.y, j = 2 * pair;
+  const bool has2 = (j + 1) < p.T;
+  const float* w0 = p.work + (size_t)j * nx + 2 * g * kF16N2;   // chunks 2g, 2g+1 are contiguous
+  const float* w1 = w0 + nx;
+  const int tid = threadIdx.x;
+#pragma unroll 4
+  for (int i = tid; i < 2 * kF16N2 / 4; i += NT) {   // four points per 16-B load of each row
+    const int e = 4 * i;
+    const float4 a = *reinterpret_cast<const float4*>(w0 + e);
+    const float4 b = has2 ? *reinterpret_cast<const float4*>(w1 + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+    C* d = A + (e >> 12) * L;
+    const int el = e & (kF16N2 - 1);
+    d[pix(el)] = make_float2(a.x, b.x);
+    d[pix(el + 1)] = make_float2(a.y, b.y);
+    d[pix(el + 2)] = make_float2(a.z, b.z);
+    d[pix(el + 3)] = make_float2(a.w, b.w);
+  }
+  lds_sync();
+  lds_fft_inplace_tl<C, kF16N2, 2, NT>(A, twl);
+  float2* Yp = Y + (size_t)pair * nx + 2 * g * kF16N2;
+#pragma unroll 4
+  for (int i = tid; i < kF16N2; i += NT) {   // two complex per 16-B store
+    const int e = 2 * i;
+    const C* s = A + (e >> 12) * L;
+    const int el = e & (kF16N2 - 1);
+    const C u0 = s[pix(el)], u1 = s[pix(el + 1)];
+    *reinterpret_cast<float4*>(Yp + e) = make_float4(u0.x, u0.y, u1.x, u1.y);
+  }
+}
+
+// Stage A' (inverse) + primal update.  grid (2048/256, pairs); block 256: thread t owns columns t and
+// 4096 - t (t = 0: the self-partnered columns 0 and 2048).  One partial row of err1 sums per workgroup.
+__global__ void __launch_bounds__(256) k_f16a_inv_1d(KP<float> p, const float2* __restrict__ twN,
+                                                     const float2* __restrict__ Y) {
+  using C = float2;
+  double s[3] = {0.0, 0.0, 0.0};
+  const int row = blockIdx.y * gridDim.x + blockIdx.x;
+  if (p.ctrl->done) {
+    block_reduce_store<3>(s, p.partials, row);
+    return;
+  }
+  const int nx = p.nx, pair = blockIdx.y, j = 2 * pair;
+  const bool has2 = (j + 1) < p.T;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int ca = t, cb = (t == 0) ? kF16N2 / 2 : kF16N2 - t;
+  const C* Yp = Y + (size_t)pair * nx;
+  auto column = [&](int cc, C (&v)[16]) {
+#pragma unroll
+    for (int k1 = 0; k1 < 16; ++k1) v[k1] = Yp[(size_t)k1 * kF16N2 + cc];
+    C w[16];
+    twiddles_from3<C, 16>(w, twN, cc);
+#pragma unroll
+    for (int k1 = 1; k1 < 16; ++k1) v[k1] = cmul(v[k1], w[k1]);
+    dft_any<C, 16>(v);
+  };
+  C fa[16], fb[16];
+  column(ca, fa);
+  column(cb, fb);
+  const float scale = p.tau * p.inv_n;
+  float* phi1 = p.phi + (size_t)(j + 1) * nx;   // phi rows j+1, j+2 (row 0 is the fixed initial condition)
+  float* pb1 = p.phibar + (size_t)(j + 1) * nx;
+  auto upd = [&](float old, float u, float* ph, float* pbar, int n) {
+    const float nw = old + scale * u;
+    ph[n] = nw;
+    pbar[n] = 2.f * nw - old;
+    const double d = (double)nw - (double)old;
+    s[0] += d * d;
+    s[1] += (double)old * (double)old;
+    s[2] += (double)nw * (double)nw;
+  };
+  // 8 x-positions per half: their phi loads are issued together, before any store of the half
+  // (the stores go through the same pointer, so the compiler cannot move later loads above them)
+#pragma unroll
+  for (int h0 = 0; h0 < 16; h0 += 8) {
+    float oa[8][2], ob[8][2];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int n1 = h0 + q;
+      const int na = kF16N2 * n1 + ca, nb = kF16N2 * (15 - n1) + cb;
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const float* ph = phi1 + (size_t)r * nx;
+        const bool live = r == 0 || has2;
+        oa[q][r] = live ? ph[na] : 0.f;
+        ob[q][r] = live ? ph[(t == 0) ? kF16N2 * n1 + cb : nb] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int n1 = h0 + q;
+      HPair ha, hb;
+      int na, nb;
+      if (t != 0) {   // x = 4096 n1 + t pairs with 4096 (15 - n1) + 4096 - t
+        ha = hunpack(fa[n1], fb[15 - n1]);
+        hb.ha = ha.ma;
+        hb.hb = ha.mb;
+        na = kF16N2 * n1 + ca;
+        nb = kF16N2 * (15 - n1) + cb;
+      } else {        // column 0: partner row (16 - n1) mod 16; column 2048: partner row 15 - n1
+        ha = hunpack(fa[n1], fa[(16 - n1) & 15]);
+        const HPair h2 = hunpack(fb[n1], fb[15 - n1]);
+        hb.ha = h2.ha;
+        hb.hb = h2.hb;
+        na = kF16N2 * n1;
+        nb = kF16N2 * n1 + cb;
+      }
+      upd(oa[q][0], ha.ha, phi1, pb1, na);
+      upd(ob[q][0], hb.ha, phi1, pb1, nb);
+      if (has2) {
+        upd(oa[q][1], ha.hb, phi1 + nx, pb1 + nx, na);
+        upd(ob[q][1], hb.hb, phi1 + nx, pb1 + nx, nb);
+      }
+    }
+  }
+  block_reduce_store<3>(s, p.partials, row);
+}
+
+}  // namespace pdhg

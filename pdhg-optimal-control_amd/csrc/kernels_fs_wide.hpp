@@ -72,15 +72,15 @@ template <int EGNO>
 __device__ __forceinline__ float res1d(const KP<float>& p, float r0, float rm, float rp, float rnext, float b1c,
                                        float b1m, float b2c, float b2p, float ac, float am, float ap, bool last) {
   const float eps = 1e-4f;
+  // branch-free (the callers unroll 16 rows): epsl * Dxx is added as the reference does, even for epsl = 0
   float res = (rnext - r0) * p.inv_dt;
-  if (p.epsl != 0.f) res = res + p.epsl * ((rp + rm - 2.f * r0) * p.inv_dx2);
+  res = res + p.epsl * ((rp + rm - 2.f * r0) * p.inv_dx2);
   const float m1c = (r0 + eps) * fpos<float>(fval<float, EGNO>(b1c, ac));
   const float m1m = (rm + eps) * fpos<float>(fval<float, EGNO>(b1m, am));
   const float m2c = (r0 + eps) * fneg<float>(fval<float, EGNO>(b2c, ac));
   const float m2p = (rp + eps) * fneg<float>(fval<float, EGNO>(b2p, ap));
   res = res - ((m1c - m1m) * p.inv_dx + (m2p - m2c) * p.inv_dx);
-  if (last) res = res + p.c_over_dt;
-  return res;
+  return res + (last ? p.c_over_dt : 0.f);
 }
 
 // Stage 1.  grid (256/64, pairs); block 1024 (16 waves: wave w handles n1 rows w, w + 16, ...); LDS 64 lines.

@@ -22,6 +22,7 @@
 #include "kernels_xt_batch.hpp"
 #include "kernels_thomas_chunk.hpp"
 #include "kernels_fs_wide.hpp"
+#include "kernels_fs16.hpp"
 
 using namespace pdhg;
 
@@ -130,10 +131,14 @@ struct Impl : ImplBase {
   int xt_rpre = 0;
   bool thomas_chunk = false;      // 1-D fp32: t-solve in chunks of 32 rows (k_thomas_chunk_1d)
   bool fs_wide = true;            // four-step DHT with 64-column / 32-row tiles (k_fs1w_1d / k_fs2w_1d)
+  int f16_group = 16;             // rows n1 per load group of k_f16a_fwd_1d (PDHG_F16_GROUP: 4, 8, 16; 16 measured best)
+  bool fs16 = false;              // 16 x 4096 split with a chunk-major spectrum (kernels_fs16.hpp)
   size_t lds_fast_xt = 0;
   int RWf = 8, NTf = 1024, g_fast_upd = 1;
   size_t lds_fast = 0, lds_fast_tw = 0;
   size_t partial_rows = 0;
+  static constexpr int kFoldRows = 64;   // rows of the first fold level (k_fold_partials) after the table
+  double* fold_out = nullptr;
   bool primal_done = false;
   int stop_conv = 1, stop_nan = 1;   // reference stop rules (utils_pdhg_solver.py:74-80)
   // profiling
@@ -352,6 +357,9 @@ struct Impl : ImplBase {
         fourstep = sizeof(R) == 4 && nx == 65536;
         if (const char* e = getenv("PDHG_FOURSTEP")) fourstep = fourstep && atoi(e) != 0;   // tuning override
         if (const char* e = getenv("PDHG_FS_WIDE")) fs_wide = atoi(e) != 0;                 // tuning override
+        fs16 = fourstep;
+        if (const char* e = getenv("PDHG_FS16")) fs16 = fs16 && atoi(e) != 0;               // tuning override
+        if (const char* e = getenv("PDHG_F16_GROUP")) f16_group = atoi(e);                   // tuning override
       }
       g4 = 1;
       gx5 = (nx + 255) / 256;
@@ -400,7 +408,8 @@ struct Impl : ImplBase {
       for (int a = 0; a < 4; ++a) p.alp[1][a] = p.alp[0][a];
     }
     for (int a = na; a < 4; ++a) p.alp[0][a] = p.alp[1][a] = nullptr;
-    if ((rc = alloc(&p.partials, partial_rows * kNumSums))) return rc;
+    if ((rc = alloc(&p.partials, (partial_rows + kFoldRows) * kNumSums))) return rc;
+    fold_out = p.partials + partial_rows * kNumSums;
     if ((rc = alloc(&p.ctrl, 1))) return rc;
     if (glb_line) {   // 2 lines of nx complex per concurrent workgroup (gx1 >= gx4)
       C* g = nullptr;
@@ -452,6 +461,12 @@ struct Impl : ImplBase {
       }
       lamx[k] = (R)l;
       d0[k] = (R)std::pow(pb.C - l, pb.pow_);   // 1-D thomas_b = (C - fv)^pow, :125-126
+    }
+    if (fs16) {   // chunk-major spectrum of kernels_fs16.hpp: mode k1 + 16 k2 at position 4096 k1 + k2
+      std::vector<R> d0p(nxg);
+      for (int k1 = 0; k1 < 16; ++k1)
+        for (int k2 = 0; k2 < kF16N2; ++k2) d0p[(size_t)k1 * kF16N2 + k2] = d0[k1 + 16 * k2];
+      d0.swap(d0p);
     }
     if (dct_x) {
       dctw.resize(nxg);
@@ -908,6 +923,7 @@ struct Impl : ImplBase {
   // 1-D primal with the four-step DHT (nx = 65536, fp32): residual + DHT, Thomas, inverse DHT + update
   int launch_fourstep_1d(const KP<R>& p) {
     if constexpr (sizeof(R) == 4) {
+      if (fs16) return launch_fs16_1d(p);
       if (fs_wide) return launch_fourstep_wide_1d(p);
       constexpr int kFsNT = 1024;   // 16 waves: the load / unpack loops keep more rows in flight
       const int npairs = (pb.T + 1) / 2;
@@ -979,6 +995,44 @@ struct Impl : ImplBase {
     return PDHG_OK;
   }
 
+  // the same as 16 x 4096 with a chunk-major spectrum (kernels_fs16.hpp): 16 + 8 workgroups per row pair
+  // forward, 8 + 8 inverse
+  int launch_fs16_1d(const KP<R>& p) {
+    if constexpr (sizeof(R) == 4) {
+      const int npairs = (pb.T + 1) / 2;
+      const size_t ldsb = (size_t)(2 * kF16Line + twlds_size(kF16N2)) * sizeof(C);
+      float2* Y = reinterpret_cast<float2*>(p.gscr);
+      int rc;
+      {
+        ProfScope ps(this, "residual");
+        const dim3 ga(kF16N2 / 256, npairs);
+        auto fwd = [&](auto eg) {
+          constexpr int E = decltype(eg)::value;
+          if (f16_group == 4) hipLaunchKernelGGL((k_f16a_fwd_1d<E, 4>), ga, dim3(256), 0, stream, p, twx, Y);
+          else if (f16_group == 8) hipLaunchKernelGGL((k_f16a_fwd_1d<E, 8>), ga, dim3(256), 0, stream, p, twx, Y);
+          else hipLaunchKernelGGL((k_f16a_fwd_1d<E, 16>), ga, dim3(256), 0, stream, p, twx, Y);
+        };
+        if (pb.egno == 1) fwd(std::integral_constant<int, 1>{});
+        else fwd(std::integral_constant<int, 2>{});
+        if ((rc = ensure_lds(k_f16b_fwd_1d, ldsb))) return rc;
+        hipLaunchKernelGGL(k_f16b_fwd_1d, dim3(8, npairs), dim3(512), ldsb, stream, p, twx, Y);
+      }
+      {
+        ProfScope ps(this, "precond");
+        launch_thomas_1d(p);
+      }
+      {
+        ProfScope ps(this, "update");
+        if ((rc = ensure_lds(k_f16b_inv_1d, ldsb))) return rc;
+        hipLaunchKernelGGL(k_f16b_inv_1d, dim3(8, npairs), dim3(512), ldsb, stream, p, twx, Y);
+        hipLaunchKernelGGL(k_f16a_inv_1d, dim3(kF16N2 / 2 / 256, npairs), dim3(256), 0, stream, p, twx, Y);
+      }
+      hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, p.partials, 8 * npairs, row0_sq, p.ctrl);
+      HIP_TRY(hipGetLastError());
+    }
+    return PDHG_OK;
+  }
+
   // fast dual over time rows [lo, hi); its partials start at block row zbase.  Returns the z extent.
   template <int EGNO>
   void launch_dual_fast_e(const KP<R>& p, int lo, int hi, int gz, int zbase) {
@@ -1037,8 +1091,16 @@ struct Impl : ImplBase {
         }
       }
       const int nrows_d = (pb.ndim == 2 && fast_dual) ? gxd * gyd * gzd : gx5 * g5;
-      hipLaunchKernelGGL(k_finalize_dual, dim3(1), dim3(1024), 0, stream, p.partials, nrows_d, na, n_dead, eps, s,
-                         p.ctrl);
+      const double* rows = p.partials;
+      int nrows = nrows_d;
+      if (nrows_d > 2 * kFoldRows * 16) {   // one workgroup reading ~1 MiB of rows took 45-65 us at C1 / C3
+        const int chunk = (nrows_d + kFoldRows - 1) / kFoldRows;
+        hipLaunchKernelGGL(k_fold_partials, dim3(kFoldRows), dim3(1024), 0, stream, p.partials, nrows_d, 3 + 3 * na,
+                           chunk, fold_out);
+        rows = fold_out;
+        nrows = kFoldRows;
+      }
+      hipLaunchKernelGGL(k_finalize_dual, dim3(1), dim3(1024), 0, stream, rows, nrows, na, n_dead, eps, s, p.ctrl);
     }
     HIP_TRY(hipGetLastError());
     return PDHG_OK;
@@ -1794,7 +1856,8 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
     else if (k == "fourstep") *value = im.fourstep ? 1 : 0;
     else if (k == "glb_line") *value = im.glb_line ? 1 : 0;
     else if (k == "thomas_chunk") *value = im.thomas_chunk ? 1 : 0;
-    else if (k == "fs_wide") *value = (im.fourstep && im.fs_wide) ? 1 : 0;
+    else if (k == "fs_wide") *value = (im.fourstep && im.fs_wide && !im.fs16) ? 1 : 0;
+    else if (k == "fs16") *value = im.fs16 ? 1 : 0;
     else if (k == "rows_rw") *value = im.fast_rows ? im.RWf : 0;   // rows per fast row-kernel workgroup
     // threads of the fast row kernels as launched (ny = 4096: 512 instead of 1024 per half_nt)
     else if (k == "res_threads") *value = im.fast_rows ? ((im.NTf == 1024 && im.RWf == 8 && (im.half_nt & 1) &&

@@ -61,9 +61,10 @@ CASES = {
                                                 "upd_threads": 512}),
     "c4_halfreal_x8192": ({"PDHG_FUSE_RES": "0"}, {"fast_xt": 2, "half_real": 1, "fused_residual": 0}),
     "c4_rows_ny8192": ({}, {"rows_rw": 4, "fused_residual": 0, "res_threads": 1024, "upd_threads": 1024}),
-    "c1_exact": ({}, {"fourstep": 1, "glb_line": 1, "thomas_chunk": 1, "fs_wide": 1}),
-    "c1_exact@fs16": ({"PDHG_FS_WIDE": "0"}, {"fourstep": 1, "fs_wide": 0}),
-    "c1_exact@thomas1": ({"PDHG_THOMAS_CHUNK": "0"}, {"fourstep": 1, "thomas_chunk": 0}),
+    "c1_exact": ({}, {"fourstep": 1, "glb_line": 1, "thomas_chunk": 1, "fs16": 1, "fs_wide": 0}),
+    "c1_exact@wide": ({"PDHG_FS16": "0"}, {"fourstep": 1, "fs16": 0, "fs_wide": 1}),
+    "c1_exact@tile16": ({"PDHG_FS16": "0", "PDHG_FS_WIDE": "0"}, {"fourstep": 1, "fs16": 0, "fs_wide": 0}),
+    "c1_exact@thomas1": ({"PDHG_THOMAS_CHUNK": "0"}, {"fourstep": 1, "fs16": 1, "thomas_chunk": 0}),
     # the row-batched x transform (k_precond_xt_batch_2d) on the same fixtures
     "c3_ws_T200@batch": ({"PDHG_XT_BATCH": "1"}, {"fast_xt": 3}),
     "c3_fr_4096x256@batch": ({"PDHG_FUSE_RES": "1", "PDHG_XT_BATCH": "1"}, {"fast_xt": 3, "fused_residual": 1}),
