@@ -20,9 +20,10 @@ namespace pdhg {
 // One in-place radix-R pass of the padded line-major schedule (as inplace_pass with REG twiddle seeds), with
 // each twiddle applied as soon as it is formed: the seeds W^k, W^4k, W^8k and at most W^1..W^7 are live at
 // once instead of all fifteen products, which keeps the batched kernel within 128 VGPRs.
+// t: the thread index (a caller in a loop passes a laundered copy so the pass's LDS addresses are not
+// hoisted out of the loop as loop-invariant registers)
 template <typename C, int N, int NLT, int NT, int LS, int R>
-__device__ __forceinline__ void batch_pass(C* __restrict__ a, const C* twl) {
-  const int t = threadIdx.x;
+__device__ __forceinline__ void batch_pass(C* __restrict__ a, const C* twl, int t = threadIdx.x) {
   constexpr int nR = N / R;
   constexpr int total = nR * NLT;
   constexpr int PER = (total + NT - 1) / NT;
@@ -88,25 +89,27 @@ __device__ __forceinline__ void batch_pass(C* __restrict__ a, const C* twl) {
 }
 
 template <typename C, int N, int NLT, int NT, int LS>
-__device__ __forceinline__ void batch_fft(C* a, const C* twl) {
+__device__ __forceinline__ void batch_fft(C* a, const C* twl, int t = threadIdx.x) {
   if constexpr (LS < N) {
     constexpr int rem = N / LS;
     constexpr int R = (rem >= 16) ? 16 : rem;
-    batch_pass<C, N, NLT, NT, LS, R>(a, twl);
-    batch_fft<C, N, NLT, NT, LS * R>(a, twl);
+    batch_pass<C, N, NLT, NT, LS, R>(a, twl, t);
+    batch_fft<C, N, NLT, NT, LS * R>(a, twl, t);
   }
 }
 
-template <int N, int NL, int RB = 4, int RPRE = 0>
-__global__ void __launch_bounds__(1024) k_precond_xt_batch_2d(KP<float> p, const float2* __restrict__ twx) {
+// NT = 512, RB = 2: half the LDS (76 KiB) and threads, so two workgroups share a CU and one's transform
+// overlaps the other's row traffic; each thread then owns IT = 8 items.
+template <int N, int NL, int RB = 4, int RPRE = 0, int NT = 1024>
+__global__ void __launch_bounds__(NT, NT == 1024 ? 1 : 4) k_precond_xt_batch_2d(KP<float> p,
+                                                                                const float2* __restrict__ twx) {
   using C = float2;
-  constexpr int NT = 1024;
   constexpr int NI = N * NL;             // items per block
   constexpr int IT = NI / NT;            // items per thread
   constexpr int B = 2 * NL;
   constexpr int LINE = Pad<N>::LINE;
   constexpr int lnl = (NL == 1) ? 0 : (NL == 2) ? 1 : (NL == 4) ? 2 : 3;
-  static_assert(NI == 4096 && IT == 4, "sized for 4096 items per block");
+  static_assert(NI == 4096 && (IT == 4 || IT == 8), "sized for 4096 items per block");
   if (p.ctrl->done) return;
   extern __shared__ __align__(16) unsigned char smem_raw[];
   C* A = reinterpret_cast<C*>(smem_raw);          // RB*NL lines: row r, line l at (r*NL + l) * LINE

@@ -20,6 +20,7 @@
 #include "kernels_common.hpp"
 #include "kernels_xslab.hpp"
 #include "kernels_xt_batch.hpp"
+#include "kernels_xt_dma.hpp"
 #include "kernels_thomas_chunk.hpp"
 #include "kernels_fs_wide.hpp"
 #include "kernels_fs16.hpp"
@@ -129,6 +130,8 @@ struct Impl : ImplBase {
   bool batch_xt = false;          // row-batched variant (k_precond_xt_batch_2d: 4 rows per transform, 1024 threads)
   size_t lds_batch_xt = 0;
   int xt_rpre = 0;
+  bool xt_pair = false;           // batched x transform as 2 rows x 512 threads, two workgroups per CU
+  bool xt_dma = false;            // x transform with the rows staged HBM -> LDS by DMA (k_precond_xt_dma_2d)
   bool thomas_chunk = false;      // 1-D fp32: t-solve in chunks of 32 rows (k_thomas_chunk_1d)
   bool fs_wide = true;            // four-step DHT with 64-column / 32-row tiles (k_fs1w_1d / k_fs2w_1d)
   int f16_group = 16;             // rows n1 per load group of k_f16a_fwd_1d (PDHG_F16_GROUP: 4, 8, 16; 16 measured best)
@@ -285,6 +288,10 @@ struct Impl : ImplBase {
         batch_xt = (nxg == 4096 || nxg == 2048) && T >= 4;
         if (const char* e = getenv("PDHG_XT_BATCH")) batch_xt = atoi(e) != 0;   // tuning override
         if (const char* e = getenv("PDHG_XT_RPRE")) xt_rpre = atoi(e);           // tuning: rows prefetched across the FFT
+        if (const char* e = getenv("PDHG_XT_PAIR")) xt_pair = atoi(e) != 0;      // tuning: 2 rows x 512 threads
+        // LDS-DMA staged rows (k_precond_xt_dma_2d) at nx = 4096: C3 14.24 -> 13.52 ms
+        xt_dma = nxg == 4096;
+        if (const char* e = getenv("PDHG_XT_DMA")) xt_dma = atoi(e) != 0 && nxg == 4096;   // tuning override
         lds_batch_xt = (size_t)(4 * (4096 + 4096 / 16) + twlds_size(nxg)) * sizeof(C);
         // padded FFT buffer + theta, E, b' (float2 per item) + twiddle seeds (TwLds<nx>)
         lds_fast_xt = ws_xt ? (size_t)(2 * (4096 + 4096 / 16) + 816) * sizeof(C)
@@ -778,9 +785,19 @@ struct Impl : ImplBase {
             hipLaunchKernelGGL(kern, g, dim3(1024), lds_batch_xt, stream, p, twx);
             return (int)PDHG_OK;
           };
+          auto gob2 = [&](auto kern) -> int {   // RB = 2 rows, 512 threads: two workgroups per CU
+            int r2;
+            const size_t lds = (size_t)(2 * (4096 + 4096 / 16) + twlds_size(p.nx)) * sizeof(C);
+            if ((r2 = ensure_lds(kern, lds))) return r2;
+            hipLaunchKernelGGL(kern, g, dim3(512), lds, stream, p, twx);
+            return (int)PDHG_OK;
+          };
           switch (p.nx) {
             case 4096:
-              if (xt_rpre == 2) rc = gob(k_precond_xt_batch_2d<4096, 1, 4, 2>);
+              if (xt_dma) {   // static LDS (kernels_xt_dma.hpp)
+                hipLaunchKernelGGL(k_precond_xt_dma_2d<4096>, g, dim3(1024), 0, stream, p, twx);
+              } else if (xt_pair) rc = gob2(k_precond_xt_batch_2d<4096, 1, 2, 0, 512>);
+              else if (xt_rpre == 2) rc = gob(k_precond_xt_batch_2d<4096, 1, 4, 2>);
               else rc = gob(k_precond_xt_batch_2d<4096, 1>);
               break;
             case 2048: rc = gob(k_precond_xt_batch_2d<2048, 2>); break;
@@ -1851,7 +1868,8 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
     if (k == "fused_residual") *value = im.fuse_res ? 1 : 0;
     else if (k == "fast_rows") *value = im.fast_rows ? 1 : 0;
     else if (k == "fast_dual") *value = im.fast_dual ? im.dual_rx : -1;
-    else if (k == "fast_xt") *value = im.fast_xt ? (im.batch_xt && !im.half_real ? 3 : im.ws_xt ? 2 : 1) : 0;
+    else if (k == "fast_xt")
+      *value = im.fast_xt ? (im.batch_xt && !im.half_real ? (im.xt_dma && im.pb.nx == 4096 ? 4 : 3) : im.ws_xt ? 2 : 1) : 0;
     else if (k == "half_real") *value = im.half_real ? 1 : 0;
     else if (k == "fourstep") *value = im.fourstep ? 1 : 0;
     else if (k == "glb_line") *value = im.glb_line ? 1 : 0;

@@ -66,8 +66,13 @@ CASES = {
     "c1_exact@tile16": ({"PDHG_FS16": "0", "PDHG_FS_WIDE": "0"}, {"fourstep": 1, "fs16": 0, "fs_wide": 0}),
     "c1_exact@thomas1": ({"PDHG_THOMAS_CHUNK": "0"}, {"fourstep": 1, "fs16": 1, "thomas_chunk": 0}),
     # the row-batched x transform (k_precond_xt_batch_2d) on the same fixtures
-    "c3_ws_T200@batch": ({"PDHG_XT_BATCH": "1"}, {"fast_xt": 3}),
-    "c3_fr_4096x256@batch": ({"PDHG_FUSE_RES": "1", "PDHG_XT_BATCH": "1"}, {"fast_xt": 3, "fused_residual": 1}),
+    "c3_ws_T200@batch": ({"PDHG_XT_BATCH": "1", "PDHG_XT_DMA": "0"}, {"fast_xt": 3}),
+    "c3_fr_4096x256@batch": ({"PDHG_FUSE_RES": "1", "PDHG_XT_BATCH": "1", "PDHG_XT_DMA": "0"},
+                             {"fast_xt": 3, "fused_residual": 1}),
+    # the LDS-DMA staged x transform (k_precond_xt_dma_2d)
+    "c3_ws_T200@dma": ({"PDHG_XT_BATCH": "1", "PDHG_XT_DMA": "1"}, {"fast_xt": 4}),
+    "c3_fr_4096x256@dma": ({"PDHG_FUSE_RES": "1", "PDHG_XT_BATCH": "1", "PDHG_XT_DMA": "1"},
+                           {"fast_xt": 4, "fused_residual": 1}),
     "c2_x2048@batch": ({"PDHG_FUSE_RES": "1", "PDHG_XT_BATCH": "1"}, {"fast_xt": 3, "fused_residual": 1}),
     # the fused residual with 1024 threads (k_res_fwdy_fused_2d<2,4096,8,1024>)
     "c3_rows_ny4096@nt1024": ({"PDHG_FUSE_RES": "1", "PDHG_HALF_NT": "2"}, {"fused_residual": 1, "res_threads": 1024}),
@@ -161,9 +166,12 @@ ONE_STEP = {
     "rows_ny4096_fr": (2, 64, 4096, 4, {"PDHG_FUSE_RES": "1"}, {"fused_residual": 1, "res_threads": 512}),
     "halfreal_x8192": (2, 8192, 16, 4, {}, {"fast_xt": 2, "half_real": 1}),
     "rows_ny8192": (2, 64, 8192, 4, {}, {"rows_rw": 4}),
-    "batch_fr_4096x256": (2, 4096, 256, 8, {"PDHG_XT_BATCH": "1", "PDHG_FUSE_RES": "1"},
+    "batch_fr_4096x256": (2, 4096, 256, 8, {"PDHG_XT_BATCH": "1", "PDHG_XT_DMA": "0", "PDHG_FUSE_RES": "1"},
                           {"fast_xt": 3, "fused_residual": 1}),
     "batch_x2048_T6": (1, 2048, 256, 6, {"PDHG_XT_BATCH": "1"}, {"fast_xt": 3}),   # partial last batch
+    "dma_fr_4096x256": (2, 4096, 256, 8, {"PDHG_XT_BATCH": "1", "PDHG_XT_DMA": "1", "PDHG_FUSE_RES": "1"},
+                        {"fast_xt": 4, "fused_residual": 1}),
+    "dma_4096_T7": (1, 4096, 256, 7, {"PDHG_XT_BATCH": "1", "PDHG_XT_DMA": "1"}, {"fast_xt": 4}),   # odd T
 }
 
 
@@ -175,9 +183,30 @@ def test_batched_x_transform_matches_ws(native, monkeypatch, nx, T):
     out = []
     for batch in ("0", "1"):
         monkeypatch.setenv("PDHG_XT_BATCH", batch)   # 0: warp-specialised (nx = 4096, T >= 16) / single-role
+        monkeypatch.setenv("PDHG_XT_DMA", "0")
         ctx = device_ctx(P, "fp32")
         try:
             assert ctx.path_info("fast_xt") == (3 if batch == "1" else (2 if (nx == 4096 and T >= 16) else 1))
+            ctx.set_state(*_f32_state(P))
+            ctx.iterate(3, TAU, SIGMA, -1.0, 1)
+            out.append(ctx.get_state())
+        finally:
+            ctx.close()
+    assert rel(out[1][0], out[0][0]) < 1e-6 and rel(out[1][1], out[0][1]) < 1e-6
+
+
+@pytest.mark.parametrize("T", [37, 8, 5, 4])
+def test_dma_x_transform_matches_batched(native, monkeypatch, T):
+    """The LDS-DMA staged x transform against the row-batched one on the same state (same arithmetic per mode,
+    2 rows per batch instead of 4: partial batches at both sweep ends for odd T; 3 iterations, fp32 <= 1e-6)."""
+    P = make_problem(2, 2, 4096, 256, T, 0.0, seeded=True)
+    out = []
+    monkeypatch.setenv("PDHG_XT_BATCH", "1")
+    for dma in ("0", "1"):
+        monkeypatch.setenv("PDHG_XT_DMA", dma)
+        ctx = device_ctx(P, "fp32")
+        try:
+            assert ctx.path_info("fast_xt") == (4 if dma == "1" else 3)
             ctx.set_state(*_f32_state(P))
             ctx.iterate(3, TAU, SIGMA, -1.0, 1)
             out.append(ctx.get_state())

@@ -54,7 +54,7 @@ def test_slabs_match_single_context(native, egno, nx, ny, T, nr, k, overlap, exc
     slabs = _slabs(P, nr, k)
     for s in slabs:   # the x kernel the slab runs (see CASES)
         if nx == 4096:
-            assert s.path_info("fast_xt") == (3 if s.T >= 4 else 1), (s.T, s.path_info("fast_xt"))
+            assert s.path_info("fast_xt") == (4 if s.T >= 4 else 1), (s.T, s.path_info("fast_xt"))
     for s, part in zip(slabs, split_state(P["phi"], P["rho"], P["alp"], slab_bounds(T, nr))):
         s.set_state(*part)
     runner = SlabRunner(slabs, LocalComm(nr), overlap=overlap, exchange=exchange)
@@ -76,22 +76,26 @@ def test_slabs_match_single_context(native, egno, nx, ny, T, nr, k, overlap, exc
     ref.close()
 
 
-def test_ws_slabs(native, monkeypatch):
-    """The warp-specialised x transform (PDHG_XT_BATCH=0, slabs of >= 16 rows) through the slab phases (forward
-    sweep, carry fix-up, backward sweep from the right carry) against the single context."""
+@pytest.mark.parametrize("env,path", [({"PDHG_XT_BATCH": "0"}, 2), ({"PDHG_XT_BATCH": "1", "PDHG_XT_DMA": "0"}, 3)],
+                         ids=["ws", "batched"])
+def test_ws_slabs(native, monkeypatch, env, path):
+    """The warp-specialised (PDHG_XT_BATCH=0, slabs of >= 16 rows) and the register-staged batched x transforms
+    through the slab phases (forward sweep, carry fix-up, backward sweep from the right carry) against the
+    single context (the default LDS-DMA kernel runs the CASES above)."""
     import torch
     from pdhg_amd.context import PDHGContext
     from pdhg_amd.slab import LocalComm, SlabRunner, join_state, slab_bounds, split_state
-    monkeypatch.setenv("PDHG_XT_BATCH", "0")
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     P = make_problem(2, 2, 4096, 256, 40, 0.0)
     tau, sigma, n = 0.1 / 1.5, 0.1 * 1.5, 4
     ref = PDHGContext(2, 2, 4096, 256, 40, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"], precision="fp32")
-    assert ref.path_info("fast_xt") == 2
+    assert ref.path_info("fast_xt") == path
     ref.set_state(P["phi"], P["rho"], P["alp"])
     ref.iterate(n, tau, sigma, -1.0, 1)
     phi_r, rho_r, _ = ref.get_state()
     slabs = _slabs(P, 2, 1)
-    assert all(s.path_info("fast_xt") == 2 for s in slabs)
+    assert all(s.path_info("fast_xt") == path for s in slabs)
     for s, part in zip(slabs, split_state(P["phi"], P["rho"], P["alp"], slab_bounds(40, 2))):
         s.set_state(*part)
     SlabRunner(slabs, LocalComm(2)).iterate(n, tau, sigma, -1.0, 1)
