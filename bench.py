@@ -138,22 +138,28 @@ def pmc_traffic(args):
                                     vals.setdefault((cls, ctr), {}).setdefault(r["Kernel_Name"], []).append(
                                         float(r["Counter_Value"]) * 1024.0)
         shutil.rmtree(d, ignore_errors=True)
-    # a class can hold two kernels (the first primal of a fused-residual context forms the residual
-    # unfused): keep the one launched most, i.e. the steady-state kernel the timed region runs
-    vals = {key: max(by_name.values(), key=len) for key, by_name in vals.items()}
+    # a class can hold several kernels: the stages of one launch class (C1's 16 x 4096 transform runs two
+    # kernels per residual and per update, launched equally often: their bytes add up) and a first-iteration
+    # variant (the first primal of a fused-residual context forms the residual unfused: launched less, dropped)
+    def per_launch(by_name):
+        most = max(len(v) for v in by_name.values())
+        return sum(sum(v) / len(v) for v in by_name.values() if len(v) == most)
+    vals = {key: per_launch(by_name) for key, by_name in vals.items()}
     out = {}
     for cls in KERNEL_SYMBOL:
         f, w = vals.get((cls, "FETCH_SIZE")), vals.get((cls, "WRITE_SIZE"))
-        if f and w:
-            fb, wb = 2.0 * sum(f) / len(f), sum(w) / len(w)
+        if f is not None and w is not None:
+            fb, wb = 2.0 * f, w
             out[cls] = {"bytes": fb + wb, "fetch_bytes_x2": fb, "write_bytes": wb}
     return (out, None) if out else (None, "no PMC rows matched")
 
 
 # kernel-name substrings of the four classes (precond: k_precond_xt_* and the one-row k_precond_x_t1_2d,
-# 1-D k_thomas_1d; the 1-D four-step kernels k_fs1/k_fs2 serve both residual and update and are not attributed)
-KERNEL_SYMBOL = {"dual": ("k_dual_",), "residual": ("k_res_fwd",), "precond": ("k_precond_x", "k_thomas_1d"),
-                 "update": ("k_inv",)}
+# 1-D k_thomas_1d / k_thomas_chunk_1d; C1's 16 x 4096 transform: k_f16a/b_fwd_1d form the residual class,
+# k_f16b/a_inv_1d the update class; the older four-step kernels k_fs1/k_fs2 (PDHG_FS16=0) are not attributed)
+KERNEL_SYMBOL = {"dual": ("k_dual_",), "residual": ("k_res_fwd", "k_f16a_fwd", "k_f16b_fwd"),
+                 "precond": ("k_precond_x", "k_thomas_1d", "k_thomas_chunk"),
+                 "update": ("k_inv", "k_f16b_inv", "k_f16a_inv")}
 
 
 def _free_port():
