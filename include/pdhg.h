@@ -251,6 +251,26 @@ int pdhg_xslab_wire(pdhg_ctx* ctx, int stage, void* buf);
 int pdhg_xslab_precond(pdhg_ctx* ctx);                                     /* x-DHT, Thomas, inverse x-DHT */
 int pdhg_xslab_update(pdhg_ctx* ctx, double tau, double* sums);            /* inverse y-DHT + update + sums */
 
+/* ---------------- multi-device context (create over a device list) ----------------
+ * Replaces the single-device pdhg_create of the drop-in for callers that bring no communicator: one host
+ * thread drives ndev t-slab contexts (pdhg_create_slab, one per listed device; a device may repeat) through
+ * the choreography above, with planes moved device to device by hipMemcpyPeerAsync (xGMI) and the stop-test
+ * sums folded in slab order on the first device, so a C / Go / Java caller gets the multi-GPU window without
+ * re-implementing pdhg_amd/slab.py or linking RCCL.  The window's rows [0, p->T) are split near-equally
+ * (the first T % ndev slabs get one more row).  State arrays are the WHOLE window in the reference layouts
+ * (as pdhg_set_state / pdhg_get_state).  Same support as the t-slab: fp32, ndim 2, bc (0,0), power-of-two nx
+ * in [512, 8192].  Keys of pdhg_multi_info: "ndev", "long_modes", "rows:<i>" (rows of slab i). */
+typedef struct pdhg_multi pdhg_multi;
+int pdhg_create_multi(const pdhg_problem* p, const int* devices, int ndev, pdhg_multi** out);
+int pdhg_multi_destroy(pdhg_multi* m);
+int pdhg_multi_set_state(pdhg_multi* m, const double* phi, const double* rho, const double* alp);
+int pdhg_multi_get_state(pdhg_multi* m, double* phi, double* rho, double* alp);
+int pdhg_multi_iterate(pdhg_multi* m, int n_iters, double tau, double sigma, double eps, int rho_alp_iters,
+                       pdhg_stats* out);                          /* utils_pdhg_solver.py:51-88 on all slabs */
+int pdhg_multi_set_stop_rules(pdhg_multi* m, int stop_on_converge, int stop_on_nan);
+int pdhg_multi_synchronize(pdhg_multi* m);
+int pdhg_multi_info(pdhg_multi* m, const char* key, int* value);
+
 #ifdef __cplusplus
 }
 #endif

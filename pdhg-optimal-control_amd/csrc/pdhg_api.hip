@@ -2156,3 +2156,5 @@ int pdhg_slab_update(pdhg_ctx* ctx, double tau, double* sums) {
 }
 
 }  // extern "C"
+
+#include "pdhg_multi.hpp"   // multi-device context over the t-slab entry points above

@@ -34,6 +34,9 @@ EXPORTS = (
     # x-slab decomposition (multi-GPU for T = 1 windows)
     "pdhg_create_xslab", "pdhg_xslab_layout", "pdhg_xslab_sizes", "pdhg_xslab_halo_out", "pdhg_xslab_halo_in",
     "pdhg_xslab_residual", "pdhg_xslab_wire", "pdhg_xslab_precond", "pdhg_xslab_update",
+    # multi-device context (one host thread, t-slabs over a device list)
+    "pdhg_create_multi", "pdhg_multi_destroy", "pdhg_multi_set_state", "pdhg_multi_get_state",
+    "pdhg_multi_iterate", "pdhg_multi_set_stop_rules", "pdhg_multi_synchronize", "pdhg_multi_info",
 )
 
 
@@ -152,6 +155,16 @@ def load():
         "pdhg_xslab_wire": ([P, ctypes.c_int, P], ctypes.c_int),
         "pdhg_xslab_precond": ([P], ctypes.c_int),
         "pdhg_xslab_update": ([P, ctypes.c_double, P], ctypes.c_int),
+        "pdhg_create_multi": ([ctypes.POINTER(pdhg_problem), ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                               ctypes.POINTER(P)], ctypes.c_int),
+        "pdhg_multi_destroy": ([P], ctypes.c_int),
+        "pdhg_multi_set_state": ([P, dp, dp, dp], ctypes.c_int),
+        "pdhg_multi_get_state": ([P, dp, dp, dp], ctypes.c_int),
+        "pdhg_multi_iterate": ([P, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_int,
+                                ctypes.POINTER(pdhg_stats)], ctypes.c_int),
+        "pdhg_multi_set_stop_rules": ([P, ctypes.c_int, ctypes.c_int], ctypes.c_int),
+        "pdhg_multi_synchronize": ([P], ctypes.c_int),
+        "pdhg_multi_info": ([P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
     }
     missing = set(EXPORTS) - set(sig)
     if missing:

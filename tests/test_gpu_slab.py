@@ -13,15 +13,15 @@ pytestmark = pytest.mark.gpu
 
 CASES = [
     # (egno, nx, ny, T, P, k)   the x kernel follows the SLAB's row count (path asserted in the test):
-    # nx = 512: k_precond_xt_fast_2d; nx = 4096: k_precond_xt_batch_2d for slabs of >= 4 rows, else the
+    # nx = 512: k_precond_xt_fast_2d; nx = 4096: k_precond_xt_dma_2d for slabs of >= 4 rows, else the
     # single-role k_precond_xt_fast_2d (k_precond_xt_ws_2d: test_ws_slabs below)
     (1, 512, 256, 6, 2, 1),
     (2, 512, 256, 7, 3, 1),
     (1, 512, 256, 5, 5, 3),
     (2, 4096, 256, 6, 2, 1),     # 3-row slabs: single-role
     (1, 4096, 256, 4, 3, 2),
-    (2, 4096, 256, 50, 2, 1),    # 25-row slabs (C3's slab length on 8 GPUs): batched x transform
-    (2, 4096, 256, 11, 2, 1),    # 6 + 5 rows: batched x transform with partial last batches
+    (2, 4096, 256, 50, 2, 1),    # 25-row slabs (C3's slab length on 8 GPUs): LDS-DMA x transform
+    (2, 4096, 256, 11, 2, 1),    # 6 + 5 rows: LDS-DMA x transform with partial last batches
     (2, 8192, 256, 5, 2, 1),    # half-real x blocks (C4's nx)
     (1, 512, 256, 3, 3, 1),     # one-row slabs: the halo row is the whole slab
     (2, 512, 256, 19, 2, 1),    # residual tiles of 8 rows + untiled remainder rows
