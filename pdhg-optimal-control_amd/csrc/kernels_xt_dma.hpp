@@ -144,7 +144,7 @@ __global__ void __launch_bounds__(1024) k_precond_xt_dma_2d(KP<float> p, const f
     static_assert(RB * nR == NT / 2, "first pass: one butterfly per thread for half the block");
     C v[16];
     // first radix-16 pass, read half: S (unpadded, line r = row r).  512 butterflies: the upper half of the
-    // block repeats the lower half's reads and DFTs (no divergent register state) and skips the writes.
+    // block repeats the lower half's reads (no divergent register state across the barrier), then idles.
     auto pass1_read = [&]() {
       launder();
       const int bt = tl & (NT / 2 - 1);
@@ -154,8 +154,8 @@ __global__ void __launch_bounds__(1024) k_precond_xt_dma_2d(KP<float> p, const f
     auto pass1_write = [&]() {
       const int bt = tl & (NT / 2 - 1);
       const int l = bt / nR, j = bt - l * nR;
-      dft_any<C, 16>(v);
-      if (tl < NT / 2) {
+      if (tl < NT / 2) {   // the upper half only loaded (no divergent state across the barrier)
+        dft_any<C, 16>(v);
         C* d = A + l * LINE + pix(j * 16);
 #pragma unroll
         for (int r = 0; r < 16; ++r) d[r] = v[r];
