@@ -137,6 +137,11 @@ __global__ void __launch_bounds__(RX * 64, FR ? 2 : 3) k_dual_lds_2d(KP<float> p
       float4 rn4, an4[NA];
       float4 m1x4, m2x4;
       float m1y[4], m2y[4];
+      // this step's 4 points summed in fp32 (4 terms), then one fp64 add per sum: the fixed-order fp64
+      // accumulation over t stays, with a quarter of the fp64 work
+      float fs[NS];
+#pragma unroll
+      for (int i = 0; i < NS; ++i) fs[i] = 0.f;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float c = f4(pc, e);
@@ -158,18 +163,21 @@ __global__ void __launch_bounds__(RX * 64, FR ? 2 : 3) k_dual_lds_2d(KP<float> p
         }
 #pragma unroll
         for (int a = 0; a < NA; ++a) f4set(an4[a], e, an[a]);
-        if (!live) continue;
-        const double dr = (double)rn - (double)rho;
-        s[0] += dr * dr;
-        s[1] += (double)rn * (double)rn;
-        s[2] += (double)rho * (double)rho;
+        const float dr = rn - rho;
+        fs[0] = fmaf(dr, dr, fs[0]);
+        fs[1] = fmaf(rn, rn, fs[1]);
+        fs[2] = fmaf(rho, rho, fs[2]);
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
-          const double da = (double)an[a] - (double)ao[a];
-          s[3 + 3 * a] += da * da;
-          s[4 + 3 * a] += (double)an[a] * (double)an[a];
-          s[5 + 3 * a] += (double)ao[a] * (double)ao[a];
+          const float da = an[a] - ao[a];
+          fs[3 + 3 * a] = fmaf(da, da, fs[3 + 3 * a]);
+          fs[4 + 3 * a] = fmaf(an[a], an[a], fs[4 + 3 * a]);
+          fs[5 + 3 * a] = fmaf(ao[a], ao[a], fs[5 + 3 * a]);
         }
+      }
+      if (live) {
+#pragma unroll
+        for (int i = 0; i < NS; ++i) s[i] += (double)fs[i];
       }
       const size_t o = (size_t)j * plane + rxc + y;
       if (live) {
