@@ -481,6 +481,7 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
           if (xr < p.xl0 || xr >= p.xl1) continue;   // x-slab ghost row (workgroup-uniform)
           const size_t idx = (size_t)xr * N + y;
           float4 nw, pb;
+          float fs[3] = {0.f, 0.f, 0.f};   // the 4 points in fp32, then one fp64 add per sum
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const float o = f4(o4[h], e);
@@ -488,10 +489,12 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
             f4set(nw, e, n);
             f4set(pb, e, 2.f * n - o);
             const float d = n - o;
-            s[0] += (double)d * (double)d;
-            s[1] += (double)o * (double)o;
-            s[2] += (double)n * (double)n;
+            fs[0] = fmaf(d, d, fs[0]);
+            fs[1] = fmaf(o, o, fs[1]);
+            fs[2] = fmaf(n, n, fs[2]);
           }
+#pragma unroll
+          for (int i = 0; i < 3; ++i) s[i] += (double)fs[i];
           st4(phi + idx, nw);
           st4(pbar + idx, pb);
         }
