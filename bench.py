@@ -138,19 +138,31 @@ def pmc_traffic(args):
                                     vals.setdefault((cls, ctr), {}).setdefault(r["Kernel_Name"], []).append(
                                         float(r["Counter_Value"]) * 1024.0)
         shutil.rmtree(d, ignore_errors=True)
-    # a class can hold several kernels: the stages of one launch class (C1's 16 x 4096 transform runs two
-    # kernels per residual and per update, launched equally often: their bytes add up) and a first-iteration
-    # variant (the first primal of a fused-residual context forms the residual unfused: launched less, dropped)
-    def per_launch(by_name):
-        most = max(len(v) for v in by_name.values())
-        return sum(sum(v) / len(v) for v in by_name.values() if len(v) == most)
-    vals = {key: per_launch(by_name) for key, by_name in vals.items()}
+    # by kernel name: a class's bytes per launch are the sum over its kernels of each kernel's average (C1's
+    # 16 x 4096 transform runs two kernels per residual / update launch).  The first primal of a fused-residual
+    # context forms its residual unfused (k_res_fwdy_fast_2d, from rho + 4 alp: ~3x the fused kernel's bytes);
+    # with a fused kernel present that one is reported apart as "residual_first" and kept out of "residual".
+    names = {}
+    for (cls, ctr), by_name in vals.items():
+        for name, v in by_name.items():
+            names.setdefault(name, {})[ctr] = (sum(v) / len(v), len(v))
+    split = {}
+    for (cls, ctr), by_name in list(vals.items()):
+        if cls == "residual" and any("fused" in n for n in by_name):
+            split[("residual_first", ctr)] = {n: v for n, v in by_name.items() if "fused" not in n}
+            vals[(cls, ctr)] = {n: v for n, v in by_name.items() if "fused" in n}
+    vals.update(split)
+    vals = {key: sum(sum(v) / len(v) for v in by_name.values()) for key, by_name in vals.items() if by_name}
     out = {}
-    for cls in KERNEL_SYMBOL:
+    for cls in list(KERNEL_SYMBOL) + ["residual_first"]:
         f, w = vals.get((cls, "FETCH_SIZE")), vals.get((cls, "WRITE_SIZE"))
         if f is not None and w is not None:
             fb, wb = 2.0 * f, w
             out[cls] = {"bytes": fb + wb, "fetch_bytes_x2": fb, "write_bytes": wb}
+    if out:
+        out["_by_kernel"] = {n: {"fetch_bytes_x2": 2.0 * c["FETCH_SIZE"][0] if "FETCH_SIZE" in c else None,
+                                 "write_bytes": c["WRITE_SIZE"][0] if "WRITE_SIZE" in c else None,
+                                 "launches": max(x[1] for x in c.values())} for n, c in names.items()}
     return (out, None) if out else (None, "no PMC rows matched")
 
 
@@ -194,6 +206,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--rho-alp-iters", type=int, default=1)
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp64", "mixed"],
+                    help="fp32 (default), fp64 (the reference's arithmetic) or mixed (phi / phi_bar in fp64)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-T", type=int, default=1)
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
@@ -264,7 +278,7 @@ def main():
                           rho_alp_iters=k, device=torch.cuda.current_device())
     else:
         ctx = PDHGContext(egno, ndim, nx, ny, T, 2.0 / nx, 2.0 / ny if ndim == 2 else 0.0, dt, xs, ys, epsl=epsl,
-                          precision="fp32", rho_alp_iters=k, device=0)
+                          precision=args.precision, rho_alp_iters=k, device=0)
     if ndim == 1:
         g = np.sin(np.pi * xs)
     else:
@@ -337,8 +351,11 @@ def main():
     # the timed runs execute exactly the requested iterations (NaN stop off), each from the reference state
     ctx.set_stop_rules(converge=True, nan=False)
 
-    def timed(n):
-        init()
+    def timed(n, fresh):
+        """n iterations bracketed by barrier + synchronize; fresh: from the reference state, else continuing
+        the current state (after the warm-up)."""
+        if fresh:
+            init()
         sync()
         ctx.profile_enable(True)
         barrier()
@@ -356,23 +373,29 @@ def main():
         ctx.profile_enable(False)
         return st, el, kern
 
-    # finite segment: iterations 1..F from the reference state, all before the first non-finite one
+    # finite segment: iterations 2..F from the reference state (the first, untimed, forms its residual from
+    # scratch), all before the first non-finite one
     finite = None
     if not args.no_probe:
         F = 10 if first_nonfinite is None else min(10, first_nonfinite - 1)
-        if F >= 1:
-            st_f, el_f, kern_f = timed(F)
+        if F >= 2:
+            init()
+            run(1)
+            st_f, el_f, kern_f = timed(F - 1, fresh=False)
             el_f = max_over_ranks(el_f)
-            finite = {"iters": F, "ms_per_step": el_f / F * 1e3, "value": F / el_f, "nonfinite": bool(st_f["nan_seen"]),
+            finite = {"iters": "2..{}".format(F), "ms_per_step": el_f / (F - 1) * 1e3, "value": (F - 1) / el_f,
+                      "nonfinite": bool(st_f["nan_seen"]),
                       "kernels_avg_ms": {c: d["avg_ms"] for c, d in kern_f.items()}}
 
+    # the contract's run: W untimed warm-up iterations from the reference state, then exactly K timed
+    # iterations continuing from there (so the first iteration's unfused residual is in the warm-up)
+    init()
     if args.warmup > 0:
-        init()
         run(args.warmup)
     sync()
     if runner is not None:
         runner.timing = True
-    st, el, kern = timed(args.steps)
+    st, el, kern = timed(args.steps, fresh=args.warmup == 0)
     exch = runner.exchange_times() if runner is not None else None
     if runner is not None:
         runner.timing = False
@@ -410,15 +433,18 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if world > 1 else "weak",
         "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic (reference initial state phi=g, rho=70, alp=0; every timed run starts from it)",
+        "dtype": {"fp32": "f32", "fp64": "f64", "mixed": "f32 (phi, phi_bar f64)"}[args.precision],
+        "data": "synthetic: the reference initial state (phi=g, rho=70, alp=0), W warm-up iterations from it, "
+                "then the K timed iterations continuing from there",
         "config": {"workload": "egno{} ndim{} epsl{} nx={} ny={} nt={}: one PDHG window of T={} rows, "
                                "rho_alp_iters={}".format(egno, ndim, epsl, nx, ny, nt, T, k),
                    "parallelism": ("x-slab x{} (halo-row allgathers, two all-to-all spectrum transposes per "
                                    "iteration)".format(world) if xslab else
                                    "t-slab x{} (RCCL point-to-point halos and carries, overlapped)".format(world))
                    if (world > 1 or xslab) else "single GPU",
+                   "precision": args.precision,
                    "iters_executed": iters, "stop_status": st["status"], "state_nonfinite": bool(st["nan_seen"]),
+                   "dual_subiters_mean": (st.get("inner_total", 0) / max(iters, 1)) if k > 1 else 1,
                    "first_nonfinite_iter": first_nonfinite,
                    "nonfinite_probe_iters": probe_n},
         "hbm_gbps_iteration": it_bytes / (ms_per_step * 1e-3) / 1e9,
@@ -444,6 +470,9 @@ def main():
         for cls in kern:
             if cls in pmc:
                 kern[cls]["pmc_bytes_per_launch"] = pmc[cls]["bytes"]
+        if "residual_first" in pmc:   # the unfused residual of a run's first iteration (in the warm-up here)
+            out["kernels_first_iteration"] = {"residual_unfused": {"pmc_bytes_per_launch": pmc["residual_first"]["bytes"]}}
+        out["pmc_by_kernel"] = pmc.get("_by_kernel")
     elif world == 1:
         out["roofline"]["traffic_note"] = pmc_err
     if world == 1 and not args.no_cpu_baseline:

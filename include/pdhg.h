@@ -23,7 +23,10 @@
  * Return convention: every function returns PDHG_OK (0) or a negative
  * pdhg_status; pdhg_last_error() gives the message (thread-local).
  * Threading: a context is single-caller.  It drives one GPU on its own HIP
- * stream; multi-GPU runs use one process per GPU.
+ * stream (every entry point makes the context's device current first).  Multi-GPU:
+ * either one process per GPU with a t-slab / x-slab context each and the caller's
+ * communicator (pdhg_create_slab, pdhg_create_xslab; pdhg_amd/slab.py over RCCL), or
+ * one host thread over a device list (pdhg_create_multi).  See DESIGN.md §7.
  */
 #ifndef PDHG_MI355X_H
 #define PDHG_MI355X_H
@@ -142,7 +145,10 @@ int pdhg_device_bytes(pdhg_ctx* ctx, unsigned long long* bytes);
 /* Which kernel variant a context selected (no reference counterpart; tests and benches assert the fast
  * paths engaged): "fused_residual" 1/0 (the dual sweep forms the next residual, k_dual_lds_2d FR),
  * "fast_rows" 1/0 (fp32 8/4-row y-transform kernels), "fast_dual" (-1 generic, 0 row-per-thread,
- * RX rows through LDS), "fast_xt" (0 generic, 1 single-role, 2 warp-specialised x-transform). */
+ * RX rows through LDS), "fast_xt" (0 generic, 1 single-role, 2 warp-specialised, 3 row-batched,
+ * 4 row-batched with LDS-DMA staging x-transform), "half_real", "fourstep", "fs16", "fs_wide",
+ * "glb_line", "thomas_chunk", "rows_rw", "res_threads", "upd_threads", "phi64" (1: phi / phi_bar held
+ * in fp64, the mixed-precision fp32 path). */
 int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value);
 
 /* Per-launch kernel timing for the benchmark: HIP events recorded on the
@@ -265,11 +271,20 @@ int pdhg_create_multi(const pdhg_problem* p, const int* devices, int ndev, pdhg_
 int pdhg_multi_destroy(pdhg_multi* m);
 int pdhg_multi_set_state(pdhg_multi* m, const double* phi, const double* rho, const double* alp);
 int pdhg_multi_get_state(pdhg_multi* m, double* phi, double* rho, double* alp);
+int pdhg_multi_init_state(pdhg_multi* m, const double* g);        /* pdhg_init_state on every slab */
 int pdhg_multi_iterate(pdhg_multi* m, int n_iters, double tau, double sigma, double eps, int rho_alp_iters,
                        pdhg_stats* out);                          /* utils_pdhg_solver.py:51-88 on all slabs */
 int pdhg_multi_set_stop_rules(pdhg_multi* m, int stop_on_converge, int stop_on_nan);
 int pdhg_multi_synchronize(pdhg_multi* m);
-int pdhg_multi_info(pdhg_multi* m, const char* key, int* value);
+int pdhg_multi_info(pdhg_multi* m, const char* key, int* value);   /* + "parts", "device:<i>" */
+/* Per-phase timing of the choreography (events on slab 0's main stream, cross-slab waits included) while
+ * enabled; phases "residual", "forward", "backward", "allreduce", "dual", "outer", "step". */
+int pdhg_multi_profile(pdhg_multi* m, int enable);
+int pdhg_multi_phase_ms(pdhg_multi* m, const char* phase, double* total_ms, int* steps);
+
+/* Identity of the built library: a hash of the sources it was compiled from (build() compares it with
+ * the tree and rebuilds on a mismatch, so a stale libpdhg.so is never what the tests load). */
+const char* pdhg_build_id(void);
 
 #ifdef __cplusplus
 }

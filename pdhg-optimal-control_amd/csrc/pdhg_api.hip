@@ -85,14 +85,18 @@ struct ProfEntry {
 };
 
 struct ImplBase {
+  int device = 0;   // every entry point selects it before touching the context (dispatch)
   virtual ~ImplBase() {}
 };
+
+// handle tags: a pdhg_ctx* and a pdhg_multi* both start with one; an entry point rejects the other kind
+constexpr uint32_t kCtxMagic = 0x50444843u;    // "PDHC"
+constexpr uint32_t kMultiMagic = 0x5044484du;  // "PDHM"
 
 template <typename R>
 struct Impl : ImplBase {
   using C = cplx<R>;
   pdhg_problem pb{};
-  int device = 0;
   hipStream_t stream = nullptr;
   KP<R> kp{};
   FFTPlan plx{}, ply{};
@@ -1689,14 +1693,25 @@ struct Impl : ImplBase {
 };
 
 struct CtxBox {
+  uint32_t magic = kCtxMagic;
   int precision;
   std::unique_ptr<ImplBase> impl;
 };
 
+// the context behind a handle, with its device made current (a thread may drive contexts on several GPUs:
+// every kernel launch, allocation and hipFuncSetAttribute of the call then lands on the context's device)
+CtxBox* ctx_box(pdhg_ctx* ctx) {
+  if (!ctx) return nullptr;
+  CtxBox* b = reinterpret_cast<CtxBox*>(ctx);
+  if (b->magic != kCtxMagic || !b->impl) return nullptr;
+  if (hipSetDevice(b->impl->device) != hipSuccess) return nullptr;
+  return b;
+}
+
 template <typename F>
 int dispatch(pdhg_ctx* ctx, F&& f) {
-  if (!ctx) return fail(PDHG_ERR_ARG, "null context");
-  CtxBox* b = reinterpret_cast<CtxBox*>(ctx);
+  CtxBox* b = ctx_box(ctx);
+  if (!b) return fail(PDHG_ERR_ARG, "null or foreign context handle");
   if (b->precision == 8) return f(*static_cast<Impl<double>*>(b->impl.get()));
   return f(*static_cast<Impl<float>*>(b->impl.get()));
 }
@@ -1704,8 +1719,8 @@ int dispatch(pdhg_ctx* ctx, F&& f) {
 // phases shared by the t-slab and x-slab contexts (begin, finalizers, dual, outer, status)
 template <typename F>
 int phase_dispatch(pdhg_ctx* ctx, F&& f) {
-  if (!ctx) return fail(PDHG_ERR_ARG, "null context");
-  CtxBox* b = reinterpret_cast<CtxBox*>(ctx);
+  CtxBox* b = ctx_box(ctx);
+  if (!b) return fail(PDHG_ERR_ARG, "null or foreign context handle");
   if (b->precision != 4) return fail(PDHG_ERR_STATE, "not a t-slab / x-slab context");
   auto& im = *static_cast<Impl<float>*>(b->impl.get());
   if (!im.slab && !im.xslab) return fail(PDHG_ERR_STATE, "not a t-slab / x-slab context");
@@ -1714,8 +1729,8 @@ int phase_dispatch(pdhg_ctx* ctx, F&& f) {
 
 template <typename F>
 int xslab_dispatch(pdhg_ctx* ctx, F&& f) {
-  if (!ctx) return fail(PDHG_ERR_ARG, "null context");
-  CtxBox* b = reinterpret_cast<CtxBox*>(ctx);
+  CtxBox* b = ctx_box(ctx);
+  if (!b) return fail(PDHG_ERR_ARG, "null or foreign context handle");
   if (b->precision != 4) return fail(PDHG_ERR_STATE, "not an x-slab context");
   auto& im = *static_cast<Impl<float>*>(b->impl.get());
   int rc = im.need_xslab();
@@ -1724,12 +1739,31 @@ int xslab_dispatch(pdhg_ctx* ctx, F&& f) {
 
 template <typename F>
 int slab_dispatch(pdhg_ctx* ctx, F&& f) {
-  if (!ctx) return fail(PDHG_ERR_ARG, "null context");
-  CtxBox* b = reinterpret_cast<CtxBox*>(ctx);
+  CtxBox* b = ctx_box(ctx);
+  if (!b) return fail(PDHG_ERR_ARG, "null or foreign context handle");
   if (b->precision != 4) return fail(PDHG_ERR_STATE, "not a t-slab context");
   auto& im = *static_cast<Impl<float>*>(b->impl.get());
   int rc = im.need_slab();
   return rc ? rc : f(im);
+}
+
+// the multi-device context (pdhg_multi.hpp): the done flag of a slab's control block, read by a synchronous
+// copy that does not wait for the slab's stream (the caller synchronised on an event recorded after the
+// iteration it wants), and the device a slab computes on
+int slab_done_flag(pdhg_ctx* ctx, int* done) {
+  return slab_dispatch(ctx, [&](auto& im) {
+    HIP_TRY(hipMemcpy(im.h_done, &im.kp.ctrl->done, sizeof(int), hipMemcpyDeviceToHost));
+    *done = *im.h_done;
+    return (int)PDHG_OK;
+  });
+}
+int slab_device(pdhg_ctx* ctx, int* device) {
+  return slab_dispatch(ctx, [&](auto& im) {
+    int d = -1;
+    HIP_TRY(hipGetDevice(&d));
+    *device = d;
+    return (int)PDHG_OK;
+  });
 }
 
 }  // namespace
@@ -1737,6 +1771,11 @@ int slab_dispatch(pdhg_ctx* ctx, F&& f) {
 extern "C" {
 
 const char* pdhg_last_error(void) { return g_err.c_str(); }
+#ifndef PDHG_BUILD_ID
+#define PDHG_BUILD_ID "unknown"
+#endif
+__attribute__((used)) static const char kBuildTag[] = "PDHG_BUILD_ID=" PDHG_BUILD_ID;   // read by build()
+const char* pdhg_build_id(void) { return kBuildTag + 14; }
 int pdhg_abi_version(void) { return PDHG_ABI_VERSION; }
 
 int pdhg_device_count(int* count) {
@@ -1794,7 +1833,10 @@ int pdhg_create(const pdhg_problem* prob, int device, pdhg_ctx** out) {
 
 int pdhg_destroy(pdhg_ctx* ctx) {
   if (!ctx) return PDHG_OK;
-  delete reinterpret_cast<CtxBox*>(ctx);
+  CtxBox* b = ctx_box(ctx);
+  if (!b) return fail(PDHG_ERR_ARG, "foreign context handle");
+  b->magic = 0;
+  delete b;
   return PDHG_OK;
 }
 

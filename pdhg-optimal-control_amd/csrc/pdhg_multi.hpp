@@ -3,14 +3,23 @@
 // SlabRunner: the window's T rows are split into ndev t-slabs (one pdhg_create_slab context per listed device,
 // a device may repeat), and pdhg_multi_iterate runs the outer iteration of utils_pdhg_solver.py:51-88 with
 // the slab choreography documented in include/pdhg.h (neighbour carry exchange), from this one thread:
-//   * every slab computes on its own stream of its own device;
-//   * planes move device to device with hipMemcpyPeerAsync (xGMI / SDMA; plain device copies when two slabs
-//     share a GPU): rho halo up, phi_bar halo down, D to the next slab, S1 to the previous one, the
-//     long-range modes to everybody;
-//   * the 16-double sum vectors are gathered on slab 0's device, folded in slab order by k_multi_sum, and
-//     copied back, so every slab takes the same stop decisions in its own control block;
-//   * an exchange is bracketed by stream barriers (events): producers done -> copies -> consumers.
-// Included by pdhg_api.hip after the C ABI (uses only the slab entry points).
+//   * slab r computes on its main stream st[r] and receives planes on its side stream ss[r] (both on dev[r]);
+//   * a plane moves device to device with hipMemcpyPeerAsync (xGMI / SDMA; a plain device copy when two slabs
+//     share a GPU) on the RECEIVER's side stream, after an event its producer recorded; the receiver's main
+//     stream waits for the side stream's event only where the plane is consumed.  So the rho halo travels
+//     while the residual rows that do not read it compute, the phi_bar halo while the primal sums are
+//     reduced and the dual rows that do not read it run, and the column-block part q's carry planes while
+//     part q+1 sweeps forward (SlabRunner's schedule, pdhg_amd/slab.py);
+//   * waits are per neighbour (rho halo: r+1 -> r, phi_bar halo: r-1 -> r, D: r-1 -> r, S1: r+1 -> r), never
+//     all-to-all; only the long-range carry modes (few, pdhg_slab_long_modes) and the sums need every slab;
+//   * the 16-double sum vectors are gathered on slab 0's device (slab 0's stream waits each slab's event),
+//     folded in slab order by k_multi_sum, and copied back by every slab's main stream after one event, so
+//     every slab takes the same stop decisions in its own control block.
+// Reuse of an exchange buffer is safe without extra events: every plane a receiver consumes is consumed
+// before that receiver's next sums contribution, and every producer overwrites its send buffer only after
+// the following sums fold, which waited for every slab's contribution.
+// Included by pdhg_api.hip after the C ABI (uses the slab entry points and, for the lagged done read, the
+// slab context's control block).
 #pragma once
 #include <vector>
 
@@ -25,11 +34,12 @@ __global__ void k_multi_sum(const double* __restrict__ in, int n, double* __rest
 }  // namespace pdhg
 
 struct pdhg_multi {
+  uint32_t magic = kMultiMagic;
   int P = 0;
+  int parts = 2;           // column-block parts of the carry exchange
   std::vector<int> dev;
   std::vector<pdhg_ctx*> s;
-  std::vector<hipStream_t> st;
-  std::vector<hipEvent_t> ev;
+  std::vector<hipStream_t> st, ss;
   std::vector<int> j0, j1;
   pdhg_problem pb{};
   std::vector<double> xs, ys;
@@ -41,11 +51,23 @@ struct pdhg_multi {
     float *DS = nullptr, *GS = nullptr, *Dl = nullptr, *S1r = nullptr, *LONG = nullptr, *allLong = nullptr,
           *allGS = nullptr;
     double* sums = nullptr;
+    // events: producer side (main stream) and receiver side (side stream)
+    hipEvent_t rho = nullptr, rho_in = nullptr, longp = nullptr, long_in = nullptr, pb = nullptr, pb_in = nullptr,
+               sum = nullptr;
+    std::vector<hipEvent_t> ds, carry_in;   // per part
   };
   std::vector<Buf> b;
   double* gather = nullptr;   // slab 0's device: [P][16] sums, then the folded [16]
+  hipEvent_t folded = nullptr;
   std::vector<void*> allocs;  // (device, pointer) freed at destroy
   std::vector<int> alloc_dev;
+  std::vector<hipEvent_t> all_events;   // (created on the device of the slab that records them)
+  std::vector<int> event_dev;
+  // per-phase timing on slab 0's main stream (waits included): marks between the phases of step()
+  bool prof = false;
+  static constexpr int kMarks = 8;
+  std::vector<std::vector<hipEvent_t>> marks;   // [step][kMarks]
+  size_t marks_used = 0;
 
   int on(int r) { return hipSetDevice(dev[r]) == hipSuccess ? 0 : -1; }
   template <typename T>
@@ -60,38 +82,71 @@ struct pdhg_multi {
     *p = static_cast<T*>(q);
     return PDHG_OK;
   }
-  // every stream waits for everything enqueued so far on every stream
-  int barrier() {
-    for (int r = 0; r < P; ++r) {
-      if (on(r)) return fail(PDHG_ERR_HIP, "hipSetDevice");
-      HIP_TRY(hipEventRecord(ev[r], st[r]));
-    }
-    for (int r = 0; r < P; ++r) {
-      if (on(r)) return fail(PDHG_ERR_HIP, "hipSetDevice");
-      for (int q = 0; q < P; ++q)
-        if (q != r) HIP_TRY(hipStreamWaitEvent(st[r], ev[q], 0));
-    }
+  int event(int r, hipEvent_t* e, bool timing = false) {
+    if (on(r)) return fail(PDHG_ERR_HIP, "hipSetDevice(%d)", dev[r]);
+    HIP_TRY(hipEventCreateWithFlags(e, timing ? hipEventDefault : hipEventDisableTiming));
+    all_events.push_back(*e);
+    event_dev.push_back(dev[r]);
     return PDHG_OK;
   }
-  // copy on the destination slab's stream (call between barriers)
-  int copy(int rd, void* dst, int rs, const void* src, size_t bytes) {
+  int rec(hipEvent_t e, int r, hipStream_t s_) {
+    if (on(r)) return fail(PDHG_ERR_HIP, "hipSetDevice");
+    HIP_TRY(hipEventRecord(e, s_));
+    return PDHG_OK;
+  }
+  int wait(int r, hipStream_t s_, hipEvent_t e) {
+    if (on(r)) return fail(PDHG_ERR_HIP, "hipSetDevice");
+    HIP_TRY(hipStreamWaitEvent(s_, e, 0));
+    return PDHG_OK;
+  }
+  // copy on stream s_ of slab rd (the receiver)
+  int copy(int rd, hipStream_t s_, void* dst, int rs, const void* src, size_t bytes) {
     if (on(rd)) return fail(PDHG_ERR_HIP, "hipSetDevice");
-    if (dev[rd] == dev[rs]) HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st[rd]));
-    else HIP_TRY(hipMemcpyPeerAsync(dst, dev[rd], src, dev[rs], bytes, st[rd]));
+    if (dev[rd] == dev[rs]) HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s_));
+    else HIP_TRY(hipMemcpyPeerAsync(dst, dev[rd], src, dev[rs], bytes, s_));
     return PDHG_OK;
   }
-  int allreduce() {   // sums of every slab -> fixed-order fold on slab 0 -> back to every slab
+  // every main stream waits for everything enqueued so far on every main and side stream (setup only)
+  int full_barrier() {
+    for (int r = 0; r < P; ++r) {
+      if (on(r)) return fail(PDHG_ERR_HIP, "hipSetDevice");
+      HIP_TRY(hipStreamSynchronize(ss[r]));
+      HIP_TRY(hipStreamSynchronize(st[r]));
+    }
+    return PDHG_OK;
+  }
+  int mark(int i) {
+    if (!prof) return PDHG_OK;
+    if (i == 0) {
+      if (marks_used == marks.size()) {
+        marks.emplace_back(kMarks, nullptr);
+        for (int m = 0; m < kMarks; ++m) {
+          int rc = event(0, &marks.back()[m], true);
+          if (rc) return rc;
+        }
+      }
+      ++marks_used;
+    }
+    return rec(marks[marks_used - 1][i], 0, st[0]);
+  }
+  // sums of every slab -> fixed-order fold on slab 0 -> back to every slab
+  int allreduce() {
     int rc;
-    if ((rc = barrier())) return rc;
     for (int q = 0; q < P; ++q)
-      if ((rc = copy(0, gather + (size_t)q * kNumSums, q, b[q].sums, kNumSums * sizeof(double)))) return rc;
+      if ((rc = rec(b[q].sum, q, st[q]))) return rc;
+    for (int q = 1; q < P; ++q)
+      if ((rc = wait(0, st[0], b[q].sum))) return rc;
+    for (int q = 0; q < P; ++q)
+      if ((rc = copy(0, st[0], gather + (size_t)q * kNumSums, q, b[q].sums, kNumSums * sizeof(double)))) return rc;
     if (on(0)) return fail(PDHG_ERR_HIP, "hipSetDevice");
     hipLaunchKernelGGL(pdhg::k_multi_sum, dim3(1), dim3(64), 0, st[0], gather, P, gather + (size_t)P * kNumSums);
     HIP_TRY(hipGetLastError());
-    if ((rc = barrier())) return rc;
-    for (int q = 0; q < P; ++q)
-      if ((rc = copy(q, b[q].sums, 0, gather + (size_t)P * kNumSums, kNumSums * sizeof(double)))) return rc;
-    return barrier();
+    if ((rc = rec(folded, 0, st[0]))) return rc;
+    for (int q = 0; q < P; ++q) {
+      if (q > 0 && (rc = wait(q, st[q], folded))) return rc;
+      if ((rc = copy(q, st[q], b[q].sums, 0, gather + (size_t)P * kNumSums, kNumSums * sizeof(double)))) return rc;
+    }
+    return PDHG_OK;
   }
 
   int setup(const pdhg_problem& prob, const int* devices, int ndev) {
@@ -105,6 +160,7 @@ struct pdhg_multi {
     nc = prob.egno == 3 ? 1 : 2;
     const int T = prob.T;
     if (P < 1 || P > T) return fail(PDHG_ERR_ARG, "need 1 <= ndev <= T (ndev %d, T %d)", P, T);
+    if (const char* e = getenv("PDHG_MULTI_PARTS")) parts = std::max(1, atoi(e));   // tuning override
     const int base = T / P, extra = T % P;
     for (int q = 0, j = 0; q < P; ++q) {   // pdhg_amd.slab.slab_bounds
       const int n = base + (q < extra ? 1 : 0);
@@ -126,7 +182,7 @@ struct pdhg_multi {
       }
     s.assign(P, nullptr);
     st.assign(P, nullptr);
-    ev.assign(P, nullptr);
+    ss.assign(P, nullptr);
     b.assign(P, Buf{});
     int rc;
     for (int r = 0; r < P; ++r) {
@@ -135,9 +191,17 @@ struct pdhg_multi {
       if ((rc = pdhg_create_slab(&q, j0[r], T, dev[r], &s[r]))) return rc;
       if (on(r)) return fail(PDHG_ERR_HIP, "hipSetDevice");
       HIP_TRY(hipStreamCreateWithFlags(&st[r], hipStreamNonBlocking));
-      HIP_TRY(hipEventCreateWithFlags(&ev[r], hipEventDisableTiming));
+      HIP_TRY(hipStreamCreateWithFlags(&ss[r], hipStreamNonBlocking));
       if ((rc = pdhg_set_stream(s[r], st[r]))) return rc;
+      Buf& x = b[r];
+      for (hipEvent_t* e : {&x.rho, &x.rho_in, &x.longp, &x.long_in, &x.pb, &x.pb_in, &x.sum})
+        if ((rc = event(r, e))) return rc;
+      x.ds.assign(parts, nullptr);
+      x.carry_in.assign(parts, nullptr);
+      for (int q = 0; q < parts; ++q)
+        if ((rc = event(r, &x.ds[q])) || (rc = event(r, &x.carry_in[q]))) return rc;
     }
+    if ((rc = event(0, &folded))) return rc;
     unsigned long long a = 0, c = 0;
     if ((rc = pdhg_slab_plane_size(s[0], &a, &c))) return rc;
     sp = a;
@@ -153,15 +217,11 @@ struct pdhg_multi {
     }
     if ((rc = alloc(0, &gather, (size_t)(P + 1) * kNumSums))) return rc;
     // iteration-invariant gains of every slab to every slab, then the long-range classification
-    if ((rc = barrier())) return rc;
+    if ((rc = full_barrier())) return rc;
     for (int r = 0; r < P; ++r)
       for (int q = 0; q < P; ++q)
-        if ((rc = copy(r, b[r].allGS + (size_t)q * 2 * spec, q, b[q].GS, 2 * spec * sizeof(float)))) return rc;
-    if ((rc = barrier())) return rc;
-    for (int r = 0; r < P; ++r) {   // the classification reads the planes on the host side
-      if (on(r)) return fail(PDHG_ERR_HIP, "hipSetDevice");
-      HIP_TRY(hipStreamSynchronize(st[r]));
-    }
+        if ((rc = copy(r, st[r], b[r].allGS + (size_t)q * 2 * spec, q, b[q].GS, 2 * spec * sizeof(float)))) return rc;
+    if ((rc = full_barrier())) return rc;
     for (int r = 0; r < P; ++r) {
       int k = 0;
       if ((rc = pdhg_slab_long_modes(s[r], b[r].allGS, P, 9.094947017729282e-13 /* 2^-40 */, &k))) return rc;
@@ -172,97 +232,163 @@ struct pdhg_multi {
       if ((rc = alloc(r, &b[r].LONG, (size_t)std::max(1, 2 * K))) ||
           (rc = alloc(r, &b[r].allLong, (size_t)std::max(1, 2 * K) * P)))
         return rc;
-    for (int r = 0; r < P; ++r) {
-      if (on(r)) return fail(PDHG_ERR_HIP, "hipSetDevice");
-      HIP_TRY(hipStreamSynchronize(st[r]));
-    }
-    return PDHG_OK;
+    return full_barrier();
   }
 
   ~pdhg_multi() {
-    for (int r = 0; r < P; ++r)
-      if (r < (int)st.size() && st[r]) {
-        hipSetDevice(dev[r]);
-        hipStreamSynchronize(st[r]);
-      }
+    for (int r = 0; r < P; ++r) {
+      if (r < (int)st.size() && st[r]) { hipSetDevice(dev[r]); hipStreamSynchronize(st[r]); }
+      if (r < (int)ss.size() && ss[r]) { hipSetDevice(dev[r]); hipStreamSynchronize(ss[r]); }
+    }
     for (auto* c : s) pdhg_destroy(c);
     for (size_t i = 0; i < allocs.size(); ++i) {
       hipSetDevice(alloc_dev[i]);
       hipFree(allocs[i]);
     }
-    for (int r = 0; r < P; ++r) {
-      if (r < (int)ev.size() && ev[r]) { hipSetDevice(dev[r]); hipEventDestroy(ev[r]); }
-      if (r < (int)st.size() && st[r]) { hipSetDevice(dev[r]); hipStreamDestroy(st[r]); }
+    for (size_t i = 0; i < all_events.size(); ++i) {
+      hipSetDevice(event_dev[i]);
+      hipEventDestroy(all_events[i]);
     }
+    for (int r = 0; r < P; ++r) {
+      if (r < (int)st.size() && st[r]) { hipSetDevice(dev[r]); hipStreamDestroy(st[r]); }
+      if (r < (int)ss.size() && ss[r]) { hipSetDevice(dev[r]); hipStreamDestroy(ss[r]); }
+    }
+    magic = 0;
   }
 
-  // one outer iteration (include/pdhg.h t-slab choreography, neighbour exchange)
+  // one outer iteration (include/pdhg.h t-slab choreography, neighbour exchange in `parts` column-block parts)
   int step(double tau, double sigma, double eps, int k) {
     int rc;
-    const size_t pbytes = sp * sizeof(float), sbytes = spec * sizeof(float);
+    const size_t pbytes = sp * sizeof(float);
+    if ((rc = mark(0))) return rc;
+    // rho halo (row 0 of slab r+1 -> slab r) on the receiver's side stream || the residual rows without it
     for (int r = 0; r < P; ++r)
-      if ((rc = pdhg_slab_plane_out(s[r], 0, b[r].rho_send))) return rc;
-    if ((rc = barrier())) return rc;
-    for (int r = 0; r + 1 < P; ++r)   // rho row 0 of slab r+1 -> slab r
-      if ((rc = copy(r, b[r].rho_recv, r + 1, b[r + 1].rho_send, pbytes))) return rc;
-    if ((rc = barrier())) return rc;
+      if ((rc = pdhg_slab_plane_out(s[r], 0, b[r].rho_send)) || (rc = rec(b[r].rho, r, st[r]))) return rc;
+    for (int r = 0; r + 1 < P; ++r)
+      if ((rc = wait(r, ss[r], b[r + 1].rho)) ||
+          (rc = copy(r, ss[r], b[r].rho_recv, r + 1, b[r + 1].rho_send, pbytes)) || (rc = rec(b[r].rho_in, r, ss[r])))
+        return rc;
+    for (int r = 0; r < P; ++r)
+      if ((rc = pdhg_slab_residual(s[r], 1))) return rc;
     for (int r = 0; r < P; ++r) {
-      if (r + 1 < P && (rc = pdhg_slab_plane_in(s[r], 0, b[r].rho_recv))) return rc;
-      if ((rc = pdhg_slab_residual(s[r], 3))) return rc;
-      if ((rc = pdhg_slab_forward(s[r], tau))) return rc;
-      if ((rc = pdhg_slab_plane_out(s[r], 2, b[r].DS))) return rc;
-      if ((rc = pdhg_slab_plane_out(s[r], 3, b[r].LONG))) return rc;
+      if (r + 1 < P && ((rc = wait(r, st[r], b[r].rho_in)) || (rc = pdhg_slab_plane_in(s[r], 0, b[r].rho_recv))))
+        return rc;
+      if ((rc = pdhg_slab_residual(s[r], 2))) return rc;
     }
-    if ((rc = barrier())) return rc;
-    for (int r = 0; r < P; ++r) {
-      if (r > 0 && (rc = copy(r, b[r].Dl, r - 1, b[r - 1].DS, sbytes))) return rc;              // D -> next
-      if (r + 1 < P && (rc = copy(r, b[r].S1r, r + 1, b[r + 1].DS + spec, sbytes))) return rc;  // S1 -> previous
-      for (int q = 0; q < P && K > 0; ++q)
-        if ((rc = copy(r, b[r].allLong + (size_t)q * 2 * K, q, b[q].LONG, 2 * (size_t)K * sizeof(float)))) return rc;
-    }
-    if ((rc = barrier())) return rc;
-    for (int r = 0; r < P; ++r) {
-      if ((rc = pdhg_slab_fixup_nb(s[r], b[r].Dl, b[r].S1r, b[r].allLong, b[r].allGS, r, P))) return rc;
-      if ((rc = pdhg_slab_backward(s[r], tau, b[r].sums))) return rc;
-    }
-    if ((rc = allreduce())) return rc;
-    for (int r = 0; r < P; ++r) {
-      if ((rc = pdhg_slab_primal_finalize(s[r], b[r].sums))) return rc;
-      if ((rc = pdhg_slab_plane_out(s[r], 1, b[r].pb_send))) return rc;
-    }
-    if ((rc = barrier())) return rc;
-    for (int r = 1; r < P; ++r)   // phi_bar row T of slab r-1 -> slab r
-      if ((rc = copy(r, b[r].pb_recv, r - 1, b[r - 1].pb_send, pbytes))) return rc;
-    if ((rc = barrier())) return rc;
-    for (int sub = 0; sub < k; ++sub) {
+    if ((rc = mark(1))) return rc;
+    // zero-carry forward sweeps part by part; part q's D (to r+1) and S1 (to r-1) travel during part q+1
+    for (int q = 0; q < parts; ++q) {
+      unsigned long long m0 = 0, m1 = 0;
+      if ((rc = pdhg_slab_part_modes(s[0], q, parts, &m0, &m1))) return rc;
+      const size_t off = m0, n = (m1 - m0) * sizeof(float);
+      for (int r = 0; r < P; ++r)
+        if ((rc = pdhg_slab_forward_part(s[r], tau, q, parts)) || (rc = pdhg_slab_carry_out_part(s[r], b[r].DS, q, parts)) ||
+            (rc = rec(b[r].ds[q], r, st[r])))
+          return rc;
       for (int r = 0; r < P; ++r) {
-        if (sub == 0 && r > 0 && (rc = pdhg_slab_plane_in(s[r], 1, b[r].pb_recv))) return rc;
-        if ((rc = pdhg_slab_dual(s[r], sigma, k, sub, b[r].sums, 3))) return rc;
+        if (r > 0 && ((rc = wait(r, ss[r], b[r - 1].ds[q])) ||
+                      (rc = copy(r, ss[r], b[r].Dl + off, r - 1, b[r - 1].DS + off, n))))
+          return rc;
+        if (r + 1 < P && ((rc = wait(r, ss[r], b[r + 1].ds[q])) ||
+                          (rc = copy(r, ss[r], b[r].S1r + off, r + 1, b[r + 1].DS + spec + off, n))))
+          return rc;
+        if ((rc = rec(b[r].carry_in[q], r, ss[r]))) return rc;
       }
+    }
+    // the long-range modes go to every slab
+    if (K > 0) {
+      for (int r = 0; r < P; ++r)
+        if ((rc = pdhg_slab_plane_out(s[r], 3, b[r].LONG)) || (rc = rec(b[r].longp, r, st[r]))) return rc;
+      for (int r = 0; r < P; ++r) {
+        for (int q = 0; q < P; ++q)
+          if ((rc = wait(r, ss[r], b[q].longp)) ||
+              (rc = copy(r, ss[r], b[r].allLong + (size_t)q * 2 * K, q, b[q].LONG, 2 * (size_t)K * sizeof(float))))
+            return rc;
+        if ((rc = rec(b[r].long_in, r, ss[r]))) return rc;
+      }
+    }
+    if ((rc = mark(2))) return rc;
+    // carry fix-ups and backward sweeps part by part, then the inverse y transform + update (primal sums)
+    for (int q = 0; q < parts; ++q)
+      for (int r = 0; r < P; ++r) {
+        if ((rc = wait(r, st[r], b[r].carry_in[q]))) return rc;
+        if (q == 0 && K > 0 && (rc = wait(r, st[r], b[r].long_in))) return rc;
+        if ((rc = pdhg_slab_fixup_nb_part(s[r], b[r].Dl, b[r].S1r, b[r].allLong, b[r].allGS, r, P, q, parts)) ||
+            (rc = pdhg_slab_backward_part(s[r], tau, q, parts)))
+          return rc;
+      }
+    for (int r = 0; r < P; ++r)
+      if ((rc = pdhg_slab_update(s[r], tau, b[r].sums))) return rc;
+    if ((rc = mark(3))) return rc;
+    // phi_bar halo (row T of slab r-1 -> row 0 of slab r) || the primal sums and the interior dual rows
+    for (int r = 0; r < P; ++r)
+      if ((rc = pdhg_slab_plane_out(s[r], 1, b[r].pb_send)) || (rc = rec(b[r].pb, r, st[r]))) return rc;
+    for (int r = 1; r < P; ++r)
+      if ((rc = wait(r, ss[r], b[r - 1].pb)) || (rc = copy(r, ss[r], b[r].pb_recv, r - 1, b[r - 1].pb_send, pbytes)) ||
+          (rc = rec(b[r].pb_in, r, ss[r])))
+        return rc;
+    if ((rc = allreduce())) return rc;
+    for (int r = 0; r < P; ++r)
+      if ((rc = pdhg_slab_primal_finalize(s[r], b[r].sums))) return rc;
+    if ((rc = mark(4))) return rc;
+    for (int sub = 0; sub < k; ++sub) {
+      for (int r = 0; r < P; ++r)
+        if ((rc = pdhg_slab_dual(s[r], sigma, k, sub, b[r].sums, sub == 0 ? 1 : 3))) return rc;
+      if (sub == 0)
+        for (int r = 0; r < P; ++r) {
+          if (r > 0 && ((rc = wait(r, st[r], b[r].pb_in)) || (rc = pdhg_slab_plane_in(s[r], 1, b[r].pb_recv))))
+            return rc;
+          if ((rc = pdhg_slab_dual(s[r], sigma, k, sub, b[r].sums, 2))) return rc;
+        }
       if ((rc = allreduce())) return rc;
       for (int r = 0; r < P; ++r)
         if ((rc = pdhg_slab_dual_finalize(s[r], eps, sub, b[r].sums))) return rc;
     }
+    if ((rc = mark(5))) return rc;
     for (int r = 0; r < P; ++r)
       if ((rc = pdhg_slab_outer(s[r], k, b[r].sums))) return rc;
     if (k > 1 && (rc = allreduce())) return rc;
     for (int r = 0; r < P; ++r)
       if ((rc = pdhg_slab_outer_finalize(s[r], eps, k, b[r].sums))) return rc;
-    return PDHG_OK;
+    return mark(6);
   }
 
   int iterate(int n, double tau, double sigma, double eps, int k, pdhg_stats* out) {
     int rc;
     for (int r = 0; r < P; ++r)
       if ((rc = pdhg_slab_begin(s[r]))) return rc;
-    for (int it = 0; it < n; ++it) {
-      if ((rc = step(tau, sigma, eps, k))) return rc;
-      if ((it + 1) % 8 == 0 && it + 1 < n) {   // the device loop control, read every 8 iterations
-        pdhg_stats h{};
-        if ((rc = pdhg_slab_status(s[0], &h))) return rc;
-        if (h.status) break;
+    // the device loop control of Impl::iterate: at most two windows of 8 iterations ahead of the device,
+    // the done flag of the window before the last one read without draining the pipeline
+    const int window = 8;
+    std::vector<hipEvent_t> evs;
+    int ret = PDHG_OK;
+    for (int it = 0; it < n && ret == PDHG_OK; ++it) {
+      if ((ret = step(tau, sigma, eps, k))) break;
+      if ((it + 1) % window == 0 && it + 1 < n) {
+        hipEvent_t e;
+        if ((ret = event(0, &e))) break;
+        if ((ret = rec(e, 0, st[0]))) break;
+        evs.push_back(e);
+        if (evs.size() >= 2) {
+          int done = 0;
+          if (hipEventSynchronize(evs[evs.size() - 2]) != hipSuccess) { ret = fail(PDHG_ERR_HIP, "event sync"); break; }
+          if ((ret = slab_done_flag(s[0], &done))) break;
+          if (done) break;
+        }
       }
     }
+    for (auto e : evs) {   // drop the window events (created through event(): remove from the pool)
+      for (size_t i = 0; i < all_events.size(); ++i)
+        if (all_events[i] == e) {
+          hipSetDevice(event_dev[i]);
+          hipEventSynchronize(e);
+          hipEventDestroy(e);
+          all_events.erase(all_events.begin() + i);
+          event_dev.erase(event_dev.begin() + i);
+          break;
+        }
+    }
+    if (ret) return ret;
     pdhg_stats h{};
     if ((rc = pdhg_slab_status(s[0], &h))) return rc;
     if (out) *out = h;
@@ -274,10 +400,7 @@ struct pdhg_multi {
     const size_t npl = (size_t)pb.nx * pb.ny;
     const int T = pb.T;
     int rc;
-    for (int r = 0; r < P; ++r) {   // the state copies are synchronous (null stream): drain the slab streams
-      if (on(r)) return fail(PDHG_ERR_HIP, "hipSetDevice");
-      HIP_TRY(hipStreamSynchronize(st[r]));
-    }
+    if ((rc = full_barrier())) return rc;   // the state copies are synchronous: drain the slab streams
     for (int r = 0; r < P; ++r) {
       const int Tr = j1[r] - j0[r];
       std::vector<double> ph(phi ? (size_t)(Tr + 1) * npl : 0), rh(rho ? (size_t)Tr * npl : 0),
@@ -311,7 +434,26 @@ struct pdhg_multi {
     }
     return PDHG_OK;
   }
+
+  // total ms between marks [m0, m1) over the recorded steps
+  int phase_ms(int m0, int m1, double* ms, int* n) {
+    *ms = 0.0;
+    *n = 0;
+    if (on(0)) return fail(PDHG_ERR_HIP, "hipSetDevice");
+    HIP_TRY(hipStreamSynchronize(st[0]));
+    for (size_t i = 0; i < marks_used; ++i) {
+      float t = 0.f;
+      HIP_TRY(hipEventElapsedTime(&t, marks[i][m0], marks[i][m1]));
+      *ms += t;
+      ++*n;
+    }
+    return PDHG_OK;
+  }
 };
+
+namespace {
+pdhg_multi* multi_handle(pdhg_multi* m) { return (m && m->magic == kMultiMagic) ? m : nullptr; }
+}  // namespace
 
 extern "C" {
 
@@ -329,25 +471,38 @@ int pdhg_create_multi(const pdhg_problem* prob, const int* devices, int ndev, pd
   return PDHG_OK;
 }
 int pdhg_multi_destroy(pdhg_multi* m) {
+  if (!m) return PDHG_OK;
+  if (!multi_handle(m)) return fail(PDHG_ERR_ARG, "not a multi-device context");
   delete m;
   return PDHG_OK;
 }
+#define MULTI_GET(m)                                                                       \
+  do {                                                                                     \
+    if (!multi_handle(m)) return fail(PDHG_ERR_ARG, "null or foreign multi-device handle"); \
+  } while (0)
 int pdhg_multi_set_state(pdhg_multi* m, const double* phi, const double* rho, const double* alp) {
-  if (!m) return fail(PDHG_ERR_ARG, "null context");
+  MULTI_GET(m);
   return m->state(true, const_cast<double*>(phi), const_cast<double*>(rho), const_cast<double*>(alp));
 }
+int pdhg_multi_init_state(pdhg_multi* m, const double* g) {
+  MULTI_GET(m);
+  if (!g) return fail(PDHG_ERR_ARG, "null g");
+  int rc = m->full_barrier();
+  for (int r = 0; r < m->P && !rc; ++r) rc = pdhg_init_state(m->s[r], g);   // utils_pdhg_solver.py:123-137
+  return rc;
+}
 int pdhg_multi_get_state(pdhg_multi* m, double* phi, double* rho, double* alp) {
-  if (!m) return fail(PDHG_ERR_ARG, "null context");
+  MULTI_GET(m);
   return m->state(false, phi, rho, alp);
 }
 int pdhg_multi_iterate(pdhg_multi* m, int n_iters, double tau, double sigma, double eps, int rho_alp_iters,
                        pdhg_stats* out) {
-  if (!m) return fail(PDHG_ERR_ARG, "null context");
+  MULTI_GET(m);
   if (n_iters < 0 || rho_alp_iters < 1) return fail(PDHG_ERR_ARG, "bad iteration counts");
   return m->iterate(n_iters, tau, sigma, eps, rho_alp_iters, out);
 }
 int pdhg_multi_set_stop_rules(pdhg_multi* m, int stop_on_converge, int stop_on_nan) {
-  if (!m) return fail(PDHG_ERR_ARG, "null context");
+  MULTI_GET(m);
   for (auto* c : m->s) {
     int rc = pdhg_set_stop_rules(c, stop_on_converge, stop_on_nan);
     if (rc) return rc;
@@ -355,23 +510,47 @@ int pdhg_multi_set_stop_rules(pdhg_multi* m, int stop_on_converge, int stop_on_n
   return PDHG_OK;
 }
 int pdhg_multi_synchronize(pdhg_multi* m) {
-  if (!m) return fail(PDHG_ERR_ARG, "null context");
-  for (int r = 0; r < m->P; ++r) {
-    if (m->on(r)) return fail(PDHG_ERR_HIP, "hipSetDevice");
-    HIP_TRY(hipStreamSynchronize(m->st[r]));
-  }
-  return PDHG_OK;
+  MULTI_GET(m);
+  return m->full_barrier();
 }
 int pdhg_multi_info(pdhg_multi* m, const char* key, int* value) {
-  if (!m || !key || !value) return fail(PDHG_ERR_ARG, "null argument");
+  MULTI_GET(m);
+  if (!key || !value) return fail(PDHG_ERR_ARG, "null argument");
   const std::string k(key);
   if (k == "ndev") *value = m->P;
   else if (k == "long_modes") *value = m->K;
+  else if (k == "parts") *value = m->parts;
   else if (k.rfind("rows:", 0) == 0) {
     const int r = atoi(k.c_str() + 5);
     if (r < 0 || r >= m->P) return fail(PDHG_ERR_ARG, "slab %d of %d", r, m->P);
     *value = m->j1[r] - m->j0[r];
+  } else if (k.rfind("device:", 0) == 0) {   // the HIP device slab r computes on (its context's device)
+    const int r = atoi(k.c_str() + 7);
+    if (r < 0 || r >= m->P) return fail(PDHG_ERR_ARG, "slab %d of %d", r, m->P);
+    return slab_device(m->s[r], value);
   } else return fail(PDHG_ERR_ARG, "unknown key '%s'", key);
+  return PDHG_OK;
+}
+int pdhg_multi_profile(pdhg_multi* m, int enable) {
+  MULTI_GET(m);
+  int rc = m->full_barrier();
+  if (rc) return rc;
+  m->prof = enable != 0;
+  m->marks_used = 0;
+  return PDHG_OK;
+}
+int pdhg_multi_phase_ms(pdhg_multi* m, const char* phase, double* total_ms, int* steps) {
+  MULTI_GET(m);
+  if (!phase || !total_ms || !steps) return fail(PDHG_ERR_ARG, "null argument");
+  // marks: 0 start, 1 residual done, 2 forward sweeps + carry planes issued, 3 fix-up + backward + update,
+  // 4 primal sums folded, 5 dual sub-iterations (with their sums), 6 outer sums
+  static const struct { const char* name; int m0, m1; } kPh[] = {
+      {"residual", 0, 1}, {"forward", 1, 2}, {"backward", 2, 3}, {"allreduce", 3, 4}, {"dual", 4, 5},
+      {"outer", 5, 6}, {"step", 0, 6}};
+  for (const auto& ph : kPh)
+    if (!strcmp(ph.name, phase)) return m->phase_ms(ph.m0, ph.m1, total_ms, steps);
+  *total_ms = 0.0;
+  *steps = 0;
   return PDHG_OK;
 }
 

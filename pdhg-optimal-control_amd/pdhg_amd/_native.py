@@ -37,6 +37,7 @@ EXPORTS = (
     # multi-device context (one host thread, t-slabs over a device list)
     "pdhg_create_multi", "pdhg_multi_destroy", "pdhg_multi_set_state", "pdhg_multi_get_state",
     "pdhg_multi_iterate", "pdhg_multi_set_stop_rules", "pdhg_multi_synchronize", "pdhg_multi_info",
+    "pdhg_multi_profile", "pdhg_multi_phase_ms", "pdhg_multi_init_state", "pdhg_build_id",
 )
 
 
@@ -165,6 +166,10 @@ def load():
         "pdhg_multi_set_stop_rules": ([P, ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "pdhg_multi_synchronize": ([P], ctypes.c_int),
         "pdhg_multi_info": ([P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+        "pdhg_multi_profile": ([P, ctypes.c_int], ctypes.c_int),
+        "pdhg_multi_init_state": ([P, dp], ctypes.c_int),
+        "pdhg_multi_phase_ms": ([P, ctypes.c_char_p, dp, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+        "pdhg_build_id": ([], ctypes.c_char_p),
     }
     missing = set(EXPORTS) - set(sig)
     if missing:

@@ -2,35 +2,65 @@
 
 The C ABI's multi-device context (include/pdhg.h, ``pdhg_create_multi``; SURVEY.md 8(b)'s
 ``pdhg_create(prob, devices, ndev)``) splits the window's T rows into one t-slab per listed device and
-runs the slab choreography natively (``csrc/pdhg_multi.hpp``: device-to-device plane copies over xGMI,
-fixed-order sum folds), so a caller needs no communicator.  ``pdhg_amd.slab`` is the one-process-per-GPU
-form of the same algorithm (RCCL through torch.distributed), used by ``bench.py --gpus N``.
-Arrays are the whole window in the reference layouts, as for PDHGContext.
+runs the slab choreography natively (``csrc/pdhg_multi.hpp``: device-to-device plane copies over xGMI on
+per-slab side streams, per-neighbour events, fixed-order sum folds), so a caller needs no communicator.
+``pdhg_amd.slab`` is the one-process-per-GPU form of the same algorithm (RCCL through torch.distributed),
+used by ``bench.py --gpus N``.  Arrays are the whole window in the reference layouts, as for PDHGContext.
+
+The handle is a ``pdhg_multi*``, not a ``pdhg_ctx*``: this class therefore does not derive from
+PDHGContext, and offers only the whole-window calls the multi-device ABI has (state, iterate, stop rules,
+synchronize, info).  The library also rejects a foreign handle passed to a ``pdhg_ctx`` entry point.
 """
 import ctypes
 
 import numpy as np
 
 from . import _native as N
-from .context import PDHGContext
 
 
-class MultiContext(PDHGContext):
-    def __init__(self, egno, nx, ny, T, dx, dy, dt, xs, ys, devices=(0, 0), **kw):
+class MultiContext:
+    def __init__(self, egno, nx, ny, T, dx, dy, dt, xs, ys, devices=(0, 0), epsl=0.0, c_on_rho=70.0,
+                 precision="fp32", rho_alp_iters=1):
+        if precision not in ("fp32", 4):
+            raise N.PDHGUnsupported(N.PDHG_ERR_UNSUPPORTED, "the multi-device context is fp32 only (t-slab kernels)")
+        self._lib = N.load()
+        self.egno, self.ndim, self.nx, self.ny, self.T = int(egno), 2, int(nx), int(ny), int(T)
+        self.n_ctrl = 1 if egno == 3 else 2
+        self.n_alp = 4
+        self.rho_alp_iters = int(rho_alp_iters)
+        self._xs = np.ascontiguousarray(xs, dtype=np.float64).reshape(-1)
+        self._ys = np.ascontiguousarray(ys, dtype=np.float64).reshape(-1)
+        bcx = 1 if egno == 3 else 0
+        prob = N.pdhg_problem()
+        prob.egno, prob.ndim, prob.bc_x, prob.bc_y = self.egno, 2, bcx, 0
+        prob.nx, prob.ny, prob.T = self.nx, self.ny, self.T
+        prob.precision = 4
+        prob.rho_alp_iters = self.rho_alp_iters
+        prob.dx, prob.dy, prob.dt = float(dx), float(dy), float(dt)
+        prob.epsl, prob.c_on_rho = float(epsl), float(c_on_rho)
+        prob.C, prob.pow_, prob.Ct = 1.0, 1.0, 1.0
+        prob.xs, prob.ys = N.dptr(self._xs), N.dptr(self._ys)
+        self._prob = prob
         self._devices = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
         self._ndev = len(devices)
-        kw.setdefault("precision", "fp32")
-        super().__init__(egno, 2, nx, ny, T, dx, dy, dt, xs, ys, **kw)
-
-    def _create(self, prob, device):
         h = ctypes.c_void_p()
         N.check(self._lib.pdhg_create_multi(ctypes.byref(prob), self._devices, self._ndev, ctypes.byref(h)))
-        return h
+        self._h = h
+
+    @property
+    def _space(self):
+        return (self.nx, self.ny)
 
     def close(self):
         if getattr(self, "_h", None):
             self._lib.pdhg_multi_destroy(self._h)
             self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def set_state(self, phi=None, rho=None, alp=None):
         phi = None if phi is None else np.ascontiguousarray(phi, dtype=np.float64).reshape((self.T + 1,) + self._space)
@@ -39,6 +69,11 @@ class MultiContext(PDHGContext):
             alp = np.ascontiguousarray(np.stack([np.asarray(a, dtype=np.float64) for a in alp], axis=0))
             alp = alp.reshape((self.n_alp, self.T) + self._space + (self.n_ctrl,))
         N.check(self._lib.pdhg_multi_set_state(self._h, N.dptr(phi), N.dptr(rho), N.dptr(alp)))
+
+    def init_state(self, g):
+        """The reference initial state (phi = g on every row, rho = c_on_rho, alp = 0) on every slab."""
+        g = np.ascontiguousarray(g, dtype=np.float64).reshape(self._space)
+        N.check(self._lib.pdhg_multi_init_state(self._h, N.dptr(g)))
 
     def get_state(self):
         phi = np.empty((self.T + 1,) + self._space)
@@ -65,3 +100,20 @@ class MultiContext(PDHGContext):
         v = ctypes.c_int()
         N.check(self._lib.pdhg_multi_info(self._h, key.encode(), ctypes.byref(v)))
         return v.value
+
+    def phase_ms(self, reset=True):
+        """{phase: total ms} recorded on slab 0's streams since profiling was switched on
+        (pdhg_multi_profile): per-phase cost of the slab choreography."""
+        out = {}
+        for key in ("residual", "forward", "backward", "allreduce", "dual", "outer", "step"):
+            ms = ctypes.c_double()
+            n = ctypes.c_int()
+            N.check(self._lib.pdhg_multi_phase_ms(self._h, key.encode(), ctypes.byref(ms), ctypes.byref(n)))
+            if n.value:
+                out[key] = ms.value
+        if reset:
+            N.check(self._lib.pdhg_multi_profile(self._h, 1))
+        return out
+
+    def profile(self, on=True):
+        N.check(self._lib.pdhg_multi_profile(self._h, 1 if on else 0))

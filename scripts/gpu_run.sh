@@ -1,0 +1,35 @@
+#!/bin/bash
+# One parameterised GPU-box script (replaces the per-experiment gpu_r02*.sh files).
+# usage (via gpurun): bash scripts/gpu_run.sh <tag> <step> [<step> ...]
+#   smoke                 __graft_entry__.smoke()
+#   tests[:<pytest -k>]   pytest -m gpu (optionally filtered)
+#   bench[:<args>]        python bench.py <args, commas for spaces>  -> bench_<n>.json
+#   prof:<config>         scripts/profile.sh <config> <tag>
+# Every GPU step runs under its own time limit; the first failure ends the script.
+set -o pipefail
+TAG=$1; shift
+REPO=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$REPO"
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+n=0
+for step in "$@"; do
+  n=$((n + 1))
+  kind=${step%%:*}; arg=${step#*:}; [ "$arg" = "$step" ] && arg=""
+  arg=${arg//,/ }
+  echo "[$(date +%T)] step $n: $kind $arg"
+  case $kind in
+    smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { echo "smoke failed rc=$?"; tail -20 "$OUT/smoke.log"; exit 1; } ;;
+    tests) if [ -n "$arg" ]; then K=(-k "$arg"); else K=(); fi
+           timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread "${K[@]}" > "$OUT/tests_$n.log" 2>&1 || { echo "tests failed rc=$?"; tail -30 "$OUT/tests_$n.log"; exit 1; }
+           tail -3 "$OUT/tests_$n.log" ;;
+    bench) timeout -k 10 900 python -u bench.py $arg > "$OUT/bench_$n.json" 2> "$OUT/bench_$n.err" || { echo "bench failed rc=$?"; tail -20 "$OUT/bench_$n.err"; exit 1; }
+           cat "$OUT/bench_$n.json" ;;
+    prof)  timeout -k 10 1000 bash scripts/profile.sh "$arg" "${TAG}_$arg" > "$OUT/prof_$n.log" 2>&1 || { echo "prof failed rc=$?"; tail -20 "$OUT/prof_$n.log"; exit 1; }
+           cd "$REPO" ;;
+    py)    timeout -k 10 900 python -u $arg > "$OUT/py_$n.log" 2>&1 || { echo "py failed rc=$?"; tail -30 "$OUT/py_$n.log"; exit 1; }
+           tail -40 "$OUT/py_$n.log" ;;
+    *) echo "unknown step $kind"; exit 2 ;;
+  esac
+done
+echo all-done

@@ -5,7 +5,11 @@ costs the sum of the P slabs' kernels plus the copies; step_ms / P estimates the
 of a P-GPU run (RCCL transfer time excluded).  Per-kernel-class times come from the contexts' HIP-event
 profiles (pdhg_profile_query), summed over slabs and divided by P.
 
-usage: python scripts/slab_local_bench.py [tslab|xslab] [config] [P] [steps]
+mode "multi": the same t-slabs driven by the native multi-device context (pdhg_create_multi with the device
+list [0] * P: one host thread, per-slab main + side streams, per-neighbour events), with the per-phase times
+of slab 0's stream (pdhg_multi_phase_ms: cross-slab waits included).
+
+usage: python scripts/slab_local_bench.py [tslab|xslab|multi] [config] [P] [steps]
 """
 import json
 import os
@@ -31,6 +35,26 @@ def main():
     xs, ys = bench.grid(ndim, nx, ny)
     dt = 1.0 / (nt - 1)
     g = np.sin(np.pi * xs)[:, None] + np.sin(np.pi * ys)[None, :]
+    if mode == "multi":
+        from pdhg_amd.multi import MultiContext
+        m = MultiContext(egno, nx, ny, T, 2.0 / nx, 2.0 / ny, dt, xs, ys, devices=[0] * P, epsl=epsl)
+        m.init_state(g)
+        m.set_stop_rules(converge=True, nan=False)
+        tau, sigma = 0.1 / 1.5, 0.1 * 1.5
+        m.iterate(2, tau, sigma, 1e-6, 1)
+        m.synchronize()
+        m.profile(True)
+        t0 = time.perf_counter()
+        st = m.iterate(steps, tau, sigma, 1e-6, 1)
+        m.synchronize()
+        el = time.perf_counter() - t0
+        ph = {k: v / steps for k, v in m.phase_ms(reset=False).items()}
+        print(json.dumps({"mode": mode, "config": cfg, "P": P, "steps": steps, "iters": st["iters_run"],
+                          "step_ms": el / steps * 1e3, "per_slab_ms": el / steps * 1e3 / P,
+                          "long_modes": m.info("long_modes"), "parts": m.info("parts"),
+                          "phase_ms_slab0_stream": ph}), flush=True)
+        m.close()
+        return
     if mode == "tslab":
         from pdhg_amd.slab import LocalComm, SlabContext, SlabRunner
         slabs = [SlabContext(r, P, T, egno, nx, ny, 2.0 / nx, 2.0 / ny, dt, xs, ys, epsl=epsl) for r in range(P)]

@@ -1,5 +1,7 @@
+import json
 import os
 import sys
+import time
 
 import pytest
 
@@ -25,3 +27,21 @@ def native():
     if _native.device_count() < 1:
         pytest.fail("gpu test selected but no HIP device is visible")
     return _native
+
+
+@pytest.fixture(scope="session")
+def parity_log():
+    """Append one JSON line per measured parity case to $PDHG_PARITY_LOG (default gpurun_out/parity.jsonl):
+    the achieved errors and the bounds they were held to, so the numbers outlive pytest's stdout
+    (profiles/parity_r03.json is made from this file)."""
+    path = os.environ.get("PDHG_PARITY_LOG", os.path.join(ROOT, "gpurun_out", "parity.jsonl"))
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+
+    def record(test, case, measured, bounds, **extra):
+        row = {"test": test, "case": case, "time": time.strftime("%Y-%m-%dT%H:%M:%S"),
+               "measured": {k: float(v) for k, v in measured.items()},
+               "bounds": {k: float(v) for k, v in bounds.items()}}
+        row.update(extra)
+        with open(path, "a") as fh:
+            fh.write(json.dumps(row) + "\n")
+    return record

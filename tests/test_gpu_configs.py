@@ -21,17 +21,28 @@ same oracle executed in float32 (complex64 FFTs and Thomas) lands from its float
 the reference algorithm itself reaches in float32.  The device runs the same iterations in fp32 and is
 compared on those points.
 
-Bounds (relative L2 over the sampled points): the larger of a fixed bound and K32 = 4 x e32 of that
-quantity ("the fp32 device agrees with the fp64 reference within 4x of the reference run in fp32"):
-  fixed: phi after the first primal update 1e-6, phi after the run 1e-5 (the north-star bound), rho 1e-5
-  and each live alp array 1e-4 from the reference state; from the seeded rough state the primal update
-  U itself 5e-4 and rho / alp 2e-4 / 1e-3 (test_gpu_parity's fp32 bounds for that state); err1 1e-3.
-  e32 is large where the problem is ill-conditioned at these sizes: with epsl = 0.1 the reference's
-  explicit sigma*epsl*Lap(phi_bar) dual term amplifies rounding by ~sigma*epsl*8/dx^2 = 5e5 per iteration
-  at dx = 2/4096 (rho after one iteration: e32 = 4.9e-5; the fp64 oracle moves by 14 % after two under a
-  single float32 rounding of its input); from a rough state the H1 preconditioner recovers the low modes of
-  U from a residual dominated by high ones (phi' of the seeded C3 state: e32 = 1.5e-5); the controls follow
-  one-sided differences of phi_bar whose float32 precision is ulp(phi)/(dx*|grad phi|) (~1e-3 at C1).
+Bounds (relative L2 over the sampled points; every achieved value is also written to
+gpurun_out/parity.jsonl -> profiles/parity_r03.json):
+  phi, epsl = 0 runs (the ref state and the seeded rough state): FIXED 1e-6 after the first primal
+  update and 1e-5 (the north-star bound) after the run, on every default kernel path -- no e32 escape.
+  Measured on the device (round 3): ref runs 5e-8 - 4.4e-7 (C1 2.5e-7, C3-T200 1.3e-7), seeded C1
+  6.4e-6, C2 3.3e-8.  The float32 ORACLE is worse than that at T = 200 / 400 (e32 = 1.6e-5 at C3-T200,
+  4.7e-5 at C1): tests/golden/precision_study.py locates all of it in the reference's Thomas recurrence
+  (utils_precond.py:10-35) run in float32 -- with the Thomas solve alone in float64 the float32 oracle
+  lands at 4.1e-7 -- while the device's cancellation-free pivot recurrence with closed-form backward
+  pivots, emulated in float32 by the same study ("dth32"), lands at 5.7e-7.
+  Other quantities keep max(fixed, K32 x e32), K32 = 4, because fp32 storage itself limits them:
+  rho, epsl = 0.1: the explicit sigma*epsl*Lap(phi_bar) dual term amplifies the float32 representation
+    of phi_bar by ~sigma*epsl*8/dx^2 = 5e5 at dx = 2/4096 (rho after one iteration: 4.9e-5 in the
+    float32 oracle and on the device; 3e-8 with phi / phi_bar alone held in float64, precision_study
+    "phi64");
+  alp: the controls follow one-sided differences of phi_bar, whose float32 precision is
+    ulp(phi)/(dx |grad phi|) (9.4e-4 at C1's dx = 2/65536; 4.9e-5 with phi in float64);
+  phi, epsl = 0.1 seeded runs: from a rough state the residual is dominated by the epsl*Lap(rho) term
+    at high frequency (|R| ~ 1e7) while U = H1^-1 R lives in the low modes, so the float32 rounding of R
+    itself bounds U (U1 1.1e-4 in the float32 oracle, 1.2e-4 on the device; phi1 1.4e-5 / 1.5e-5 at
+    C3-T200): precision_study moves it neither with the transforms in float64 (1.4e-5) nor with the
+    t-solve in float64 (1.7e-5), only with rho and the residual in float64 (2e-10).
 Runs with epsl = 0.1 therefore stop after one iteration; test_one_step_eps below checks a further
 iteration (the fused residual formed by the first dual sweep) from the device's own state, against the
 oracle in float64 and in float32 from that state.
@@ -79,6 +90,11 @@ CASES = {
 }
 
 
+# non-default schedules whose phi keeps the e32 escape on epsl = 0 runs: the one-thread-per-mode 1-D t-solve
+# (PDHG_THOMAS_CHUNK=0; measured 1.6e-5 on C1's seeded state against 6.4e-6 for the default chunked solve)
+PHI_E32_ESCAPE = {"c1_exact@thomas1"}
+
+
 def _fixture(name):
     path = os.path.join(HERE, "golden", "cfg_{}.npz".format(name))
     if not os.path.exists(path):
@@ -102,7 +118,7 @@ def _norm_dev(x, ref_norm):
 
 
 @pytest.mark.parametrize("name", list(CASES))
-def test_config_instantiation(native, name, monkeypatch):
+def test_config_instantiation(native, name, monkeypatch, parity_log):
     env, expect = CASES[name]
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -114,7 +130,11 @@ def test_config_instantiation(native, name, monkeypatch):
         epsl, n, seeded = float(g("epsl")), int(g("iters")), bool(int(g("seeded")))
         ip, ir = g("idx_phi"), g("idx_rho")
         e32 = g("e32")    # [phi1, U1, phi, rho, alp0.., err1]
-        tol = {"phi1": max(1e-6, K32 * e32[0]), "U1": max(5e-4, K32 * e32[1]), "phi": max(1e-5, K32 * e32[2]),
+        # phi: the north-star bound 1e-5 (1e-6 after the first update) as a FIXED bound on every epsl = 0 run
+        # (ref and seeded), no e32 escape; runs with epsl > 0 keep the escape (see the module docstring)
+        fixed_phi = epsl == 0.0 and name not in PHI_E32_ESCAPE
+        tol = {"phi1": 1e-6 if fixed_phi else max(1e-6, K32 * e32[0]), "U1": max(5e-4, K32 * e32[1]),
+               "phi": 1e-5 if fixed_phi else max(1e-5, K32 * e32[2]),
                "rho": max(2e-4 if seeded else 1e-5, K32 * e32[3]), "err1": max(1e-3, K32 * e32[-1])}
         for a in range(len(e32) - 5):
             tol["alp{}".format(a)] = max(1e-3 if seeded else 1e-4, K32 * e32[4 + a])
@@ -147,6 +167,9 @@ def test_config_instantiation(native, name, monkeypatch):
             ctx.close()
         print("CFG {} {}: {} | e32 {}".format(name, tag, " ".join("{}={:.2e}".format(k, v) for k, v in m.items()),
                                               " ".join("{:.1e}".format(v) for v in e32)), flush=True)
+        parity_log("test_config_instantiation", "{}/{}".format(name, tag), m,
+                   {k: tol[k[:-5] if k.endswith("_norm") else k] for k in m}, e32=[float(v) for v in e32],
+                   iters=n, epsl=epsl, seeded=seeded)
         if not (st["iters_run"] == n and st["status"] == 0 and not st["nan_seen"]):
             failures.append((tag, "run", st))
         for k, v in m.items():
@@ -216,7 +239,7 @@ def test_dma_x_transform_matches_batched(native, monkeypatch, T):
 
 
 @pytest.mark.parametrize("name", list(ONE_STEP))
-def test_one_step_eps(native, name, monkeypatch):
+def test_one_step_eps(native, name, monkeypatch, parity_log):
     """Device iteration 2 vs one oracle iteration from the device's iteration-1 state (float32 values, so the
     oracle starts from exactly the device's state).  Bounds: the larger of the seeded-state bounds (phi 1e-5,
     rho 2e-4, alp 1e-3) and K32 x the distance between that oracle step in float32 and in float64."""
@@ -254,6 +277,7 @@ def test_one_step_eps(native, name, monkeypatch):
     for a in range(4):
         if np.linalg.norm(live_o[a]) > 0:
             m["alp{}".format(a)] = (rel(live_d[a], live_o[a]), max(1e-3, K32 * rel(live_p[a], live_o[a])))
+    parity_log("test_one_step_eps", name, {k: v for k, (v, b) in m.items()}, {k: b for k, (v, b) in m.items()})
     print("ONESTEP {}: {}".format(name, " ".join("{}={:.2e}(<{:.1e})".format(k, v, b) for k, (v, b) in m.items())),
           flush=True)
     assert all(v <= b for v, b in m.values()), m

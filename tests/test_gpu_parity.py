@@ -387,7 +387,7 @@ PRECOND_1D = [   # (C, pow, Ct): utils_precond.py:125-134, run_example.py:436-43
 @pytest.mark.parametrize("cpc", PRECOND_1D, ids=["C{}_pow{}_Ct{}".format(*c) for c in PRECOND_1D])
 @pytest.mark.parametrize("prec", ["fp64", "fp32"])
 @pytest.mark.parametrize("case", [(1, 1, 256, 1, 8, 0.0), (2, 1, 65536, 1, 6, 0.0)], ids=["e1_256_T8", "e2_65536_T6"])
-def test_precond_1d_parameters(native, case, prec, cpc):
+def test_precond_1d_parameters(native, case, prec, cpc, parity_log):
     """H1_precond_1d with non-default C, pow and Ct (diagonal (C - fv)^pow + Ct * Lap_t, off-diagonals
     -Ct/dt^2; Ct = 0 decouples the time rows): the primal update and 3 iterations vs the oracle.  fp64
     <= 1e-10 (x10 at 65536 points, see _big); fp32 from the seeded state: phi' <= max(1e-6, 4 e32) and
@@ -440,6 +440,10 @@ def test_precond_1d_parameters(native, case, prec, cpc):
                                 P["x_arr"].astype(f), None, 1, -1.0)
                 p32 = pn
             e_phi, e_rho = rel(p32, phi), rel(r32, rho)
+            parity_log("test_precond_1d_parameters", "{}_{}_C{}_pow{}_Ct{}".format(case[2], case[4], *cpc),
+                       {"phi": rel(phi_d, phi), "rho": rel(rho_d, rho)}, {"phi": max(1e-5, 8 * e_phi),
+                                                                          "rho": max(2e-4, 8 * e_rho)},
+                       e32={"phi": e_phi, "rho": e_rho})
             # x8: with Ct = 0 at 65536 points the device's 65536-point four-step DHT (twiddled fp32 passes)
             # rounds deeper than the oracle's float32 FFT and the decoupled low modes amplify it (measured 3.6-4.4x)
             assert rel(phi_d, phi) < max(1e-5, 8 * e_phi), (rel(phi_d, phi), e_phi)
