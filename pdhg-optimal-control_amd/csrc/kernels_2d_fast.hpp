@@ -364,13 +364,15 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
     const int nxt = min(task + (int)gridDim.x, ntask - 1);
     load_rows(nxt, 0, RSPLIT);
     lds_sync();
-    if constexpr (TWL) lds_fft_inplace_tl<C, N, NL, NT>(A, twl);
-    else lds_fft_inplace<C, N, NL, NT>(A, twy);
+    if (!(p.dbg & 16)) {   // timing experiments only (PDHG_DBG): 16 skips the transform
+      if constexpr (TWL) lds_fft_inplace_tl<C, N, NL, NT>(A, twl);
+      else lds_fft_inplace<C, N, NL, NT>(A, twy);
+    }
     if (tid < NEY) eyl[buf ^ 1][tid] = ev;   // read one barrier after its last use two tasks ago
     if constexpr (RSPLIT < RW) load_rows(nxt, RSPLIT, RW);
     load_edges(nxt);
     float* wk = p.work + (size_t)j * nb * nx * B;
-    for (int t = tid; t < nb * CS4; t += NT) {
+    for (int t = tid; t < nb * CS4 && !(p.dbg & 32); t += NT) {   // PDHG_DBG 32: no unpack / stores (timing)
       const int b = t >> lCS4, part = t & (CS4 - 1);
       float4 v;
 #pragma unroll
@@ -456,8 +458,10 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
     float4 nx0, nx1;
     ldpair(0, 0, nx0, nx1);
     lds_sync();
-    if constexpr (TWL) lds_fft_inplace_tl<C, N, NL, NT>(A, twl);
-    else lds_fft_inplace<C, N, NL, NT>(A, twy);
+    if (!(p.dbg & 64)) {   // timing experiments only (PDHG_DBG): 64 skips the transform
+      if constexpr (TWL) lds_fft_inplace_tl<C, N, NL, NT>(A, twl);
+      else lds_fft_inplace<C, N, NL, NT>(A, twy);
+    }
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
       const int y = 4 * (tid + gi * NT);

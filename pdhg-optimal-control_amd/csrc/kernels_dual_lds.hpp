@@ -180,13 +180,13 @@ __global__ void __launch_bounds__(RX * 64, FR ? 2 : 3) k_dual_lds_2d(KP<float> p
         for (int i = 0; i < NS; ++i) s[i] += (double)fs[i];
       }
       const size_t o = (size_t)j * plane + rxc + y;
-      if (live) {
+      if (live && !(p.dbg & 128)) {   // PDHG_DBG 128: no rho / alp stores (timing experiments only)
         st4(rd + o, rn4);
 #pragma unroll
         for (int a = 0; a < NA; ++a) st4(ad[a] + o, an4[a]);
       }
       f0 = pc;
-      if constexpr (FR) {
+      if constexpr (FR) if (!(p.dbg & 256)) {   // PDHG_DBG 256: no residual / edge terms (timing only)
         if (j > j0) finish_res(j - 1, buf ^ 1, rn4, 0.f);   // row j-1, with rho'_j
         flux[buf][r][0][lane] = rn4;
         flux[buf][r][1][lane] = m1x4;

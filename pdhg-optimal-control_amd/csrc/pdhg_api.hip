@@ -24,6 +24,7 @@
 #include "kernels_thomas_chunk.hpp"
 #include "kernels_fs_wide.hpp"
 #include "kernels_fs16.hpp"
+#include "kernels_xt_f64.hpp"
 
 using namespace pdhg;
 
@@ -136,6 +137,7 @@ struct Impl : ImplBase {
   int xt_rpre = 0;
   bool xt_pair = false;           // batched x transform as 2 rows x 512 threads, two workgroups per CU
   bool xt_dma = false;            // x transform with the rows staged HBM -> LDS by DMA (k_precond_xt_dma_2d)
+  bool f64_xt = false;            // fp64 nx = 4096: in-place line + register carries (k_precond_xt_f64_2d)
   bool thomas_chunk = false;      // 1-D fp32: t-solve in chunks of 32 rows (k_thomas_chunk_1d)
   bool fs_wide = true;            // four-step DHT with 64-column / 32-row tiles (k_fs1w_1d / k_fs2w_1d)
   int f16_group = 16;             // rows n1 per load group of k_f16a_fwd_1d (PDHG_F16_GROUP: 4, 8, 16; 16 measured best)
@@ -173,6 +175,7 @@ struct Impl : ImplBase {
 
   ~Impl() override {
     if (stream) hipStreamSynchronize(stream);
+    drop_graph();
     for (void* p : allocs) hipFree(p);
     for (auto& kv : prof_ev)
       for (auto& e : kv.second.ev) {
@@ -247,7 +250,10 @@ struct Impl : ImplBase {
       // fp32 nx = 8192 (C4): one real column per block, packed into a 4096-point FFT (half_real)
       half_real = sizeof(R) == 4 && nxg == 8192 && pb.bc_x == 0;
       if (half_real) B = 1;
-      if (!half_real && (size_t)nxg * B > cap)
+      // fp64 nx = 4096 (C3's grid in the reference's precision): k_precond_xt_f64_2d keeps the carries in
+      // registers, so the column pair (B = 2) fits LDS although 5 M reals would not
+      f64_xt = sizeof(R) == 8 && nxg == 4096 && pb.bc_x == 0 && !xslab && !slab && B == 2;
+      if (!half_real && !f64_xt && (size_t)nxg * B > cap)
         return fail(PDHG_ERR_UNSUPPORTED, "nx=%d too large for the x-transform slab (max %zu in this precision)", nxg,
                     cap / 2);
       p.half_real = half_real ? 1 : 0;
@@ -771,6 +777,18 @@ struct Impl : ImplBase {
         return PDHG_OK;
       }
     }
+    if constexpr (sizeof(R) == 8) {
+      if (f64_xt) {
+        ProfScope ps(this, "precond");
+        if (p.xt_phase != 0 || p.b0 != 0 || nblk != p.nb)
+          return fail(PDHG_ERR_UNSUPPORTED, "the fp64 nx = 4096 x transform runs whole windows only");
+        const size_t lds = (size_t)(Pad<4096>::LINE + TwLds<4096>::SIZE) * sizeof(C);
+        if ((rc = ensure_lds(k_precond_xt_f64_2d<4096, 512>, lds))) return rc;
+        hipLaunchKernelGGL((k_precond_xt_f64_2d<4096, 512>), dim3(nblk), dim3(512), lds, stream, p, twx);
+        HIP_TRY(hipGetLastError());
+        return PDHG_OK;
+      }
+    }
     if (fast_xt) {
       ProfScope ps(this, "precond");
       rc = PDHG_OK;
@@ -1158,18 +1176,82 @@ struct Impl : ImplBase {
     return PDHG_OK;
   }
 
+  // ---------------- iteration chunks replayed from a HIP graph ----------------
+  // The launch chain of `window` outer iterations (primal, <= k dual sub-iterations, outer tests: 8-12
+  // kernels each) is captured once per (tau, sigma, eps, k) and replayed with one hipGraphLaunch, so the
+  // host issues one call per window instead of ~10 per iteration -- the marching default's T = 1 windows
+  // and small grids are launch-bound (utils_pdhg_solver.py:166-212 runs up to N_maxiter iterations per
+  // window).  The device-side stop flags (Ctrl) make the kernels after convergence no-ops, exactly as in the
+  // eager loop, so a replayed chunk needs no host decision.  Captured only with the fused residual valid
+  // (or not in use) so every captured primal is the steady-state one; off while profiling (per-launch
+  // events) and with PDHG_GRAPH=0.
+  hipGraphExec_t gexec = nullptr;
+  double g_tau = 0, g_sigma = 0, g_eps = 0;
+  int g_k = 0, g_window = 0, g_stop = -1;
+  bool use_graph = true;
+  bool warm = false;   // one eager iteration ran (kernel attributes set outside any capture)
+  void drop_graph() {
+    if (gexec) hipGraphExecDestroy(gexec);
+    gexec = nullptr;
+  }
+  int launch_iteration(double tau, double sigma, double eps, int k) {
+    int rc;
+    if ((rc = launch_primal((R)tau))) return rc;
+    if ((rc = launch_dual((R)sigma, eps, k))) return rc;
+    return launch_outer(eps, k);
+  }
+  int ensure_graph(double tau, double sigma, double eps, int k, int window) {
+    const int stop = stop_conv * 2 + stop_nan;   // kernel arguments of k_finalize_outer
+    if (gexec && g_tau == tau && g_sigma == sigma && g_eps == eps && g_k == k && g_window == window && g_stop == stop)
+      return PDHG_OK;
+    drop_graph();
+    hipGraph_t g = nullptr;
+    HIP_TRY(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    int rc = PDHG_OK;
+    for (int i = 0; i < window && rc == PDHG_OK; ++i) rc = launch_iteration(tau, sigma, eps, k);
+    hipError_t e = hipStreamEndCapture(stream, &g);
+    if (rc) {
+      if (g) hipGraphDestroy(g);
+      return rc;
+    }
+    HIP_TRY(e);
+    e = hipGraphInstantiate(&gexec, g, nullptr, nullptr, 0);
+    hipGraphDestroy(g);
+    if (e != hipSuccess) {
+      gexec = nullptr;
+      return fail(PDHG_ERR_HIP, "hipGraphInstantiate failed: %s", hipGetErrorString(e));
+    }
+    g_tau = tau;
+    g_sigma = sigma;
+    g_eps = eps;
+    g_k = k;
+    g_window = window;
+    g_stop = stop;
+    return PDHG_OK;
+  }
+
   int iterate(int n, double tau, double sigma, double eps, int k, pdhg_stats* st) {
     int rc;
     if ((rc = reset_ctrl())) return rc;
     const int window = 8;   // host runs at most 2*window iterations ahead of the device
     std::vector<hipEvent_t> evs;
     int ran = 0;
-    for (int i = 0; i < n; ++i) {
-      if ((rc = launch_primal((R)tau))) return rc;
-      if ((rc = launch_dual((R)sigma, eps, k))) return rc;
-      if ((rc = launch_outer(eps, k))) return rc;
-      ++ran;
-      if ((i + 1) % window == 0 && i + 1 < n) {
+    if (const char* e = getenv("PDHG_GRAPH")) use_graph = atoi(e) != 0;
+    for (int i = 0; i < n;) {
+      // a whole window from the graph when one fits and the state allows it; otherwise one eager iteration
+      const bool steady = !fuse_res || res_valid;
+      if (use_graph && warm && !prof && steady && i % window == 0 && n - i >= window) {
+        if ((rc = ensure_graph(tau, sigma, eps, k, window))) return rc;
+        HIP_TRY(hipGraphLaunch(gexec, stream));
+        i += window;
+        ran += window;
+      } else {
+        if ((rc = launch_iteration(tau, sigma, eps, k))) return rc;
+        warm = true;
+        ++i;
+        ++ran;
+      }
+      if (i % window == 0 && i < n) {
         hipEvent_t e;
         HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(e, stream));
@@ -1924,6 +2006,9 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
                                                            im.fuse_res) ? 512 : im.NTf) : 0;
     else if (k == "upd_threads") *value = im.fast_rows ? ((im.NTf == 1024 && im.RWf == 8 && (im.half_nt & 2))
                                                               ? 512 : im.NTf) : 0;
+    else if (k == "f64_xt") *value = im.f64_xt ? 1 : 0;   // fp64 nx = 4096 x transform (kernels_xt_f64.hpp)
+    else if (k == "graph") *value = im.use_graph ? 1 : 0;   // iteration windows replayed from a HIP graph
+    else if (k == "graph_window") *value = im.gexec ? im.g_window : 0;   // 0: no graph captured yet
     else return fail(PDHG_ERR_ARG, "unknown path key %s", key);
     return (int)PDHG_OK;
   });

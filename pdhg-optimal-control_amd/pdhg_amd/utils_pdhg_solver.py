@@ -157,10 +157,11 @@ def PDHG_multi_step(fn_update_primal, fn_update_dual, fns_dict, g, x_arr, ndim, 
     init_t = 0
     phi_end = None
     if load_middle_dir is not None and load_middle_prefix is not None:
-        # middle results: [max_iters, phi_all, rho_all, alp_all, errs_all, phi_end, stepsz_param]; phi_all keeps
-        # phi_c[:-1] for every window but the last (utils_pdhg_solver.py:192-195), so the end row the next
-        # window starts from is saved on its own (phi_end).  The reference restarts from phi_all[-1:]
-        # (:146-150), which is the previous window's start, not its end.
+        # middle results: [max_iters, phi_all, rho_all, alp_all, errs_all, phi0_next, stepsz_param]; phi_all keeps
+        # phi_c[:-1] for every window but the last (utils_pdhg_solver.py:192-195), so the warm start the next
+        # window begins from (phi0 + (phi_c[-1:] - phi0[0:1]), :201-203) is saved whole (phi0_next) and restored
+        # bit for bit.  The reference restarts from phi_all[-1:] (:146-150), which is the previous window's
+        # start, not its end.  Files of round 2 hold only the end row there (shape [1, ...]): it is repeated.
         middle = load_middle_solution(load_middle_dir, load_middle_prefix)
         max_iters, phi_all, rho_all, alp_all, errs_all = middle[:5]
         init_t = len(phi_all)
@@ -170,7 +171,10 @@ def PDHG_multi_step(fn_update_primal, fn_update_dual, fns_dict, g, x_arr, ndim, 
                 raise ValueError("middle results {}/{} hold no end row of window {} (saved without phi_end); "
                                  "cannot resume".format(load_middle_dir, load_middle_prefix, init_t - 1))
             phi_end, stepsz_param = np.asarray(middle[5], dtype=np.float64), float(middle[6])
-            phi0 = np.repeat(phi_end.reshape((1,) + phi0.shape[1:]), time_step_per_PDHG, axis=0)
+            if phi_end.shape == phi0.shape:
+                phi0 = phi_end.copy()
+            else:
+                phi0 = np.repeat(phi_end.reshape((1,) + phi0.shape[1:]), time_step_per_PDHG, axis=0)
             rho0 = rho_all[-1]
             alp0 = tuple(alp_all[-1][i] for i in range(n_alp))
     s_delta = stepsz_param / 10
@@ -202,7 +206,7 @@ def PDHG_multi_step(fn_update_primal, fn_update_dual, fns_dict, g, x_arr, ndim, 
                 errs_all.append(errs)
                 phi0 = phi0 + (phi_c[-1:] - phi0[0:1])        # warm start, :201-203
                 rho0, alp0 = rho_c, alp_c
-                phi_end = phi0[0:1].copy()   # = phi_c[-1:] up to the warm start's roundoff
+                phi_end = phi0.copy()        # the next window's warm start, saved whole
                 break
         if save_middle_dir is not None and save_middle_prefix is not None and phi_end is not None:
             save(save_middle_dir, save_middle_prefix,

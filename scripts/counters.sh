@@ -8,10 +8,11 @@ REPO=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$REPO/gpurun_out/cnt_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-ARGS="$REPO/bench.py --config $CFG --steps 2 --warmup 1 --no-cpu-baseline --no-pmc"
+ARGS="$REPO/bench.py --config $CFG --steps 2 --warmup 1 --no-cpu-baseline --no-pmc --no-probe"
+timeout -s KILL 60 rocprofv3 -L > "$OUT/counters_available.txt" 2>&1 || true
 i=0
 for C in "$@"; do
-  timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d "$OUT/g$i" -o run -- python3 $ARGS > "$OUT/g$i.log" 2>&1 || exit 1
+  timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d "$OUT/g$i" -o run -- python3 $ARGS > "$OUT/g$i.log" 2>&1 || exit 1
   i=$((i+1))
 done
 echo "counters done: $OUT"

@@ -5,6 +5,7 @@
 #   tests[:<pytest -k>]   pytest -m gpu (optionally filtered)
 #   bench[:<args>]        python bench.py <args, commas for spaces>  -> bench_<n>.json
 #   prof:<config>         scripts/profile.sh <config> <tag>
+#   sh:<script>,<args>    bash <script> <args> ('+' inside an argument stands for a space: counter groups)
 # Every GPU step runs under its own time limit; the first failure ends the script.
 set -o pipefail
 TAG=$1; shift
@@ -29,6 +30,9 @@ for step in "$@"; do
            cd "$REPO" ;;
     py)    timeout -k 10 900 python -u $arg > "$OUT/py_$n.log" 2>&1 || { echo "py failed rc=$?"; tail -30 "$OUT/py_$n.log"; exit 1; }
            tail -40 "$OUT/py_$n.log" ;;
+    sh)    read -ra TOK <<< "$arg"; TOK=("${TOK[@]//+/ }")
+           timeout -k 10 1100 bash "${TOK[@]}" > "$OUT/sh_$n.log" 2>&1 || { echo "sh failed rc=$?"; tail -20 "$OUT/sh_$n.log"; exit 1; }
+           tail -5 "$OUT/sh_$n.log"; cd "$REPO" ;;
     *) echo "unknown step $kind"; exit 2 ;;
   esac
 done

@@ -1,0 +1,85 @@
+"""Fixture pinning the reference algorithm's divergence on C3's FULL spatial plane (BASELINE.json configs[3]:
+egno 2, ndim 2, epsl 0.1, nx = ny = 4096, dt = 1/200 as nt = 201).
+
+The bench times C3 as one window of T = 200 rows and reports the first iteration at which phi' or rho'
+turns non-finite (11 on the device).  That is the reference's own instability: its dual step holds the
+explicit sigma*epsl*Lap(phi_bar) term (update_fns_in_pdhg.py:58-70), whose amplification sigma*epsl*8/dx^2
+~ 5e5 per iteration at dx = 2/4096 no step size in the reference's back-off range cures.  This script runs
+the float64 oracle on the 4096^2 plane with a short window (T = 4 rows, the same dt) from the reference
+initial state (phi = g, rho = 70, alp = 0; utils_pdhg_solver.py:123-137), one rho_alp_iter, until phi' or
+rho' holds a NaN -- the reference's own test, jnp.isnan (utils_pdhg_solver.py:78-80), which an inf does not
+trip -- and stores per iteration: |phi'|, |rho'|, |alp'| (Frobenius over the finite entries), err1, err2,
+whether every entry of phi' and rho' is finite, and the first NaN iteration ("first_nonfinite", the name the
+bench uses for the same event).  tests/test_gpu_divergence.py runs the device (fp32 and fp64) on
+the same window and compares.
+
+Run:  python tests/golden/make_divergence_fixture.py [T] [max_iters]     (~1 min per iteration at T = 4)
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "..", "oracle"))
+import pdhg_oracle as O  # noqa: E402
+
+TAU, SIGMA = 0.1 / 1.5, 0.1 * 1.5
+
+
+def setup(nx, ny, T, dt, epsl):
+    egno, ndim = 2, 2
+    x_arr = O.make_grid(ndim, nx, ny, egno)
+    g = O.set_up_J(egno, ndim, (2.0, 2.0))(x_arr)
+    fns = O.set_up_example_fns(egno, ndim, 0)
+    dsp = (2.0 / nx, 2.0 / ny)
+    bc = O.default_bc(egno, ndim)
+    fv = O.compute_Dxx_fft_fv(ndim, (nx, ny), dsp, bc)
+    primal, dual = O.make_update_fns(ndim, bc, rho_alp_iters=1)
+    phi = np.repeat(g, T + 1, axis=0)
+    rho = np.full((T, nx, ny), 70.0)
+    alp = tuple(np.zeros((T, nx, ny, 2)) for _ in range(4))
+    return dict(x_arr=x_arr, g=g, fns=fns, dsp=dsp, fv=fv, primal=primal, dual=dual, phi=phi, rho=rho, alp=alp,
+                dt=dt, epsl=epsl)
+
+
+def run(S, max_iters, log=True):
+    phi, rho, alp = S["phi"], S["rho"], S["alp"]
+    rows = []
+    first = 0
+    t0 = time.time()
+    for it in range(1, max_iters + 1):
+        phi_n = S["primal"](phi, rho, 70.0, alp, TAU, S["dt"], S["dsp"], S["fns"], S["fv"], S["epsl"], S["x_arr"],
+                            None)
+        with np.errstate(all="ignore"):
+            rho_n, alp_n = S["dual"](2 * phi_n - phi, rho, 70.0, alp, SIGMA, S["dt"], S["dsp"], S["epsl"], S["fns"],
+                                     S["x_arr"], None, 2, -1.0)
+            e1, e2 = O.outer_errors(phi, phi_n, rho, rho_n, alp, alp_n)
+            fin = bool(np.isfinite(phi_n).all() and np.isfinite(rho_n).all())
+            nan = bool(np.isnan(phi_n).any() or np.isnan(rho_n).any())
+            nphi = float(np.linalg.norm(phi_n[np.isfinite(phi_n)]))
+            nrho = float(np.linalg.norm(rho_n[np.isfinite(rho_n)]))
+            nalp = float(np.sqrt(sum(np.sum(np.where(np.isfinite(a), a, 0.0) ** 2) for a in alp_n)))
+        rows.append([it, nphi, nrho, nalp, e1, e2, 1.0 if fin else 0.0])
+        if log:
+            print("it {:3d} |phi| {:.6e} |rho| {:.6e} |alp| {:.6e} err1 {:.3e} err2 {:.3e} finite {} nan {} ({:.0f} s)"
+                  .format(it, nphi, nrho, nalp, e1, e2, fin, nan, time.time() - t0), flush=True)
+        phi, rho, alp = phi_n, rho_n, alp_n
+        if nan:
+            first = it
+            break
+    return np.array(rows), first
+
+
+if __name__ == "__main__":
+    T = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    max_iters = int(sys.argv[2]) if len(sys.argv) > 2 else 40
+    nx = ny = 4096
+    S = setup(nx, ny, T, 1.0 / 200, 0.1)
+    rows, first = run(S, max_iters)
+    out = os.path.join(HERE, "divergence_c3_plane_T{}.npz".format(T))
+    np.savez_compressed(out, rows=rows, first_nonfinite=first, meta=np.array([2, 2, nx, ny, T]), dt=1.0 / 200,
+                        epsl=0.1, tau=TAU, sigma=SIGMA,
+                        columns=np.array(["iter", "phi_norm", "rho_norm", "alp_norm", "err1", "err2", "finite"]))
+    print("wrote", out, "first non-finite iteration", first, flush=True)

@@ -450,3 +450,54 @@ def test_precond_1d_parameters(native, case, prec, cpc, parity_log):
             assert rel(rho_d, rho) < max(2e-4, 8 * e_rho), (rel(rho_d, rho), e_rho)
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("case", [(1, 1, 160, 1, 1, 0.0), (2, 2, 64, 48, 1, 0.1), (1, 2, 256, 256, 6, 0.0)],
+                         ids=["c0_1d_T1", "e2_2d_T1", "e1_2d_fused_T6"])
+def test_graph_replay_matches_eager(native, monkeypatch, case):
+    """iterate() replays windows of 8 iterations from a captured HIP graph (PDHG_GRAPH, default on): the
+    same kernels with the same arguments as the eager loop, so the state is bit-identical, and the device
+    stop flags end a converging run at the same iteration even inside a replayed window (the converge test
+    of utils_pdhg_solver.py:74-76 with eps = 1e-3: wherever it fires, both loops must stop there)."""
+    egno, ndim, nx, ny, T, epsl = case
+    P = make_problem(egno, ndim, nx, ny, T, epsl, seeded=False)
+    out = []
+    for g in ("0", "1"):
+        monkeypatch.setenv("PDHG_GRAPH", g)
+        ctx = device_ctx(P, "fp32")
+        try:
+            ctx.set_state(P["phi"], P["rho"], P["alp"])
+            a = ctx.iterate(37, TAU, SIGMA, -1.0, 1)        # no stop: 37 = 4 windows + 5 eager
+            b = ctx.iterate(400, TAU, SIGMA, 1e-3, 1)       # stops on convergence (or runs out)
+            assert ctx.path_info("graph") == int(g)
+            if g == "1":
+                assert ctx.path_info("graph_window") == 8
+            out.append((a, b, ctx.get_state()))
+        finally:
+            ctx.close()
+    (a0, b0, s0), (a1, b1, s1) = out
+    assert a0["iters_run"] == a1["iters_run"] == 37
+    assert b0["iters_run"] == b1["iters_run"] and b0["status"] == b1["status"], (b0, b1)
+    assert b0["err1"] == b1["err1"] and b0["err2"] == b1["err2"]
+    assert np.array_equal(s0[0], s1[0]) and np.array_equal(s0[1], s1[1])
+
+
+@pytest.mark.parametrize("case", [(2, 2, 4096, 16, 6, 0.0), (1, 2, 4096, 32, 3, 0.0), (2, 2, 4096, 8, 1, 0.0)],
+                         ids=["e2_4096x16_T6", "e1_4096x32_T3", "e2_4096x8_T1"])
+def test_fp64_nx4096_x_transform(native, case):
+    """The reference's precision on C3's x extent: fp64 at nx = 4096 runs k_precond_xt_f64_2d (in-place LDS
+    line, Thomas carries in registers; the generic fp64 kernel stops at nx = 2048), 10 iterations from the
+    seeded rough state against the fp64 oracle at the fp64 bars of test_iterate_10."""
+    P = make_problem(*case)
+    phi_o, rho_o, alp_o, e1_o, e2_o = _oracle_iterate(P, 10)
+    ctx = device_ctx(P, "fp64")
+    try:
+        assert ctx.path_info("f64_xt") == 1
+        ctx.set_state(P["phi"], P["rho"], P["alp"])
+        st = ctx.iterate(10, TAU, SIGMA, -1.0, 1)
+        assert st["iters_run"] == 10 and st["status"] == 0
+        phi_d, rho_d, alp_d = ctx.get_state()
+    finally:
+        ctx.close()
+    assert rel(phi_d, phi_o) < 1e-11 and rel(rho_d, rho_o) < 1e-10, (rel(phi_d, phi_o), rel(rho_d, rho_o))
+    assert abs(st["err1"] - e1_o) <= 1e-8 * e1_o and abs(st["err2"] - e2_o) <= 1e-8 * e2_o
