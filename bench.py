@@ -174,6 +174,86 @@ KERNEL_SYMBOL = {"dual": ("k_dual_",), "residual": ("k_res_fwd", "k_f16a_fwd", "
                  "update": ("k_inv", "k_f16b_inv", "k_f16a_inv")}
 
 
+def marching(args):
+    """--marching: time to solution of the reference's default execution mode -- window marching with T = 1
+    windows (time_step_per_PDHG = 2, run_example.py:431; PDHG_multi_step, utils_pdhg_solver.py:97-225), every
+    window solved to eps = 1e-6 with the reference's dual loop (rho_alp_iters, default 10 with early exit,
+    update_fns_in_pdhg.py:167-180), stepsz 0.1, through the drop-in driver (pdhg_amd.utils_pdhg_solver), on the
+    config's grid with its nt - 1 windows.  CPU column: the float64 oracle timed for a few outer iterations of one
+    window of the same grid on this host (cpu_baseline leg), extrapolated to the device run's total iterations
+    (the same algorithm and stop rule: the oracle needs the same iterations up to rounding)."""
+    from pdhg_amd import set_fns, utils_pdhg_solver as S, utils_precond
+    egno, ndim, epsl, nx, ny, nt = CONFIGS[args.config]
+    if ndim == 1:
+        ny = 1
+    k = args.rho_alp_iters
+    n_ctrl, bc = (ndim, 0 if ndim == 1 else (0, 0)) if egno != 3 else (1, (1, 0))
+    fns = set_fns.set_up_example_fns(egno, ndim, 0)
+    xs, ys = grid(ndim, nx, ny)
+    x_arr = xs[None, :, None] if ndim == 1 else np.stack(np.meshgrid(xs, ys, indexing="ij"), axis=-1)[None]
+    dt = 1.0 / (nt - 1)
+    dsp = (2.0 / nx,) if ndim == 1 else (2.0 / nx, 2.0 / ny)
+    nsp = (nx,) if ndim == 1 else (nx, ny)
+    g = set_fns.set_up_J(egno, ndim, (2.0, 2.0))(x_arr)
+    fv = utils_precond.compute_Dxx_fft_fv(ndim, nsp, dsp, bc)
+    fp, fd = S.make_update_fns(ndim, bc, rho_alp_iters=k, precision=args.precision)
+    stats = []
+    t0 = time.perf_counter()
+    results, errs = S.PDHG_multi_step(fp, fd, fns, g, x_arr, ndim, nt, nsp, dt, dsp, 70.0, time_step_per_PDHG=2,
+                                      epsl=epsl, stepsz_param=0.1, fv=fv, n_ctrl=n_ctrl, N_maxiter=1000000,
+                                      print_freq=10000, eps=1e-6, verbose=False, stats=stats)
+    wall = time.perf_counter() - t0
+    per_window = [int(r["window_iters"]) for r in stats]
+    total = int(sum(per_window))
+    out = {"metric": "time to solution, window marching (T = 1 windows to eps 1e-6)", "value": wall, "unit": "s",
+           "higher_is_better": False, "n_gpus": 1, "dtype": {"fp32": "f32", "fp64": "f64"}.get(args.precision),
+           "config": {"workload": "egno{} ndim{} epsl{} nx={} ny={} nt={}: {} windows of T = 1, rho_alp_iters={}, "
+                                  "stepsz 0.1, eps 1e-6".format(egno, ndim, epsl, nx, ny, nt, nt - 1, k)},
+           "windows": len(errs), "total_outer_iters": total, "max_iters_per_window": int(results[0][0]),
+           "iters_per_window_first10": per_window[:10], "ms_per_outer_iter": wall / max(1, total) * 1e3,
+           "stop_status_last_window": int(stats[-1]["status"]) if stats else None}
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_marching_baseline(args.config, k, total, min(16, os.cpu_count() or 1))
+        out["cpu_baseline"]["speedup"] = out["cpu_baseline"]["extrapolated_s"] / wall
+    print(json.dumps(out), flush=True)
+
+
+def cpu_marching_baseline(config, k, total_iters, threads, reps=3):
+    """The float64 oracle (restatement of the reference, 'port') for `reps` outer iterations of the first T = 1
+    window of the config's grid (reference initial state), median per iteration, times the device run's iterations."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    os.environ["ORACLE_FFT_WORKERS"] = str(threads)
+    import pdhg_oracle as O
+    egno, ndim, epsl, nx, ny, nt = CONFIGS[config]
+    x_arr = O.make_grid(ndim, nx, ny, egno)
+    bc = O.default_bc(egno, ndim)
+    fns = O.set_up_example_fns(egno, ndim, 0)
+    g = O.set_up_J(egno, ndim, (2.0, 2.0))(x_arr)
+    dt = 1.0 / (nt - 1)
+    dsp = (2.0 / nx,) if ndim == 1 else (2.0 / nx, 2.0 / ny)
+    nsp = (nx,) if ndim == 1 else (nx, ny)
+    fv = O.compute_Dxx_fft_fv(ndim, nsp, dsp, bc)
+    inner = []
+    primal, dual = O.make_update_fns(ndim, bc, rho_alp_iters=k, dual_stats=inner)
+    n_ctrl = 1 if egno == 3 else ndim
+    phi = np.repeat(g, 2, axis=0)
+    rho = np.full((1,) + nsp, 70.0)
+    alp = tuple(np.zeros((1,) + nsp + (n_ctrl,)) for _ in range(2 if ndim == 1 else 4))
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        phi_n = primal(phi, rho, 70.0, alp, 0.1 / 1.5, dt, dsp, fns, fv, epsl, x_arr, None)
+        rho, alp = dual(2 * phi_n - phi, rho, 70.0, alp, 0.15, dt, dsp, epsl, fns, x_arr, None, ndim, 1e-6)
+        phi = phi_n
+        times.append(time.perf_counter() - t0)
+    per = float(np.median(times))
+    return {"value": per, "unit": "s per outer iteration", "cores": threads, "kind": "port",
+            "extrapolated_s": per * total_iters,
+            "sample": "float64 NumPy/SciPy oracle, {} outer iterations of the first T = 1 window ({} dual "
+                      "sub-iterations each: {}), median, times the device run's {} iterations".format(
+                          reps, k, inner, total_iters)}
+
+
 def _free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
@@ -206,14 +286,16 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--rho-alp-iters", type=int, default=1)
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp64", "mixed"],
-                    help="fp32 (default), fp64 (the reference's arithmetic) or mixed (phi / phi_bar in fp64)")
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp64"],
+                    help="fp32 (default) or fp64 (the reference's arithmetic)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-T", type=int, default=1)
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--no-probe", action="store_true", help="skip the non-finite probe and the finite segment")
     ap.add_argument("--decomp", default="tslab", choices=["tslab", "xslab"],
                     help="multi-GPU decomposition of the window (xslab also at N = 1: one slab through its phases)")
+    ap.add_argument("--marching", action="store_true",
+                    help="time to solution of the T = 1 window-marching default on the config's grid (one GPU)")
     ap.add_argument("--selftest", action="store_true",
                     help="launcher / process-group check only: no GPU work, prints the world size")
     args = ap.parse_args()
@@ -253,6 +335,9 @@ def main():
             print(json.dumps({"selftest": True, "n_gpus": world, "ranks_seen": ranks_seen, "backend": backend}),
                   flush=True)
         return
+
+    if args.marching:
+        return marching(args)
 
     pmc, pmc_err = None, "disabled"
     if world == 1 and not args.no_pmc and args.decomp == "tslab":
@@ -433,7 +518,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if world > 1 else "weak",
         "vs_baseline": None,
-        "dtype": {"fp32": "f32", "fp64": "f64", "mixed": "f32 (phi, phi_bar f64)"}[args.precision],
+        "dtype": {"fp32": "f32", "fp64": "f64"}[args.precision],
         "data": "synthetic: the reference initial state (phi=g, rho=70, alp=0), W warm-up iterations from it, "
                 "then the K timed iterations continuing from there",
         "config": {"workload": "egno{} ndim{} epsl{} nx={} ny={} nt={}: one PDHG window of T={} rows, "

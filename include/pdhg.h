@@ -147,8 +147,8 @@ int pdhg_device_bytes(pdhg_ctx* ctx, unsigned long long* bytes);
  * "fast_rows" 1/0 (fp32 8/4-row y-transform kernels), "fast_dual" (-1 generic, 0 row-per-thread,
  * RX rows through LDS), "fast_xt" (0 generic, 1 single-role, 2 warp-specialised, 3 row-batched,
  * 4 row-batched with LDS-DMA staging x-transform), "half_real", "fourstep", "fs16", "fs_wide",
- * "glb_line", "thomas_chunk", "rows_rw", "res_threads", "upd_threads", "phi64" (1: phi / phi_bar held
- * in fp64, the mixed-precision fp32 path). */
+ * "glb_line", "thomas_chunk", "rows_rw", "res_threads", "upd_threads",
+ * "row_threads" (threads of the generic row kernels). */
 int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value);
 
 /* Per-launch kernel timing for the benchmark: HIP events recorded on the

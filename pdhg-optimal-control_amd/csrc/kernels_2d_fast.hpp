@@ -323,7 +323,8 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
   __syncthreads();
   for (; task < ntask; task += gridDim.x, buf ^= 1) {
     const int jt = task / ngx, j = p.row_base + jt, x0 = (task - jt * ngx) * RW;
-    // t-slab, last row: the dual formed it with rho_{j+1} = 0; the next slab's rho row 0 (the halo) adds rho/dt
+    // t-slab, last row: the dual stored it without the time difference; the next slab's rho row 0 (the halo)
+    // completes it, (rho_T - rho_{T-1})/dt added with the fma k_dual_lds_2d's finish_res uses inside a window
     const bool hal = p.rho_halo != nullptr && j == p.T - 1;
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
@@ -332,11 +333,12 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
 #pragma unroll
       for (int r = 0; r < RW; ++r) v[r] = rows[gi][r];
       if (hal) {
+        const float* rl = p.rho[p.ctrl->cur] + (size_t)j * plane + (size_t)x0 * N;
 #pragma unroll
         for (int r = 0; r < RW; ++r) {
-          const float4 hv = ld4(p.rho_halo + (size_t)(x0 + r) * N + y);
+          const float4 hv = ld4(p.rho_halo + (size_t)(x0 + r) * N + y), rv = ld4(rl + (size_t)r * N + y);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) f4set(v[r], e, f4(v[r], e) + f4(hv, e) * p.inv_dt);
+          for (int e = 0; e < 4; ++e) f4set(v[r], e, __builtin_fmaf(f4(hv, e) - f4(rv, e), p.inv_dt, f4(v[r], e)));
         }
       }
 #pragma unroll
@@ -353,10 +355,10 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
         for (int r = 0; r < RW; ++r) v[r].w += eyl[buf][(r * NSTRIP + s) * 2 + 1];
       }
 #pragma unroll
-      for (int r = 0; r < RW; ++r) {
-        float* Af = reinterpret_cast<float*>(A + (r >> 1) * Pad<N>::LINE + pix(y)) + (r & 1);
+      for (int l = 0; l < RW / 2; ++l) {   // rows 2l, 2l+1 -> line l (real, imaginary): one 8-B LDS store each
+        C* Al = A + l * Pad<N>::LINE + pix(y);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) Af[2 * e] = f4(v[r], e);
+        for (int e = 0; e < 4; ++e) Al[e] = make_float2(f4(v[2 * l], e), f4(v[2 * l + 1], e));
       }
     }
     // the next task's loads are unconditional (the last task re-loads its own rows): a conditional load
@@ -440,11 +442,17 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
       for (int i = 0; i < BATCH; ++i) {
         const int t = tl + (i0 + i) * NT;
         const int b = t >> lCS4, part = t & (CS4 - 1);
+        if (B == 2) {   // the float4 holds rows r, r+1 (r = 2 part) at columns 2b, 2b+1: two complex elements
+          C* Al = A + part * Pad<N>::LINE;
+          Al[pix(2 * b)] = make_float2(v[i].x, v[i].z);
+          Al[pix(2 * b + 1)] = make_float2(v[i].y, v[i].w);
+        } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int f = part * 4 + e;
-          const int r = f >> lB, c = f & (B - 1);
-          Af[((r >> 1) * Pad<N>::LINE + pix(b * B + c)) * 2 + (r & 1)] = f4(v[i], e);
+          for (int e = 0; e < 4; ++e) {
+            const int f = part * 4 + e;
+            const int r = f >> lB, c = f & (B - 1);
+            Af[((r >> 1) * Pad<N>::LINE + pix(b * B + c)) * 2 + (r & 1)] = f4(v[i], e);
+          }
         }
       }
     }

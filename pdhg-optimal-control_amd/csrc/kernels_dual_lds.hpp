@@ -25,7 +25,7 @@ namespace pdhg {
 // for the next tile's first row, eps rho'/dx^2 - m2x/dx of row x0 for the previous tile's last row;
 // p.ey: likewise per strip-edge column with m1y / m2y), and k_res_fwdy_fused_2d adds them.
 template <int EGNO, int RX, bool FR = false>
-__global__ void __launch_bounds__(RX * 64, FR ? 2 : 3) k_dual_lds_2d(KP<float> p, int jchunk, int jbase, int jend,
+__global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<float> p, int jchunk, int jbase, int jend,
                                                                      int zbase) {
   if (p.ctrl->done || p.ctrl->inner_done) return;
   constexpr int NA = (EGNO == 3) ? 2 : 4;
@@ -99,8 +99,12 @@ __global__ void __launch_bounds__(RX * 64, FR ? 2 : 3) k_dual_lds_2d(KP<float> p
   const bool use_eps = p.epsl != 0.f;
   const int nstrip = ny / YW;
   // R_{jr} (row jr of the next residual) = (rho'_{jr+1} - rho'_{jr})/dt + eps*Lap rho' - div m, from the
-  // flux buffer fb (row jr's values) and rnext = rho'_{jr+1} at this thread's 4 points
-  auto finish_res = [&](int jr, int fb, const float4& rnext, float cdt) {
+  // flux buffer fb (row jr's values) and rnext = rho'_{jr+1} at this thread's 4 points.  The time difference
+  // is added last (one fma), so a t-slab's last row -- stored without it (tdiff = false) and completed by
+  // k_res_fwdy_fused_2d from the next slab's rho row 0 with the same fma -- rounds exactly as the row does
+  // inside one window (with epsl > 0 the eps*Lap rho' terms are ~1e8 at dx = 2/8192, so any other order
+  // differs by their ulp)
+  auto finish_res = [&](int jr, int fb, const float4& rnext, float cdt, bool tdiff = true) {
     const float4 rc = flux[fb][r][0][lane], m1c = flux[fb][r][1][lane], m2c = flux[fb][r][2][lane];
     const int rmi = r > 0 ? r - 1 : r, rpi = r < RX - 1 ? r + 1 : r;   // wave-uniform
     float4 rm = flux[fb][rmi][0][lane], m1m = flux[fb][rmi][1][lane];
@@ -111,13 +115,14 @@ __global__ void __launch_bounds__(RX * 64, FR ? 2 : 3) k_dual_lds_2d(KP<float> p
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float r0 = f4(rc, e);
-      float res = (f4(rnext, e) - r0) * p.inv_dt;
+      float res = 0.f;
       if (use_eps) {
-        res = res + p.epsl * ((f4(rp, e) + f4(rm, e) - 2.f * r0) * p.inv_dx2);
+        res = p.epsl * ((f4(rp, e) + f4(rm, e) - 2.f * r0) * p.inv_dx2);
         res = res + yeps[e];
       }
       const float div = (f4(m1c, e) - f4(m1m, e)) * p.inv_dx + (f4(m2p, e) - f4(m2c, e)) * p.inv_dx + ydiv[e];
-      f4set(out, e, res - div + cdt);
+      const float other = res - div + cdt;
+      f4set(out, e, tdiff ? __builtin_fmaf(f4(rnext, e) - r0, p.inv_dt, other) : other);
     }
     st4(p.res + (size_t)jr * plane + rxc + y, out);
   };
@@ -238,11 +243,12 @@ __global__ void __launch_bounds__(RX * 64, FR ? 2 : 3) k_dual_lds_2d(KP<float> p
     if constexpr (FR) {
       // the launch's last row: inside the window (t-slab halo launch of row 0) rho'_{j1} comes from memory;
       // at the window's end rho_T = 0 and + c/dt (update_fns_in_pdhg.py:80, 95); at a t-slab's end rho_T is
-      // the next slab's row 0, added by k_res_fwdy_fused_2d from the halo
+      // the next slab's row 0: the time difference is left to k_res_fwdy_fused_2d (halo)
       __syncthreads();
       const bool inner = j1 < p.T;
       const float4 rnx = inner ? ld4(rd + (size_t)j1 * plane + rxc + y) : z4();
-      finish_res(j1 - 1, (j1 - 1 - j0) & 1, rnx, (!inner && p.last_slab) ? p.c_over_dt : 0.f);
+      finish_res(j1 - 1, (j1 - 1 - j0) & 1, rnx, (!inner && p.last_slab) ? p.c_over_dt : 0.f,
+                 inner || p.last_slab);
     }
   }
   block_reduce_store<NS>(s, p.partials, ((zbase + (int)blockIdx.z) * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x);

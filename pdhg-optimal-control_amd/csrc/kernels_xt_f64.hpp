@@ -7,12 +7,12 @@
 // The generic runtime-radix kernel keeps two FFT buffers and three per-mode carry arrays in LDS (5 M reals:
 // 320 KiB for a 4096-point column pair in fp64), so it stops at nx = 2048 in fp64.  Here the block's one
 // complex line (B = 2 real columns packed as z = a + i b) is transformed in place in a padded LDS line
-// (68 KiB + 13 KiB of twiddle seeds) and every Thomas carry lives in registers: a thread owns IT = N/NT items
-// (kx), each carrying the two modes (kx, 2b) and (kx, 2b + 1), so the forward pivot state h, the dd of the
-// mode pair and b' / x never leave the thread.  The next row is prefetched into registers before the
-// transform (loads in flight across the LDS passes).
+// (68 KiB + 13 KiB of twiddle seeds); a thread owns IT = N/NT items (kx), each carrying the two modes
+// (kx, 2b) and (kx, 2b + 1): the dd of the mode pair (then theta) and the forward pivot state h (then E) stay
+// in registers, b' / x in a 64 KiB LDS array (148 KiB in all; registers for all three spilled).  The next row
+// is prefetched into registers before the transform (loads in flight across the LDS passes).
 // Single context only (no t-slab phases: the slab decomposition is fp32).
-// grid: nb column blocks; block NT; LDS (N + N/16 + TwLds<N>) * 16 B.
+// grid: nb column blocks; block NT; LDS (N + N/16 + TwLds<N> + N) * 16 B.
 #pragma once
 #include "kernels_2d_fast.hpp"
 
@@ -29,6 +29,7 @@ __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const do
   extern __shared__ __align__(16) unsigned char smem_raw[];
   C* A = reinterpret_cast<C*>(smem_raw);
   C* twl = A + LINE;
+  C* bp = twl + TwLds<N>::SIZE;   // b' / x per item
   fill_twlds<C, N>(twl, twx);
   const int T = p.T, tid = threadIdx.x;
   const int b = blockIdx.x;
@@ -37,14 +38,14 @@ __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const do
   const double inv_ae = 1.0 / p.ae;
   const double ly0 = p.lamy[2 * b], ly1 = p.lamy[2 * b + 1];
   // per item: dd = (C - lam)/ae of the two modes, then theta; h = 1 - g, then E; b', then x
-  C dd[IT], h[IT], bp[IT], pf[IT];
+  C dd[IT], h[IT], pf[IT];
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
     const int kx = tid + i * NT;
     const double lx = p.lamx[kx];
     dd[i] = make_double2((p.C - lx - ly0) * inv_ae, (p.C - lx - ly1) * inv_ae);
     h[i] = make_double2(1.0, 1.0);   // h_{-1} = 1: the first row's pivot is dd + 2
-    bp[i] = make_double2(0.0, 0.0);
+    bp[kx] = make_double2(0.0, 0.0);
   }
   auto ldrow = [&](int k) {
     const C* s = reinterpret_cast<const C*>(wb + (size_t)k * kstride);
@@ -67,14 +68,16 @@ __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const do
       const int kx = tid + i * NT;
       double ha, hb;
       hartley_padded<C, double>(A, N, kx, ha, hb);
+      const C b0 = bp[kx];
       if (k < T - 1) {
         const double s0 = dd[i].x + h[i].x, s1 = dd[i].y + h[i].y;
         const double g0 = 1.0 / (1.0 + s0), g1 = 1.0 / (1.0 + s1);
-        bp[i] = make_double2((ha * inv_ae + bp[i].x) * g0, (hb * inv_ae + bp[i].y) * g1);
+        const C bn = make_double2((ha * inv_ae + b0.x) * g0, (hb * inv_ae + b0.y) * g1);
         h[i] = make_double2(s0 * g0, s1 * g1);
-        dst[kx] = bp[i];
+        bp[kx] = bn;
+        dst[kx] = bn;
       } else {
-        bp[i] = make_double2((ha * inv_ae + bp[i].x) / (dd[i].x + h[i].x), (hb * inv_ae + bp[i].y) / (dd[i].y + h[i].y));
+        bp[kx] = make_double2((ha * inv_ae + b0.x) / (dd[i].x + h[i].x), (hb * inv_ae + b0.y) / (dd[i].y + h[i].y));
       }
     }
     lds_sync();
@@ -95,13 +98,15 @@ __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const do
   for (int k = T - 1; k >= 0; --k) {
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
+      const int kx = tid + i * NT;
+      C x = bp[kx];
       if (k < T - 1) {
         const double e1x = expm1(-2.0 * dd[i].x * (k + 1)), e1y = expm1(-2.0 * dd[i].y * (k + 1));
-        bp[i] = make_double2(pf[i].x + gk(dd[i].x, e1x, h[i].x, k) * bp[i].x,
-                             pf[i].y + gk(dd[i].y, e1y, h[i].y, k) * bp[i].y);
+        x = make_double2(pf[i].x + gk(dd[i].x, e1x, h[i].x, k) * x.x, pf[i].y + gk(dd[i].y, e1y, h[i].y, k) * x.y);
         h[i] = make_double2(e1x, e1y);
+        bp[kx] = x;
       }
-      A[pix(tid + i * NT)] = bp[i];
+      A[pix(kx)] = x;
     }
     if (k < T - 1 && k >= 1) ldrow(k - 1);
     lds_sync();

@@ -111,6 +111,7 @@ struct Impl : ImplBase {
   // launch geometry
   int NT2 = 512;
   int gx1 = 0, gx4 = 0, g4 = 1, gx5 = 0, g5 = 1, g_outer = 1;
+  int nt_row = 256;   // threads of the generic 2-D row kernels (k_res_fwdy_2d, k_invy_update_2d)
   int rows_var = 0;                       // row-kernel shape variant (see with_fast_rows)
   int half_nt = 3;                        // ny = 4096 row kernels with 512 threads (bit 0 residual, bit 1 update)
   bool fast_dual = false;                 // fp32 time-marching float4 dual kernel (k_dual_fast_2d)
@@ -266,6 +267,11 @@ struct Impl : ImplBase {
       const int nmodes = nxg * B;
       lds_xt = (size_t)5 * nmodes * sizeof(R);
       if (lds_res > kLdsBytes) return fail(PDHG_ERR_UNSUPPORTED, "ny=%d exceeds the LDS row transform", ny);
+      {   // generic row kernels: when the LDS admits few workgroups per CU (fp64 ny = 4096: one), wider
+          // workgroups keep >= 16 waves per CU in flight for the residual's scattered loads
+        const int wg = (int)std::max<size_t>(1, kLdsBytes / std::max<size_t>(lds_res, 1));
+        nt_row = std::min(1024, 256 * std::max(1, 4 / wg));
+      }
       NT2 = std::min(512, ((nmodes + 63) / 64) * 64);
       gx1 = ((nx + 1) / 2) * T;                      // row-pair tasks (flat grid)
       gx4 = (int)std::min<long long>((long long)gx1, 4096);
@@ -309,7 +315,10 @@ struct Impl : ImplBase {
       }
       if (sizeof(R) == 4 && ny % 256 == 0) {
         fast_dual = true;
-        dual_rx = (nx % 8 == 0 && !short_dual) ? 8 : 0;
+        // x rows through LDS (k_dual_lds_2d) for the fused-residual sweep; a context created for
+        // rho_alp_iters > 1 (no fused residual) sweeps row-per-thread: measured at C3 with rho_alp_iters = 10,
+        // k_dual_fast_2d 25.7 ms per sub-iteration against 38.1 for k_dual_lds_2d (2 waves per SIMD)
+        dual_rx = (nx % 8 == 0 && !short_dual && !two_sets) ? 8 : 0;
         if (const char* e = getenv("PDHG_DUAL_RX")) {   // tuning override: 0 = row-per-thread kernel
           const int v = atoi(e);
           if (v == 0 || ((v == 4 || v == 8 || v == 16) && nx % v == 0)) dual_rx = v;
@@ -718,15 +727,15 @@ struct Impl : ImplBase {
         switch (pb.egno) {
           case 1:
             if ((r2 = ensure_lds(k_res_fwdy_2d<R, 1, F>, lds_res))) return r2;
-            hipLaunchKernelGGL((k_res_fwdy_2d<R, 1, F>), g, dim3(256), lds_res, stream, p, f, twy);
+            hipLaunchKernelGGL((k_res_fwdy_2d<R, 1, F>), g, dim3(nt_row), lds_res, stream, p, f, twy);
             break;
           case 2:
             if ((r2 = ensure_lds(k_res_fwdy_2d<R, 2, F>, lds_res))) return r2;
-            hipLaunchKernelGGL((k_res_fwdy_2d<R, 2, F>), g, dim3(256), lds_res, stream, p, f, twy);
+            hipLaunchKernelGGL((k_res_fwdy_2d<R, 2, F>), g, dim3(nt_row), lds_res, stream, p, f, twy);
             break;
           default:
             if ((r2 = ensure_lds(k_res_fwdy_2d<R, 3, F>, lds_res))) return r2;
-            hipLaunchKernelGGL((k_res_fwdy_2d<R, 3, F>), g, dim3(256), lds_res, stream, p, f, twy);
+            hipLaunchKernelGGL((k_res_fwdy_2d<R, 3, F>), g, dim3(nt_row), lds_res, stream, p, f, twy);
             break;
         }
         return (int)PDHG_OK;
@@ -782,7 +791,7 @@ struct Impl : ImplBase {
         ProfScope ps(this, "precond");
         if (p.xt_phase != 0 || p.b0 != 0 || nblk != p.nb)
           return fail(PDHG_ERR_UNSUPPORTED, "the fp64 nx = 4096 x transform runs whole windows only");
-        const size_t lds = (size_t)(Pad<4096>::LINE + TwLds<4096>::SIZE) * sizeof(C);
+        const size_t lds = (size_t)(Pad<4096>::LINE + TwLds<4096>::SIZE + 4096) * sizeof(C);
         if ((rc = ensure_lds(k_precond_xt_f64_2d<4096, 512>, lds))) return rc;
         hipLaunchKernelGGL((k_precond_xt_f64_2d<4096, 512>), dim3(nblk), dim3(512), lds, stream, p, twx);
         HIP_TRY(hipGetLastError());
@@ -907,7 +916,7 @@ struct Impl : ImplBase {
           using F = decltype(f);
           int r2;
           if ((r2 = ensure_lds(k_invy_update_2d<R, F>, lds_res))) return r2;
-          hipLaunchKernelGGL((k_invy_update_2d<R, F>), dim3(gx4), dim3(256), lds_res, stream, p, f, twy);
+          hipLaunchKernelGGL((k_invy_update_2d<R, F>), dim3(gx4), dim3(nt_row), lds_res, stream, p, f, twy);
           return (int)PDHG_OK;
         });
         if (rc) return rc;
@@ -2002,6 +2011,7 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
     else if (k == "fs16") *value = im.fs16 ? 1 : 0;
     else if (k == "rows_rw") *value = im.fast_rows ? im.RWf : 0;   // rows per fast row-kernel workgroup
     // threads of the fast row kernels as launched (ny = 4096: 512 instead of 1024 per half_nt)
+    else if (k == "row_threads") *value = im.nt_row;
     else if (k == "res_threads") *value = im.fast_rows ? ((im.NTf == 1024 && im.RWf == 8 && (im.half_nt & 1) &&
                                                            im.fuse_res) ? 512 : im.NTf) : 0;
     else if (k == "upd_threads") *value = im.fast_rows ? ((im.NTf == 1024 && im.RWf == 8 && (im.half_nt & 2))

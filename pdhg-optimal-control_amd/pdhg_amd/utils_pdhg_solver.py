@@ -86,7 +86,7 @@ def _device_oneiter(tag, fns_dict, phi0, rho0, alp0, x_arr, ndim, dt, dspatial, 
     if verbose and last["status"] == 2:
         print("Nan error at iter {}".format(i))
     if stats is not None:
-        stats.append(last)
+        stats.append(dict(last, window_iters=i + 1))   # + the iterations this window ran
     phi, rho, alp = ctx.get_state()
     error = np.array([last["err1"], last["err2"]])
     results_all.append((i + 1, phi, rho, alp))

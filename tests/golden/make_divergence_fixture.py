@@ -13,7 +13,14 @@ whether every entry of phi' and rho' is finite, and the first NaN iteration ("fi
 bench uses for the same event).  tests/test_gpu_divergence.py runs the device (fp32 and fp64) on
 the same window and compares.
 
-Run:  python tests/golden/make_divergence_fixture.py [T] [max_iters]     (~1 min per iteration at T = 4)
+The growth is geometric (|rho| x ~3000 per iteration after a few iterations): float32 overflows near iteration
+13 while float64 takes ~90 iterations to reach a NaN -- too long for the CPU oracle (2.5 min per iteration here).
+So the fixture keeps the first max_iters iterations (|.|_F and max |.| per iteration; first_nonfinite = 0 when no
+NaN occurred within them), which pin (a) the device's norm sequence in fp64 and in fp32 while finite, and (b) the
+iteration at which the values outgrow float32 (max |rho'| or |phi'| > 3.4e38), where the fp32 device's first
+non-finite iteration must fall.
+
+Run:  python tests/golden/make_divergence_fixture.py [T] [max_iters]     (~2.5 min per iteration at T = 4, 6 cores)
 """
 import os
 import sys
@@ -61,7 +68,11 @@ def run(S, max_iters, log=True):
             nphi = float(np.linalg.norm(phi_n[np.isfinite(phi_n)]))
             nrho = float(np.linalg.norm(rho_n[np.isfinite(rho_n)]))
             nalp = float(np.sqrt(sum(np.sum(np.where(np.isfinite(a), a, 0.0) ** 2) for a in alp_n)))
-        rows.append([it, nphi, nrho, nalp, e1, e2, 1.0 if fin else 0.0])
+            mphi = float(np.nanmax(np.abs(phi_n)))
+            mrho = float(np.nanmax(np.abs(rho_n)))
+        rows.append([it, nphi, nrho, nalp, e1, e2, 1.0 if fin else 0.0, mphi, mrho])
+        if S.get("out"):
+            save(S["out"], np.array(rows), 0, S)
         if log:
             print("it {:3d} |phi| {:.6e} |rho| {:.6e} |alp| {:.6e} err1 {:.3e} err2 {:.3e} finite {} nan {} ({:.0f} s)"
                   .format(it, nphi, nrho, nalp, e1, e2, fin, nan, time.time() - t0), flush=True)
@@ -72,14 +83,22 @@ def run(S, max_iters, log=True):
     return np.array(rows), first
 
 
+def save(out, rows, first, S):
+    T = S["phi"].shape[0] - 1
+    nx, ny = S["phi"].shape[1:]
+    np.savez_compressed(out, rows=rows, first_nonfinite=first, meta=np.array([2, 2, nx, ny, T]), dt=S["dt"],
+                        epsl=S["epsl"], tau=TAU, sigma=SIGMA,
+                        columns=np.array(["iter", "phi_norm", "rho_norm", "alp_norm", "err1", "err2", "finite",
+                                          "phi_absmax", "rho_absmax"]))
+
+
 if __name__ == "__main__":
     T = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-    max_iters = int(sys.argv[2]) if len(sys.argv) > 2 else 40
+    max_iters = int(sys.argv[2]) if len(sys.argv) > 2 else 24
     nx = ny = 4096
     S = setup(nx, ny, T, 1.0 / 200, 0.1)
-    rows, first = run(S, max_iters)
     out = os.path.join(HERE, "divergence_c3_plane_T{}.npz".format(T))
-    np.savez_compressed(out, rows=rows, first_nonfinite=first, meta=np.array([2, 2, nx, ny, T]), dt=1.0 / 200,
-                        epsl=0.1, tau=TAU, sigma=SIGMA,
-                        columns=np.array(["iter", "phi_norm", "rho_norm", "alp_norm", "err1", "err2", "finite"]))
-    print("wrote", out, "first non-finite iteration", first, flush=True)
+    S["out"] = out            # rewritten after every iteration (a partial run is usable)
+    rows, first = run(S, max_iters)
+    save(out, rows, first, S)
+    print("wrote", out, "first NaN iteration", first or "(none within {})".format(max_iters), flush=True)

@@ -198,9 +198,12 @@ def _gloo_worker(rank, world, port, paths, d, out):
         st = SlabRunner([s], DistComm()).iterate(n, TAU, SIGMA, -1.0, 1)
         torch.cuda.synchronize()
         phi, rho, _ = s.get_state()
-        phi_r = np.load(os.path.join(d, "phi.npy"), mmap_mode="r")[j0:j1 + 1]
+        # phi row 0 of a slab r > 0 is its halo (the previous slab's phi_bar row, join_state drops it):
+        # compare the rows the slab owns
+        h = 0 if rank == 0 else 1
+        phi_r = np.load(os.path.join(d, "phi.npy"), mmap_mode="r")[j0 + h:j1 + 1]
         rho_r = np.load(os.path.join(d, "rho.npy"), mmap_mode="r")[j0:j1]
-        out.put((rank, int(st["iters"]), float(st["err1"]), rel(phi, phi_r), rel(rho, rho_r)))
+        out.put((rank, int(st["iters"]), float(st["err1"]), rel(phi[h:], phi_r), rel(rho, rho_r)))
         s.close()
     finally:
         dist.destroy_process_group()

@@ -3,14 +3,16 @@ made by tests/golden/make_divergence_fixture.py).
 
 The bench (C3: egno 2, epsl 0.1, 4096^2, dt = 1/200) reports the first iteration whose phi' or rho' is non-finite
 (bench.py "first_nonfinite_iter").  That is the reference algorithm's own instability (the explicit
-sigma*epsl*Lap(phi_bar) term of its dual step, update_fns_in_pdhg.py:58-70, amplifies ~5e5-fold per iteration at
-dx = 2/4096), so the device must reproduce it where the fp64 oracle shows it: the same window (T rows of the
-bench's dt on the whole plane) from the reference initial state, one outer iteration at a time, with the
-reference's NaN stop (utils_pdhg_solver.py:78-80) on.  Checked per iteration: |rho'| (Frobenius) and err2 against
-the oracle's, and the first non-finite iteration -- exactly in fp64 (the reference's arithmetic; the nx = 4096 x
-transform k_precond_xt_f64_2d), within one iteration in fp32 (the bench's arithmetic, whose rounding the same
-instability amplifies).  Achieved values go to parity_log."""
-import ctypes
+sigma*epsl*Lap(phi_bar) term of its dual step, update_fns_in_pdhg.py:58-70), not a device defect: on the same
+window (T rows of the bench's dt on the whole plane, from the reference initial state) the fp64 oracle's |rho'|
+grows geometrically (x ~3000 per iteration once the unstable modes dominate).  The device must follow it:
+  * fp64 (the reference's arithmetic; k_precond_xt_f64_2d at nx = 4096): |rho'|, |phi'| and err2 per iteration
+    within FP64_TOL of the oracle over every fixture iteration;
+  * fp32 (the bench's arithmetic): the same while the values are representable, and its first non-finite
+    iteration (phi' or rho' NaN, the reference's test, utils_pdhg_solver.py:78-80) within 2 iterations of the one
+    at which the oracle's values outgrow float32 (max |.| > 3.4e38; intermediate products such as
+    epsl*Lap(phi_bar)/dx^2 overflow a little earlier than the stored values) -- that is where the bench's
+    first_nonfinite_iter comes from.  Achieved values go to parity_log."""
 import glob
 import os
 
@@ -23,6 +25,9 @@ pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 TAU, SIGMA = 0.1 / 1.5, 0.1 * 1.5
+F32_MAX = float(np.finfo(np.float32).max)
+FP64_TOL = 1e-6      # relative, per iteration (the geometric growth amplifies rounding differences slowly)
+FP32_TOL = 1e-2      # relative, per finite iteration
 
 
 def _fixture():
@@ -32,46 +37,54 @@ def _fixture():
     return np.load(paths[0])
 
 
-def _rho_norm(ctx):
+def _norms(ctx):
     from pdhg_amd import _native as N
+    phi = np.empty((ctx.T + 1,) + ctx._space)
     rho = np.empty((ctx.T,) + ctx._space)
-    N.check(ctx._lib.pdhg_get_state(ctx._h, None, N.dptr(rho), None))
-    return float(np.linalg.norm(rho[np.isfinite(rho)]))
+    N.check(ctx._lib.pdhg_get_state(ctx._h, N.dptr(phi), N.dptr(rho), None))
+    fp, fr = np.isfinite(phi), np.isfinite(rho)
+    return (float(np.linalg.norm(phi[fp])), float(np.linalg.norm(rho[fr])),
+            float(np.max(np.abs(np.where(fr, rho, 0.0)))), bool(fp.all() and fr.all()))
 
 
 @pytest.mark.parametrize("prec", ["fp64", "fp32"])
 def test_c3_plane_divergence_matches_oracle(native, prec, parity_log):
     F = _fixture()
-    rows, first_o = F["rows"], int(F["first_nonfinite"])
+    rows = F["rows"]             # iter, |phi|, |rho|, |alp|, err1, err2, finite, max|phi|, max|rho|
     egno, ndim, nx, ny, T = (int(v) for v in F["meta"])
-    assert first_o > 0, "the fixture's oracle run did not diverge"
+    n = rows.shape[0]
+    over = [int(r[0]) for r in rows if max(r[7], r[8]) > F32_MAX]
+    overflow_it = over[0] if over else None
     G = make_problem(egno, ndim, nx, ny, 1, float(F["epsl"]), seeded=False)
     G.update(T=T, dt=float(F["dt"]))
     ctx = device_ctx(G, prec)
+    dev, first_d = [], 0
     try:
         if prec == "fp64":
             assert ctx.path_info("f64_xt") == 1
         ctx.init_state(G["g"][0])
         ctx.set_stop_rules(converge=True, nan=True)
-        first_d, dev = 0, []
-        for it in range(1, first_o + 3):
+        last = n if prec == "fp64" else min(n, (overflow_it or n) + 2)
+        for it in range(1, last + 1):
             st = ctx.iterate(1, TAU, SIGMA, -1.0, 1)
             if st["nan_seen"] or st["status"] == 2:
                 first_d = it
                 break
-            dev.append((it, _rho_norm(ctx), st["err2"]))
+            nphi, nrho, mrho, fin = _norms(ctx)
+            dev.append((it, nphi, nrho, st["err2"], fin))
     finally:
         ctx.close()
-    # per finite iteration, relative distance of |rho'| and err2 from the oracle's
-    e_rho = max(abs(r - rows[i - 1, 2]) / rows[i - 1, 2] for i, r, _ in dev)
-    e_err2 = max(abs(e - rows[i - 1, 5]) / rows[i - 1, 5] for i, _, e in dev)
-    tol = {"fp64": 1e-8, "fp32": 1e-2}[prec]
-    parity_log("test_c3_plane_divergence_matches_oracle", prec,
-               {"rho_norm": e_rho, "err2": e_err2, "first_nonfinite_delta": abs(first_d - first_o)},
-               {"rho_norm": tol, "err2": tol, "first_nonfinite_delta": 0 if prec == "fp64" else 1},
-               first_nonfinite_device=first_d, first_nonfinite_oracle=first_o)
+    checked = [d for d in dev if d[4] and (overflow_it is None or d[0] < overflow_it)]
+    e = {"phi_norm": max(abs(p - rows[i - 1, 1]) / rows[i - 1, 1] for i, p, _, _, _ in checked),
+         "rho_norm": max(abs(r - rows[i - 1, 2]) / rows[i - 1, 2] for i, _, r, _, _ in checked),
+         "err2": max(abs(e2 - rows[i - 1, 5]) / rows[i - 1, 5] for i, _, _, e2, _ in checked)}
+    tol = FP64_TOL if prec == "fp64" else FP32_TOL
+    parity_log("test_c3_plane_divergence_matches_oracle", prec, e, {k: tol for k in e},
+               iterations_checked=len(checked), first_nonfinite_device=first_d, oracle_fp32_overflow_iter=overflow_it,
+               rho_norm_device=[d[2] for d in dev], rho_norm_oracle=[float(v) for v in rows[:, 2]])
+    assert len(checked) >= min(n, 5), (len(checked), dev)
+    assert all(v <= tol for v in e.values()), (e, dev)
     if prec == "fp64":
-        assert first_d == first_o, (first_d, first_o)
-    else:
-        assert abs(first_d - first_o) <= 1, (first_d, first_o)
-    assert e_rho <= tol and e_err2 <= tol, (e_rho, e_err2, dev)
+        assert first_d == 0 or first_d > n, first_d     # no NaN within the fixture's iterations
+    elif overflow_it is not None:
+        assert overflow_it - 2 <= first_d <= overflow_it + 2, (first_d, overflow_it)

@@ -415,6 +415,10 @@ def test_precond_1d_parameters(native, case, prec, cpc, parity_log):
                             P["dsp"], P["fns"], P["fv"], P["epsl"], P["x_arr"].astype(f), None)
             assert phi_32.dtype == f
             e32_phi, e32_U = rel(phi_32, phi_o), rel((phi_32 - phi0) / TAU, U_o)
+            parity_log("test_precond_1d_parameters/first_update", "{}_{}_C{}_pow{}_Ct{}".format(case[2], case[4], *cpc),
+                       {"phi1": rel(phi_d, phi_o), "U1": rel(U_d, U_o)},
+                       {"phi1": max(1e-6, 4 * e32_phi), "U1": max(5e-4, 4 * e32_U)},
+                       e32={"phi1": e32_phi, "U1": e32_U})
             assert rel(phi_d, phi_o) < max(1e-6, 4 * e32_phi), (rel(phi_d, phi_o), e32_phi)
             assert rel(U_d, U_o) < max(5e-4, 4 * e32_U), (rel(U_d, U_o), e32_U)
         phi, rho, alp = P["phi"], P["rho"], P["alp"]
