@@ -201,7 +201,7 @@ def marching(args):
     t0 = time.perf_counter()
     results, errs = S.PDHG_multi_step(fp, fd, fns, g, x_arr, ndim, nt, nsp, dt, dsp, 70.0, time_step_per_PDHG=2,
                                       epsl=epsl, stepsz_param=0.1, fv=fv, n_ctrl=n_ctrl, N_maxiter=1000000,
-                                      print_freq=10000, eps=1e-6, verbose=False, stats=stats)
+                                      print_freq=10000, eps=1e-6, verbose=True, stats=stats)   # per-window progress lines
     wall = time.perf_counter() - t0
     per_window = [int(r["window_iters"]) for r in stats]
     total = int(sum(per_window))

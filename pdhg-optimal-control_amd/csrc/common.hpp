@@ -26,6 +26,15 @@ template <typename C> __device__ __forceinline__ C cmul_mi(C a) { return cmk<C>(
 // NaN-propagating max/min (jnp.maximum / jnp.minimum semantics; fmax would drop the NaN)
 template <typename R> __device__ __forceinline__ R nmax(R a, R b) { return (a != a) ? a : ((b != b) ? b : (a > b ? a : b)); }
 template <typename R> __device__ __forceinline__ R nmin(R a, R b) { return (a != a) ? a : ((b != b) ? b : (a < b ? a : b)); }
+// v_rcp_f32 (1 ulp) for the Thomas pivots of the fp32 sweeps: the recurrences are contractive, so the ulp does
+// not accumulate, and a correctly rounded 1/x (__frcp_rn) costs ~10 instructions (div_scale / fmas / fixup)
+__device__ __forceinline__ float rcp_fast(float x) { return __builtin_amdgcn_rcpf(x); }
+// jnp.minimum(hi, jnp.maximum(lo, x)) for constant bounds: the hardware min / max (which drop a NaN operand)
+// and one NaN select, instead of two NaN-propagating selects each
+template <typename R> __device__ __forceinline__ R nclamp(R x, R lo, R hi) {
+  const R c = fmin(hi, fmax(lo, x));
+  return (x != x) ? x : c;
+}
 
 // Device control block: loop control that never round-trips through the host.
 struct Ctrl {

@@ -309,8 +309,9 @@ __global__ void __launch_bounds__(256) k_dual_1d(KP<R> p) {
       const R rho = p.rho[src_set][o];
       const R pinv = (rho + (R)1e-4) / p.sigma;
       const R ao0 = p.alp[src_set][0][o], ao1 = p.alp[src_set][1][o];
-      const R an0 = alp_prox<R, EGNO>(ao0, DxR, a, pinv, true);
-      const R an1 = alp_prox<R, EGNO>(ao1, DxL, a, pinv, false);
+      const R q = prox_recip<R, EGNO>(rho, p.sigma, pinv);
+      const R an0 = alp_prox<R, EGNO>(ao0, DxR, a, pinv, q, true);
+      const R an1 = alp_prox<R, EGNO>(ao1, DxL, a, pinv, q, false);
       const R f1v = fpos<R>(fval<R, EGNO>(an0, a));
       const R f2v = fneg<R>(fval<R, EGNO>(an1, a));
       const R L = lag<R, EGNO>(an0 * an0) + lag<R, EGNO>(an1 * an1);

@@ -366,9 +366,10 @@ __device__ __forceinline__ R dual_point(const KP<R>& p, R pc, R pxm, R pxp, R py
   const R DxL = (pc - pxm) * p.inv_dx;
   const R DyR = (pyp - pc) * p.inv_dy;
   const R DyL = (pc - pym) * p.inv_dy;
-  const R pinv = (rho + (R)1e-4) / p.sigma;              // param_inv, set_fns.py:127
-  an[0] = alp_prox<R, EGNO>(ao[0], DxR, axc, pinv, true);
-  an[1] = alp_prox<R, EGNO>(ao[1], DxL, axc, pinv, false);
+  const R pinv = (rho + (R)1e-4) / p.sigma;              // param_inv, set_fns.py:127 (unused for egno 2)
+  const R q = prox_recip<R, EGNO>(rho, p.sigma, pinv);
+  an[0] = alp_prox<R, EGNO>(ao[0], DxR, axc, pinv, q, true);
+  an[1] = alp_prox<R, EGNO>(ao[1], DxL, axc, pinv, q, false);
   const R f1x = fpos<R>(fval<R, EGNO>(an[0], axc));
   const R f2x = fneg<R>(fval<R, EGNO>(an[1], axc));
   R f1y, f2y, L;
@@ -377,8 +378,8 @@ __device__ __forceinline__ R dual_point(const KP<R>& p, R pc, R pxm, R pxp, R py
     f2y = fneg<R>(axc);
     L = lag<R, EGNO>(an[0] * an[0]) + lag<R, EGNO>(an[1] * an[1]);
   } else {
-    an[2] = alp_prox<R, EGNO>(ao[2], DyR, ayc, pinv, true);
-    an[3] = alp_prox<R, EGNO>(ao[3], DyL, ayc, pinv, false);
+    an[2] = alp_prox<R, EGNO>(ao[2], DyR, ayc, pinv, q, true);
+    an[3] = alp_prox<R, EGNO>(ao[3], DyL, ayc, pinv, q, false);
     f1y = fpos<R>(fval<R, EGNO>(an[2], ayc));
     f2y = fneg<R>(fval<R, EGNO>(an[3], ayc));
     L = lag<R, EGNO>(an[0] * an[0]) + lag<R, EGNO>(an[1] * an[1]) + lag<R, EGNO>(an[2] * an[2]) +

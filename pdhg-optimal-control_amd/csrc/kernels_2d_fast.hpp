@@ -630,7 +630,7 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
         hartley_padded<C, float>(A + l * LINE, N, kx, ha, hb);
         const C dd = sth[item], h = sE[item], bp = sbp[item];
         const float s0 = dd.x + h.x, s1 = dd.y + h.y;
-        const float g0 = __frcp_rn(1.f + s0), g1 = __frcp_rn(1.f + s1);
+        const float g0 = rcp_fast(1.f + s0), g1 = rcp_fast(1.f + s1);
         const C bn = make_float2((ha * inv_ae + bp.x) * g0, (hb * inv_ae + bp.y) * g1);
         sE[item] = make_float2(s0 * g0, s1 * g1);
         sbp[item] = bn;
@@ -684,8 +684,8 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
         const C e2 = sE[item];
         // theta >= 1e-20 (clamped at the sweep start): the closed form tends to (k+1)/(k+2) as theta -> 0
         const float2 E1 = expm1_neg2(-2.f * t2.x * kk1, -2.f * t2.y * kk1);
-        const float g0 = __expf(-t2.x) * E1.x * __frcp_rn(e2.x);
-        const float g1 = __expf(-t2.y) * E1.y * __frcp_rn(e2.y);
+        const float g0 = __expf(-t2.x) * E1.x * rcp_fast(e2.x);
+        const float g1 = __expf(-t2.y) * E1.y * rcp_fast(e2.y);
         x2 = make_float2(pf[i].x + g0 * x2.x, pf[i].y + g1 * x2.y);
         sE[item] = E1;
         sbp[item] = x2;
@@ -881,7 +881,7 @@ __global__ void __launch_bounds__(512) k_precond_xt_ws_2d(KP<float> p, const flo
 #pragma unroll
         for (int i = I0; i < I1; ++i) {
           const float s0 = c1[i].x + c2[i].x, s1 = c1[i].y + c2[i].y;
-          const float g0 = __frcp_rn(1.f + s0), g1 = __frcp_rn(1.f + s1);
+          const float g0 = rcp_fast(1.f + s0), g1 = rcp_fast(1.f + s1);
           c3[i] = make_float2((ha[i - I0] * inv_ae + c3[i].x) * g0, (hb[i - I0] * inv_ae + c3[i].y) * g1);
           c2[i] = make_float2(s0 * g0, s1 * g1);
           dst[tt + i * NTT] = c3[i];
@@ -975,8 +975,8 @@ __global__ void __launch_bounds__(512) k_precond_xt_ws_2d(KP<float> p, const flo
     auto subst = [&](int i) {
       // theta >= 1e-20 (clamped at the sweep start): the closed form tends to (k+1)/(k+2) as theta -> 0
       const float2 E1 = expm1_neg2(-2.f * c1[i].x * kk1, -2.f * c1[i].y * kk1);
-      const float g0 = __expf(-c1[i].x) * E1.x * __frcp_rn(c2[i].x);
-      const float g1 = __expf(-c1[i].y) * E1.y * __frcp_rn(c2[i].y);
+      const float g0 = __expf(-c1[i].x) * E1.x * rcp_fast(c2[i].x);
+      const float g1 = __expf(-c1[i].y) * E1.y * rcp_fast(c2[i].y);
       c3[i] = make_float2(pf[i].x + g0 * c3[i].x, pf[i].y + g1 * c3[i].y);
       c2[i] = E1;
     };

@@ -128,17 +128,15 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<float> p, int jch
   };
   if (j0 < j1) {
     float4 f0 = ld4(p.phibar + (size_t)j0 * plane + rxc + y);   // phi_bar row j
-    In nxt = load(j0);
-    stage(nxt, 0);
-    __syncthreads();
-#pragma unroll 1
-    for (int j = j0; j < j1; ++j) {
+    // Two register sets, A and B, alternate between the rows (no copies: a register copy of a row still in
+    // flight would wait for it).  Step j computes from cur (row j), re-fills cur with row j+2 and stages oth
+    // (row j+1, loaded one step earlier) into LDS: the loads of a row are in flight across a whole step,
+    // and no wait ever covers a store.
+    auto step = [&](int j, In& cur, const In& oth) {
       const int buf = (j - j0) & 1;
-      const In in = nxt;
-      if (j + 1 < j1) nxt = load(j + 1);
-      const float4 pm = strip[buf][r][lane], pp = strip[buf][r + 2][lane], pc = in.pc;
-      const float pyl = lane_from_prev(pc.w, zym ? 0.f : in.el);
-      const float pyr = lane_from_next(pc.x, zyp ? 0.f : in.er);
+      const float4 pm = strip[buf][r][lane], pp = strip[buf][r + 2][lane], pc = cur.pc;
+      const float pyl = lane_from_prev(pc.w, zym ? 0.f : cur.el);
+      const float pyr = lane_from_next(pc.x, zyp ? 0.f : cur.er);
       float4 rn4, an4[NA];
       float4 m1x4, m2x4;
       float m1y[4], m2y[4];
@@ -154,8 +152,8 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<float> p, int jch
         const float rgt = e == 3 ? pyr : f4(pc, e + 1);
         float ao[4], an[4], fo[4];
 #pragma unroll
-        for (int a = 0; a < NA; ++a) ao[a] = f4(in.al[a], e);
-        const float rho = f4(in.rho, e);
+        for (int a = 0; a < NA; ++a) ao[a] = f4(cur.al[a], e);
+        const float rho = f4(cur.rho, e);
         const float rn = dual_point<float, EGNO>(p, c, f4(pm, e), f4(pp, e), lft, rgt, f4(f0, e), rho, ao, axc,
                                                  f4(ay4, e), an, FR ? fo : nullptr);
         f4set(rn4, e, rn);
@@ -180,6 +178,10 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<float> p, int jch
           fs[5 + 3 * a] = fmaf(ao[a], ao[a], fs[5 + 3 * a]);
         }
       }
+      // cur is consumed: the row after next goes into its registers now, ahead of this step's stores, so the
+      // wait for the next row's loads (at the staging below) counts these 7 loads and never this step's stores
+      const float4 pcs = pc;
+      cur = load(min(j + 2, j1 - 1));   // clamped: the last rows re-load row j1-1 (never used)
       if (live) {
 #pragma unroll
         for (int i = 0; i < NS; ++i) s[i] += (double)fs[i];
@@ -190,7 +192,7 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<float> p, int jch
 #pragma unroll
         for (int a = 0; a < NA; ++a) st4(ad[a] + o, an4[a]);
       }
-      f0 = pc;
+      f0 = pcs;
       if constexpr (FR) if (!(p.dbg & 256)) {   // PDHG_DBG 256: no residual / edge terms (timing only)
         if (j > j0) finish_res(j - 1, buf ^ 1, rn4, 0.f);   // row j-1, with rho'_j
         flux[buf][r][0][lane] = rn4;
@@ -236,9 +238,17 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<float> p, int jch
         }
       }
       if (j + 1 < j1) {     // uniform over the workgroup
-        stage(nxt, buf ^ 1);
+        stage(oth, buf ^ 1);
         __syncthreads();
       }
+    };
+    In A = load(j0), B = load(min(j0 + 1, j1 - 1));
+    stage(A, 0);
+    __syncthreads();
+#pragma unroll 1
+    for (int j = j0; j < j1; j += 2) {
+      step(j, A, B);
+      if (j + 1 < j1) step(j + 1, B, A);
     }
     if constexpr (FR) {
       // the launch's last row: inside the window (t-slab halo launch of row 0) rho'_{j1} comes from memory;

@@ -48,7 +48,7 @@ __global__ void __launch_bounds__(1024) k_thomas_chunk_1d(KP<float> p) {
       const float s = dd + h;
       float gi;
       if (j0 + i < T - 1) {
-        gi = __frcp_rn(1.f + s);
+        gi = rcp_fast(1.f + s);
         h = s * gi;
       } else {                                        // Neumann row of the window
         gi = 1.f / s;

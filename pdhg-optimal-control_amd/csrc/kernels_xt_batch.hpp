@@ -201,7 +201,7 @@ __global__ void __launch_bounds__(NT, NT == 1024 ? 1 : 4) k_precond_xt_batch_2d(
             float ha, hb;
             hartley_padded<C, float>(A + (r * NL + ln_of(i)) * LINE, N, kx_of(i), ha, hb);
             const float s0 = c1[i].x + c2[i].x, s1 = c1[i].y + c2[i].y;
-            const float g0 = __frcp_rn(1.f + s0), g1 = __frcp_rn(1.f + s1);
+            const float g0 = rcp_fast(1.f + s0), g1 = rcp_fast(1.f + s1);
             c3[i] = make_float2((ha * inv_ae + c3[i].x) * g0, (hb * inv_ae + c3[i].y) * g1);
             c2[i] = make_float2(s0 * g0, s1 * g1);
           }
@@ -256,8 +256,8 @@ __global__ void __launch_bounds__(NT, NT == 1024 ? 1 : 4) k_precond_xt_batch_2d(
         for (int i = 0; i < IT; ++i) {
           // theta >= 1e-20 (clamped above): the closed form tends to (k+1)/(k+2) as theta -> 0
           const float2 E1 = expm1_neg2(-2.f * c1[i].x * kk1, -2.f * c1[i].y * kk1);
-          const float g0 = __expf(-c1[i].x) * E1.x * __frcp_rn(c2[i].x);
-          const float g1 = __expf(-c1[i].y) * E1.y * __frcp_rn(c2[i].y);
+          const float g0 = __expf(-c1[i].x) * E1.x * rcp_fast(c2[i].x);
+          const float g1 = __expf(-c1[i].y) * E1.y * rcp_fast(c2[i].y);
           c3[i] = make_float2(pf[r][i].x + g0 * c3[i].x, pf[r][i].y + g1 * c3[i].y);
           c2[i] = E1;
         }

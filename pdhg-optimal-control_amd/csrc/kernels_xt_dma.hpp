@@ -177,7 +177,7 @@ __global__ void __launch_bounds__(1024) k_precond_xt_dma_2d(KP<float> p, const f
             hartley_padded<C, float>(A + r * LINE, N, item_of(i), ha, hb);
             const float2 dd = dd_of(item_of(i));
             const float s0 = dd.x + c2[i].x, s1 = dd.y + c2[i].y;
-            const float g0 = __frcp_rn(1.f + s0), g1 = __frcp_rn(1.f + s1);
+            const float g0 = rcp_fast(1.f + s0), g1 = rcp_fast(1.f + s1);
             c3[i] = make_float2((ha * inv_ae + c3[i].x) * g0, (hb * inv_ae + c3[i].y) * g1);
             c2[i] = make_float2(s0 * g0, s1 * g1);
           }
@@ -259,8 +259,8 @@ __global__ void __launch_bounds__(1024) k_precond_xt_dma_2d(KP<float> p, const f
           // theta >= 1e-20 (clamped above): the closed form tends to (k+1)/(k+2) as theta -> 0
           const C bp = bpv[r][i];
           const float2 E1 = expm1_neg2(-2.f * c1[i].x * kk1, -2.f * c1[i].y * kk1);
-          const float g0 = __expf(-c1[i].x) * E1.x * __frcp_rn(c2[i].x);
-          const float g1 = __expf(-c1[i].y) * E1.y * __frcp_rn(c2[i].y);
+          const float g0 = __expf(-c1[i].x) * E1.x * rcp_fast(c2[i].x);
+          const float g1 = __expf(-c1[i].y) * E1.y * rcp_fast(c2[i].y);
           c3[i] = make_float2(bp.x + g0 * c3[i].x, bp.y + g1 * c3[i].y);
           c2[i] = E1;
         }

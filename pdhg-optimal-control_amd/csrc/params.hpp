@@ -81,21 +81,28 @@ template <typename R>
 __device__ __forceinline__ R fneg(R f) { return f * (R)(f < (R)0 ? 1 : 0); }
 
 // alpha prox (set_fns.py:63-95 base functions + masks :108-110, :132-138, :157-159).
-// D = one-sided derivative of phi_bar, a = coefficient, p = (rho+1e-4)/sigma.
+// D = one-sided derivative of phi_bar, a = coefficient, p = (rho+1e-4)/sigma (param_inv, set_fns.py:127),
+// q = prox_recip(rho, sigma, p): the one reciprocal a grid point's controls share (egno 2: 1/p; egno 1/3:
+// 1/(1+p)), so a point costs one division (egno 2) instead of one per control plus param_inv's.
 // right = true -> alp1 (mask f >= 0), false -> alp2 (mask f < 0).
 template <typename R, int EGNO>
-__device__ __forceinline__ R alp_prox(R alp, R D, R a, R p, bool right) {
+__device__ __forceinline__ R prox_recip(R rho, R sigma, R p) {
+  if constexpr (EGNO == 2) return sigma / (rho + (R)1e-4);
+  else return (R)1 / ((R)1 + p);
+}
+template <typename R, int EGNO>
+__device__ __forceinline__ R alp_prox(R alp, R D, R a, R p, R q, bool right) {
   R n;
   R f;
   if constexpr (EGNO == 1) {
-    n = (D * a + p * alp) / ((R)1 + p);
+    n = (D * a + p * alp) * q;
     f = -(a * n);
   } else if constexpr (EGNO == 2) {
-    n = D * a / p + alp;
-    n = nmin<R>((R)1, nmax<R>((R)-1, n));
+    n = D * a * q + alp;
+    n = nclamp<R>(n, (R)-1, (R)1);
     f = -(a * n);
   } else {  // egno 3 x-controls: f = alp, coefficient -1 on D
-    n = (-D + p * alp) / ((R)1 + p);
+    n = (-D + p * alp) * q;
     f = n;
   }
   const bool keep = right ? (f >= (R)0) : (f < (R)0);

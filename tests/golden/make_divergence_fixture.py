@@ -20,7 +20,12 @@ NaN occurred within them), which pin (a) the device's norm sequence in fp64 and 
 iteration at which the values outgrow float32 (max |rho'| or |phi'| > 3.4e38), where the fp32 device's first
 non-finite iteration must fall.
 
-Run:  python tests/golden/make_divergence_fixture.py [T] [max_iters]     (~2.5 min per iteration at T = 4, 6 cores)
+The float32 run (argument f32: inputs rounded to float32, the oracle's arithmetic in float32 as in
+make_config_fixtures.py's e32 pass) pins the fp32 device: there fp32 rounding (1e-7 relative) seeds the unstable
+modes, which then grow ~3000-fold per iteration, so the float32 trajectory leaves the float64 one after ~2
+iterations and reaches a NaN long before float64 does.
+
+Run:  python tests/golden/make_divergence_fixture.py [T] [max_iters] [f32]   (~2.5 min per iteration at T = 4, 6 cores)
 """
 import os
 import sys
@@ -35,7 +40,7 @@ import pdhg_oracle as O  # noqa: E402
 TAU, SIGMA = 0.1 / 1.5, 0.1 * 1.5
 
 
-def setup(nx, ny, T, dt, epsl):
+def setup(nx, ny, T, dt, epsl, dtype=np.float64):
     egno, ndim = 2, 2
     x_arr = O.make_grid(ndim, nx, ny, egno)
     g = O.set_up_J(egno, ndim, (2.0, 2.0))(x_arr)
@@ -44,9 +49,11 @@ def setup(nx, ny, T, dt, epsl):
     bc = O.default_bc(egno, ndim)
     fv = O.compute_Dxx_fft_fv(ndim, (nx, ny), dsp, bc)
     primal, dual = O.make_update_fns(ndim, bc, rho_alp_iters=1)
-    phi = np.repeat(g, T + 1, axis=0)
-    rho = np.full((T, nx, ny), 70.0)
-    alp = tuple(np.zeros((T, nx, ny, 2)) for _ in range(4))
+    if dtype == np.float32:   # the oracle in float32 (as make_config_fixtures.py's e32 pass): inputs rounded
+        x_arr = x_arr.astype(dtype)
+    phi = np.repeat(g, T + 1, axis=0).astype(dtype)
+    rho = np.full((T, nx, ny), 70.0, dtype=dtype)
+    alp = tuple(np.zeros((T, nx, ny, 2), dtype=dtype) for _ in range(4))
     return dict(x_arr=x_arr, g=g, fns=fns, dsp=dsp, fv=fv, primal=primal, dual=dual, phi=phi, rho=rho, alp=alp,
                 dt=dt, epsl=epsl)
 
@@ -65,9 +72,10 @@ def run(S, max_iters, log=True):
             e1, e2 = O.outer_errors(phi, phi_n, rho, rho_n, alp, alp_n)
             fin = bool(np.isfinite(phi_n).all() and np.isfinite(rho_n).all())
             nan = bool(np.isnan(phi_n).any() or np.isnan(rho_n).any())
-            nphi = float(np.linalg.norm(phi_n[np.isfinite(phi_n)]))
-            nrho = float(np.linalg.norm(rho_n[np.isfinite(rho_n)]))
-            nalp = float(np.sqrt(sum(np.sum(np.where(np.isfinite(a), a, 0.0) ** 2) for a in alp_n)))
+            d = np.float64   # norms of float32 states in float64 (they outgrow float32 before the entries do)
+            nphi = float(np.linalg.norm(phi_n[np.isfinite(phi_n)].astype(d)))
+            nrho = float(np.linalg.norm(rho_n[np.isfinite(rho_n)].astype(d)))
+            nalp = float(np.sqrt(sum(np.sum(np.where(np.isfinite(a), a, 0.0).astype(d) ** 2) for a in alp_n)))
             mphi = float(np.nanmax(np.abs(phi_n)))
             mrho = float(np.nanmax(np.abs(rho_n)))
         rows.append([it, nphi, nrho, nalp, e1, e2, 1.0 if fin else 0.0, mphi, mrho])
@@ -95,9 +103,10 @@ def save(out, rows, first, S):
 if __name__ == "__main__":
     T = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     max_iters = int(sys.argv[2]) if len(sys.argv) > 2 else 24
+    f32 = len(sys.argv) > 3 and sys.argv[3] == "f32"   # the float32 oracle (until its first NaN)
     nx = ny = 4096
-    S = setup(nx, ny, T, 1.0 / 200, 0.1)
-    out = os.path.join(HERE, "divergence_c3_plane_T{}.npz".format(T))
+    S = setup(nx, ny, T, 1.0 / 200, 0.1, np.float32 if f32 else np.float64)
+    out = os.path.join(HERE, "divergence_c3_plane_T{}{}.npz".format(T, "_f32" if f32 else ""))
     S["out"] = out            # rewritten after every iteration (a partial run is usable)
     rows, first = run(S, max_iters)
     save(out, rows, first, S)

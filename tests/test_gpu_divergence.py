@@ -1,17 +1,19 @@
-"""C3's divergence on the FULL 4096^2 plane, against the fp64 oracle's fixture (tests/golden/divergence_c3_plane_T*.npz,
-made by tests/golden/make_divergence_fixture.py).
+"""C3's divergence on the FULL 4096^2 plane, against the oracle's fixtures (tests/golden/divergence_c3_plane_T4.npz
+in float64, divergence_c3_plane_T4_f32.npz in float32; made by tests/golden/make_divergence_fixture.py).
 
 The bench (C3: egno 2, epsl 0.1, 4096^2, dt = 1/200) reports the first iteration whose phi' or rho' is non-finite
 (bench.py "first_nonfinite_iter").  That is the reference algorithm's own instability (the explicit
 sigma*epsl*Lap(phi_bar) term of its dual step, update_fns_in_pdhg.py:58-70), not a device defect: on the same
-window (T rows of the bench's dt on the whole plane, from the reference initial state) the fp64 oracle's |rho'|
-grows geometrically (x ~3000 per iteration once the unstable modes dominate).  The device must follow it:
+window (T rows of the bench's dt on the whole plane, from the reference initial state) the oracle's |rho'| grows
+geometrically (x ~3000 per iteration once the unstable modes dominate), in either precision.  The device must
+follow the oracle of its own arithmetic:
   * fp64 (the reference's arithmetic; k_precond_xt_f64_2d at nx = 4096): |rho'|, |phi'| and err2 per iteration
-    within FP64_TOL of the oracle over every fixture iteration;
-  * fp32 (the bench's arithmetic): the same while the values are representable, and its first non-finite
-    iteration (phi' or rho' NaN, the reference's test, utils_pdhg_solver.py:78-80) within 2 iterations of the one
-    at which the oracle's values outgrow float32 (max |.| > 3.4e38; intermediate products such as
-    epsl*Lap(phi_bar)/dx^2 overflow a little earlier than the stored values) -- that is where the bench's
+    within FP64_TOL of the float64 oracle over every fixture iteration, and no NaN within them;
+  * fp32 (the bench's arithmetic): fp32 rounding (1e-7 relative) seeds the unstable modes, so the float32
+    trajectory leaves the float64 one after ~2 iterations (|rho'| 1e9 at iteration 3 against 6e5) -- the device
+    must match the float32 oracle (same norms within FP32_TOL per iteration while finite: once the unstable
+    modes dominate, a relative difference stays put while both grow) and turn non-finite (phi' or rho' NaN, the
+    reference's test, utils_pdhg_solver.py:78-80) within one iteration of it.  That is where the bench's
     first_nonfinite_iter comes from.  Achieved values go to parity_log."""
 import glob
 import os
@@ -26,14 +28,17 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 TAU, SIGMA = 0.1 / 1.5, 0.1 * 1.5
 F32_MAX = float(np.finfo(np.float32).max)
-FP64_TOL = 1e-6      # relative, per iteration (the geometric growth amplifies rounding differences slowly)
-FP32_TOL = 1e-2      # relative, per finite iteration
+FP64_TOL = 1e-6      # relative, per iteration
+FP32_TOL = 1e-3      # relative, per finite iteration, against the float32 oracle
 
 
-def _fixture():
-    paths = sorted(glob.glob(os.path.join(HERE, "golden", "divergence_c3_plane_T*.npz")))
+def _fixture(prec):
+    suffix = "_f32" if prec == "fp32" else ""
+    paths = sorted(glob.glob(os.path.join(HERE, "golden", "divergence_c3_plane_T*{}.npz".format(suffix))))
+    paths = [q for q in paths if q.endswith(suffix + ".npz") and (suffix or not q.endswith("_f32.npz"))]
     if not paths:
-        pytest.fail("missing fixture (python tests/golden/make_divergence_fixture.py)")
+        pytest.fail("missing fixture (python tests/golden/make_divergence_fixture.py 4 24 {})".format(
+            "f32" if suffix else ""))
     return np.load(paths[0])
 
 
@@ -49,12 +54,11 @@ def _norms(ctx):
 
 @pytest.mark.parametrize("prec", ["fp64", "fp32"])
 def test_c3_plane_divergence_matches_oracle(native, prec, parity_log):
-    F = _fixture()
+    F = _fixture(prec)
     rows = F["rows"]             # iter, |phi|, |rho|, |alp|, err1, err2, finite, max|phi|, max|rho|
     egno, ndim, nx, ny, T = (int(v) for v in F["meta"])
     n = rows.shape[0]
-    over = [int(r[0]) for r in rows if max(r[7], r[8]) > F32_MAX]
-    overflow_it = over[0] if over else None
+    first_o = int(F["first_nonfinite"])     # the oracle's first NaN iteration (0: none within the fixture)
     G = make_problem(egno, ndim, nx, ny, 1, float(F["epsl"]), seeded=False)
     G.update(T=T, dt=float(F["dt"]))
     ctx = device_ctx(G, prec)
@@ -64,7 +68,7 @@ def test_c3_plane_divergence_matches_oracle(native, prec, parity_log):
             assert ctx.path_info("f64_xt") == 1
         ctx.init_state(G["g"][0])
         ctx.set_stop_rules(converge=True, nan=True)
-        last = n if prec == "fp64" else min(n, (overflow_it or n) + 2)
+        last = n if not first_o else first_o + 1
         for it in range(1, last + 1):
             st = ctx.iterate(1, TAU, SIGMA, -1.0, 1)
             if st["nan_seen"] or st["status"] == 2:
@@ -74,17 +78,19 @@ def test_c3_plane_divergence_matches_oracle(native, prec, parity_log):
             dev.append((it, nphi, nrho, st["err2"], fin))
     finally:
         ctx.close()
-    checked = [d for d in dev if d[4] and (overflow_it is None or d[0] < overflow_it)]
+    checked = [d for d in dev if d[4] and d[0] <= n and rows[d[0] - 1, 6] > 0]
     e = {"phi_norm": max(abs(p - rows[i - 1, 1]) / rows[i - 1, 1] for i, p, _, _, _ in checked),
          "rho_norm": max(abs(r - rows[i - 1, 2]) / rows[i - 1, 2] for i, _, r, _, _ in checked),
-         "err2": max(abs(e2 - rows[i - 1, 5]) / rows[i - 1, 5] for i, _, _, e2, _ in checked)}
+         # err2 where the oracle's own float32 sums stayed finite (the device sums in fp64)
+         "err2": max(abs(e2 - rows[i - 1, 5]) / rows[i - 1, 5] for i, _, _, e2, _ in checked
+                     if np.isfinite(rows[i - 1, 5]))}
     tol = FP64_TOL if prec == "fp64" else FP32_TOL
     parity_log("test_c3_plane_divergence_matches_oracle", prec, e, {k: tol for k in e},
-               iterations_checked=len(checked), first_nonfinite_device=first_d, oracle_fp32_overflow_iter=overflow_it,
+               iterations_checked=len(checked), first_nonfinite_device=first_d, first_nonfinite_oracle=first_o,
                rho_norm_device=[d[2] for d in dev], rho_norm_oracle=[float(v) for v in rows[:, 2]])
     assert len(checked) >= min(n, 5), (len(checked), dev)
     assert all(v <= tol for v in e.values()), (e, dev)
-    if prec == "fp64":
-        assert first_d == 0 or first_d > n, first_d     # no NaN within the fixture's iterations
-    elif overflow_it is not None:
-        assert overflow_it - 2 <= first_d <= overflow_it + 2, (first_d, overflow_it)
+    if first_o:
+        assert abs(first_d - first_o) <= 1, (first_d, first_o)
+    else:
+        assert first_d == 0 or first_d > n, (first_d, n)   # no NaN within the fixture's iterations
