@@ -120,7 +120,8 @@ def pmc_traffic(args):
         d = tempfile.mkdtemp(prefix="pdhg_pmc_", dir="/tmp")
         cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "run", "--",
                sys.executable, os.path.abspath(__file__), "--config", args.config, "--steps", "2", "--warmup", "1",
-               "--rho-alp-iters", str(args.rho_alp_iters), "--no-cpu-baseline", "--no-pmc", "--no-probe"]
+               "--rho-alp-iters", str(args.rho_alp_iters), "--precision", args.precision, "--no-cpu-baseline",
+               "--no-pmc", "--no-probe"]
         try:
             subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=600,
                            env=dict(os.environ, TMPDIR="/tmp"))

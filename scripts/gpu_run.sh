@@ -6,7 +6,7 @@
 #   tests[:<pytest -k>]   pytest -m gpu (optionally filtered)
 #   bench[:<args>]        python bench.py <args, commas for spaces>  -> bench_<n>.json
 #                         (leading NAME=value arguments of bench / py steps go to that step's environment)
-#   prof:<config>         scripts/profile.sh <config> <tag>
+#   prof:<config>[,args]  scripts/profile.sh <config> <tag> [bench args]
 #   sh:<script>,<args>    bash <script> <args> ('+' inside an argument stands for a space: counter groups)
 # Every GPU step runs under its own time limit; the first failure ends the script.
 set -o pipefail
@@ -37,7 +37,9 @@ for step in "$@"; do
            tail -3 "$OUT/tests_$n.log" ;;
     bench) env "${ENVV[@]}" timeout -k 10 900 python -u bench.py $arg > "$OUT/bench_$n.json" 2> "$OUT/bench_$n.err" || { echo "bench failed rc=$?"; tail -20 "$OUT/bench_$n.err"; exit 1; }
            cat "$OUT/bench_$n.json" ;;
-    prof)  timeout -k 10 1000 bash scripts/profile.sh "$arg" "${TAG}_$arg" > "$OUT/prof_$n.log" 2>&1 || { echo "prof failed rc=$?"; tail -20 "$OUT/prof_$n.log"; exit 1; }
+    prof)  read -ra TOK <<< "$arg"; PT="${TAG}_$(echo "${TOK[*]}" | tr -c 'A-Za-z0-9_\n' '_')"
+           timeout -k 10 1000 bash scripts/profile.sh "${TOK[0]}" "$PT" "${TOK[@]:1}" > "$OUT/prof_$n.log" 2>&1 || { echo "prof failed rc=$?"; tail -20 "$OUT/prof_$n.log"; exit 1; }
+           echo "profile: gpurun_out/prof_$PT"
            cd "$REPO" ;;
     py)    env "${ENVV[@]}" timeout -k 10 900 python -u $arg > "$OUT/py_$n.log" 2>&1 || { echo "py failed rc=$?"; tail -30 "$OUT/py_$n.log"; exit 1; }
            tail -40 "$OUT/py_$n.log" ;;

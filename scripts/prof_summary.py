@@ -17,7 +17,7 @@ def short(name):
               "k_thomas_chunk_1d", "k_thomas_1d", "k_fs1_1d<0", "k_fs1_1d<1", "k_fs2_1d<0", "k_fs2_1d<1",
               "k_f16a_fwd_1d", "k_f16b_fwd_1d", "k_f16b_inv_1d", "k_f16a_inv_1d", "k_precond_xt_dma_2d",
               "k_fold_partials", "k_fs1w_1d<0", "k_fs1w_1d<1", "k_fs2w_1d<0", "k_fs2w_1d<1",
-              "k_invx_update_1d", "k_dual_1d", "k_finalize_primal", "k_finalize_dual", "k_finalize_outer",
+              "k_invx_update_1d", "k_dual_1d", "k_precond_xt_f64_2d", "k_finalize_primal", "k_finalize_dual", "k_finalize_outer",
               "k_outer_sums", "k_bcast_rows", "k_fill"):
         if k in name:
             return k
