@@ -386,7 +386,8 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
         if (ky < N) hartley_padded<C, float>(A + (r >> 1) * Pad<N>::LINE, N, ky, ha, hb);
         f4set(v, e, (r & 1) ? hb : ha);
       }
-      st4(wk + ((size_t)b * nx + x0) * B + part * 4, v);
+      if (p.dbg & 512) st4(wk + (size_t)x0 * N + 4 * t, v);   // PDHG_DBG 512: task-contiguous stores (timing)
+      else st4(wk + ((size_t)b * nx + x0) * B + part * 4, v);
     }
     lds_sync();
   }
@@ -394,7 +395,7 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
 
 // G workgroups striding over the T * nx/RW row-group tasks; block NT; LDS RW/2 * (N + N/16) * 8 B.
 // sums: [0] sum (phi'-phi)^2, [1] sum phi^2 (old), [2] sum phi'^2
-template <int N, int RW, int NT>
+template <int N, int RW, int NT, int PF = 1>
 __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const float2* __restrict__ twy) {
   using C = float2;
   constexpr int NL = RW / 2;
@@ -436,7 +437,8 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
 #pragma unroll
       for (int i = 0; i < BATCH; ++i) {
         const int t = tl + (i0 + i) * NT;
-        v[i] = ld4(wk + ((size_t)(t >> lCS4) * nx + x0) * B + (t & (CS4 - 1)) * 4);
+        v[i] = (p.dbg & 512) ? ld4(wk + (size_t)x0 * N + 4 * t)   // PDHG_DBG 512: task-contiguous (timing)
+                             : ld4(wk + ((size_t)(t >> lCS4) * nx + x0) * B + (t & (CS4 - 1)) * 4);
       }
 #pragma unroll
       for (int i = 0; i < BATCH; ++i) {
@@ -458,26 +460,31 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
     }
     float* phi = p.phi + (size_t)(j + 1) * plane;
     float* pbar = p.phibar + (size_t)(j + 1) * plane;
-    auto ldpair = [&](int gi, int l, float4& o0, float4& o1) {
-      const size_t idx = (size_t)(x0 + 2 * l) * N + 4 * (tid + gi * NT);
-      o0 = ld4(phi + idx);
-      o1 = ld4(phi + idx + N);
+    // old-phi row pairs, one per step s = gi * NL + l; PF steps in flight ahead of the one being updated
+    // (step 0 before the transform, steps 1 .. PF-1 right after it, when the FFT's registers are free)
+    constexpr int NS = GPT * NL;
+    float4 op[NS][2];
+    auto ldstep = [&](int s) {
+      const size_t idx = (size_t)(x0 + 2 * (s % NL)) * N + 4 * (tid + (s / NL) * NT);
+      op[s][0] = ld4(phi + idx);
+      op[s][1] = ld4(phi + idx + N);
     };
-    float4 nx0, nx1;
-    ldpair(0, 0, nx0, nx1);
+    ldstep(0);
     lds_sync();
     if (!(p.dbg & 64)) {   // timing experiments only (PDHG_DBG): 64 skips the transform
       if constexpr (TWL) lds_fft_inplace_tl<C, N, NL, NT>(A, twl);
       else lds_fft_inplace<C, N, NL, NT>(A, twy);
     }
 #pragma unroll
+    for (int s = 1; s < PF && s < NS; ++s) ldstep(s);
+#pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
       const int y = 4 * (tid + gi * NT);
 #pragma unroll
       for (int l = 0; l < NL; ++l) {   // rows 2l (real part) and 2l+1 (imaginary part) of line l
-        const float4 o4[2] = {nx0, nx1};
-        if (l + 1 < NL) ldpair(gi, l + 1, nx0, nx1);
-        else if (gi + 1 < GPT) ldpair(gi + 1, 0, nx0, nx1);
+        const int st = gi * NL + l;
+        const float4 o4[2] = {op[st][0], op[st][1]};
+        if (st + PF < NS) ldstep(st + PF);
         const C* Z = A + l * Pad<N>::LINE;
         float4 u[2];
 #pragma unroll

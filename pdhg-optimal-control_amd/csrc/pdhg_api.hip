@@ -104,6 +104,8 @@ struct Impl : ImplBase {
   C* twx = nullptr;
   C* twy = nullptr;
   std::vector<void*> allocs;
+  int n_big = 0;   // large allocations made (PDHG_STAGGER experiment)
+  int n_contig_fail = 0;   // PDHG_ALLOC=contig requests that fell back to hipMalloc
   size_t dev_bytes = 0;
   int na = 0, n_dead = 0;
   bool two_sets = false;
@@ -114,6 +116,7 @@ struct Impl : ImplBase {
   int nt_row = 256;   // threads of the generic 2-D row kernels (k_res_fwdy_2d, k_invy_update_2d)
   int rows_var = 0;                       // row-kernel shape variant (see with_fast_rows)
   int half_nt = 3;                        // ny = 4096 row kernels with 512 threads (bit 0 residual, bit 1 update)
+  int upd_pf = 4;                         // update kernel (512 threads): old-phi row pairs in flight (1..4)
   bool fast_dual = false;                 // fp32 time-marching float4 dual kernel (k_dual_fast_2d)
   int NTd = 256, gxd = 0, gyd = 0, gzd = 0, jchunk_d = 1;
   int dual_rx = 0;   // > 0: k_dual_lds_2d with dual_rx x rows per workgroup (x neighbours through LDS)
@@ -191,11 +194,20 @@ struct Impl : ImplBase {
   int alloc(T** p, size_t n) {
     void* q = nullptr;
     const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
-    hipError_t e = hipMalloc(&q, bytes);
+    // large arrays: base offset (k mod 16) * stagger bytes (tuning experiments, PDHG_STAGGER; 0 = none)
+    const size_t stagger = [] { const char* e = getenv("PDHG_STAGGER"); return e ? (size_t)atoll(e) : (size_t)0; }();
+    const size_t off = (stagger && bytes >= ((size_t)64 << 20)) ? (size_t)(n_big++ % 16) * stagger : 0;
+    const char* am = getenv("PDHG_ALLOC");   // tuning experiments: "contig" = physically contiguous
+    hipError_t e = hipErrorOutOfMemory;
+    if (am && !strcmp(am, "contig") && bytes >= ((size_t)64 << 20)) {
+      e = hipExtMallocWithFlags(&q, bytes + (off ? 15 * stagger : 0), hipDeviceMallocContiguous);
+      if (e != hipSuccess) { (void)hipGetLastError(); n_contig_fail++; }
+    }
+    if (e != hipSuccess) e = hipMalloc(&q, bytes + (off ? 15 * stagger : 0));
     if (e != hipSuccess) return fail(PDHG_ERR_NOMEM, "hipMalloc(%zu bytes) failed: %s", bytes, hipGetErrorString(e));
     allocs.push_back(q);
     dev_bytes += bytes;
-    *p = static_cast<T*>(q);
+    *p = reinterpret_cast<T*>(static_cast<char*>(q) + off);
     return PDHG_OK;
   }
 
@@ -332,6 +344,7 @@ struct Impl : ImplBase {
       }
       if (const char* e = getenv("PDHG_ROWS_VAR")) rows_var = atoi(e);   // tuning override
       if (const char* e = getenv("PDHG_HALF_NT")) half_nt = atoi(e);     // tuning: 1 fused residual, 2 update
+      if (const char* e = getenv("PDHG_UPD_PF")) upd_pf = atoi(e);       // tuning: update prefetch depth
       if (sizeof(R) == 4 && ply.pow2 && ny >= 256 && ny <= 8192) {
         RWf = (ny == 8192) ? 4 : 8;
         NTf = std::min(1024, ny / 4);
@@ -897,10 +910,18 @@ struct Impl : ImplBase {
           if constexpr (sizeof(R) == 4) {
             if constexpr (NT_ == 1024 && RW_ == 8) {
               if (half_nt & 2) {
-                if ((r2 = ensure_lds(k_invy_update_fast_2d<N_, RW_, 512>, lds_fast_tw))) return r2;
-                hipLaunchKernelGGL((k_invy_update_fast_2d<N_, RW_, 512>), dim3(g_fast_upd), dim3(512), lds_fast_tw,
-                                   stream, p, twy);
-                return (int)PDHG_OK;
+                auto go = [&](auto kern) {
+                  int r3;
+                  if ((r3 = ensure_lds(kern, lds_fast_tw))) return r3;
+                  hipLaunchKernelGGL(kern, dim3(g_fast_upd), dim3(512), lds_fast_tw, stream, p, twy);
+                  return (int)PDHG_OK;
+                };
+                switch (upd_pf) {
+                  case 2: return go(k_invy_update_fast_2d<N_, RW_, 512, 2>);
+                  case 3: return go(k_invy_update_fast_2d<N_, RW_, 512, 3>);
+                  case 4: return go(k_invy_update_fast_2d<N_, RW_, 512, 4>);
+                  default: return go(k_invy_update_fast_2d<N_, RW_, 512, 1>);
+                }
               }
             }
             if ((r2 = ensure_lds(k_invy_update_fast_2d<N_, RW_, NT_>, lds_fast_tw))) return r2;
@@ -2000,6 +2021,7 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
     const std::string k(key);
     if (k == "fused_residual") *value = im.fuse_res ? 1 : 0;
     else if (k == "fast_rows") *value = im.fast_rows ? 1 : 0;
+    else if (k == "contig_fail") *value = im.n_contig_fail;
     else if (k == "fast_dual") *value = im.fast_dual ? im.dual_rx : -1;
     else if (k == "fast_xt")
       *value = im.fast_xt ? (im.batch_xt && !im.half_real ? (im.xt_dma && im.pb.nx == 4096 ? 4 : 3) : im.ws_xt ? 2 : 1) : 0;
