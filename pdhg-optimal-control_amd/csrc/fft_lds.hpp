@@ -318,13 +318,12 @@ __host__ __device__ constexpr int twlds_size(int n) {
   return 3 * ((n > 16 ? 16 : 0) + (n > 256 ? 256 : 0) + (n > 4096 ? 4096 : 0));
 }
 
-template <typename C, int N, int NL, int NT, int LS, int R, bool REG>
+template <typename C, int N, int NL, int NT, int LS, int R, bool REG, int LINE = Pad<N>::LINE>
 __device__ __forceinline__ void inplace_pass(C* __restrict__ a, const C* __restrict__ tw, const C* twl) {
   constexpr int nR = N / R;
   constexpr int tws = N / (LS * R);
   constexpr int total = nR * NL;
   constexpr int PER = (total + NT - 1) / NT;
-  constexpr int LINE = Pad<N>::LINE;
   static_assert(nR % 16 == 0 && (LS == 1 || LS % 16 == 0) && (LS > 1 || R == 16), "padded schedule");
   C v[PER][R];
   int base[PER];
@@ -381,27 +380,28 @@ __device__ __forceinline__ void inplace_pass(C* __restrict__ a, const C* __restr
   lds_sync();
 }
 
-template <typename C, int N, int NL, int NT, int LS, bool REG>
+template <typename C, int N, int NL, int NT, int LS, bool REG, int LINE = Pad<N>::LINE>
 __device__ __forceinline__ void inplace_passes(C* a, const C* __restrict__ tw, const C* twl) {
   if constexpr (LS < N) {
     constexpr int rem = N / LS;
     constexpr int R = (rem >= 16) ? 16 : rem;
-    inplace_pass<C, N, NL, NT, LS, R, REG>(a, tw, twl);
-    inplace_passes<C, N, NL, NT, LS * R, REG>(a, tw, twl);
+    inplace_pass<C, N, NL, NT, LS, R, REG, LINE>(a, tw, twl);
+    inplace_passes<C, N, NL, NT, LS * R, REG, LINE>(a, tw, twl);
   }
 }
 
 // Forward FFT in place of NL padded line-major lines (element e of line l at a[l*LINE + pix(e)]).
-template <typename C, int N, int NL, int NT>
+template <typename C, int N, int NL, int NT, int LINE = Pad<N>::LINE>
 __device__ __forceinline__ void lds_fft_inplace(C* a, const C* __restrict__ tw) {
-  inplace_passes<C, N, NL, NT, 1, false>(a, tw, nullptr);
+  inplace_passes<C, N, NL, NT, 1, false, LINE>(a, tw, nullptr);
 }
 
 // Same transform with the twiddle seeds read from an LDS table filled by fill_twlds.
-template <typename C, int N, int NL, int NT>
+template <typename C, int N, int NL, int NT, int LINE = Pad<N>::LINE>
 __device__ __forceinline__ void lds_fft_inplace_tl(C* a, const C* twl) {
-  inplace_passes<C, N, NL, NT, 1, true>(a, nullptr, twl);
+  inplace_passes<C, N, NL, NT, 1, true, LINE>(a, nullptr, twl);
 }
+
 
 // Fill the TwLds<N> table from the global twiddle table (W_N^m at tw[m]); caller syncs before use.
 template <typename C, int N>

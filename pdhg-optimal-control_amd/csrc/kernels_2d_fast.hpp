@@ -33,6 +33,32 @@ __device__ __forceinline__ float m2f(float rho, float alp, float a) {   // (rho 
 }
 
 // grid: T * nx/RW row-group tasks (XCD-aware); block NT = min(1024, N/4); LDS RW/2 * (N + N/16) * 8 B.
+// float4 number `part` of the blocked-layout chunk of column block b (RW rows x B columns, row-major) from
+// the task's RW/2 transformed lines in LDS (line l = rows 2l, 2l+1 as real / imaginary part, stride LINE).
+// B = 2: the float4 holds rows 2 part, 2 part + 1 at columns 2b, 2b + 1, i.e. the Hartley values of line
+// `part` at ky = 2b, 2b+1 -- two element pairs read once for both rows (the generic path reads them per row).
+template <int N, int LINE>
+__device__ __forceinline__ float4 unpack_chunk4(const float2* A, int b, int part, int B, int lB) {
+  if (B == 2) {   // ky = 2b + 1 < N always (N even)
+    const float2* Z = A + part * LINE;
+    float a0, b0, a1, b1;
+    hartley_padded<float2, float>(Z, N, 2 * b, a0, b0);
+    hartley_padded<float2, float>(Z, N, 2 * b + 1, a1, b1);
+    return make_float4(a0, a1, b0, b1);
+  }
+  float4 v;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int f = part * 4 + e;
+    const int r = f >> lB, c = f & (B - 1);
+    const int ky = b * B + c;
+    float ha = 0.f, hb = 0.f;
+    if (ky < N) hartley_padded<float2, float>(A + (r >> 1) * LINE, N, ky, ha, hb);
+    f4set(v, e, (r & 1) ? hb : ha);
+  }
+  return v;
+}
+
 template <int EGNO, int N, int RW, int NT>
 __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const float2* __restrict__ twy) {
   using C = float2;
@@ -233,17 +259,7 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const floa
   float* wk = p.work + (size_t)j * nb * nx * B;
   for (int t = threadIdx.x; t < nb * CS4; t += NT) {
     const int b = t >> lCS4, part = t & (CS4 - 1);
-    float4 v;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int f = part * 4 + e;
-      const int r = f >> p.lB, c = f & (B - 1);
-      const int ky = b * B + c;
-      float ha = 0.f, hb = 0.f;
-      if (ky < N) hartley_padded<C, float>(A + (r >> 1) * Pad<N>::LINE, N, ky, ha, hb);
-      f4set(v, e, (r & 1) ? hb : ha);
-    }
-    st4(wk + ((size_t)b * nx + x0) * B + part * 4, v);
+    st4(wk + ((size_t)b * nx + x0) * B + part * 4, unpack_chunk4<N, Pad<N>::LINE>(A, b, part, B, p.lB));
   }
 }
 
@@ -263,6 +279,7 @@ template <int EGNO, int N, int RW, int NT>
 __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const float2* __restrict__ twy) {
   using C = float2;
   constexpr int NL = RW / 2;
+  constexpr int LN = Pad<N>::LINE;
   constexpr int GPT = (N / 4) / NT;
   constexpr int YW = 256, NSTRIP = N / YW;
   constexpr int NEY = RW * NSTRIP * 2;   // strip-edge terms of one task
@@ -275,7 +292,7 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
   // twiddle seeds in LDS behind the lines (N <= 4096): the passes then issue no global loads, so the next
   // task's rows stay in flight across the whole transform (vmcnt drains in order)
   constexpr bool TWL = N <= 4096;
-  C* twl = A + NL * Pad<N>::LINE;
+  C* twl = A + NL * LN;
   if constexpr (TWL) fill_twlds<C, N>(twl, twy);
   const int nx = p.nx;
   const int ngx = nx / RW;
@@ -356,7 +373,7 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
       }
 #pragma unroll
       for (int l = 0; l < RW / 2; ++l) {   // rows 2l, 2l+1 -> line l (real, imaginary): one 8-B LDS store each
-        C* Al = A + l * Pad<N>::LINE + pix(y);
+        C* Al = A + l * LN + pix(y);
 #pragma unroll
         for (int e = 0; e < 4; ++e) Al[e] = make_float2(f4(v[2 * l], e), f4(v[2 * l + 1], e));
       }
@@ -376,16 +393,7 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
     float* wk = p.work + (size_t)j * nb * nx * B;
     for (int t = tid; t < nb * CS4 && !(p.dbg & 32); t += NT) {   // PDHG_DBG 32: no unpack / stores (timing)
       const int b = t >> lCS4, part = t & (CS4 - 1);
-      float4 v;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int f = part * 4 + e;
-        const int r = f >> p.lB, c = f & (B - 1);
-        const int ky = b * B + c;
-        float ha = 0.f, hb = 0.f;
-        if (ky < N) hartley_padded<C, float>(A + (r >> 1) * Pad<N>::LINE, N, ky, ha, hb);
-        f4set(v, e, (r & 1) ? hb : ha);
-      }
+      const float4 v = unpack_chunk4<N, LN>(A, b, part, B, p.lB);
       if (p.dbg & 512) st4(wk + (size_t)x0 * N + 4 * t, v);   // PDHG_DBG 512: task-contiguous stores (timing)
       else st4(wk + ((size_t)b * nx + x0) * B + part * 4, v);
     }
@@ -472,7 +480,7 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
     ldstep(0);
     lds_sync();
     if (!(p.dbg & 64)) {   // timing experiments only (PDHG_DBG): 64 skips the transform
-      if constexpr (TWL) lds_fft_inplace_tl<C, N, NL, NT>(A, twl);
+      if constexpr (TWL) lds_fft_inplace_tl<C, N, NL, NT, Pad<N>::LINE>(A, twl);
       else lds_fft_inplace<C, N, NL, NT>(A, twy);
     }
 #pragma unroll

@@ -104,8 +104,8 @@ struct Impl : ImplBase {
   C* twx = nullptr;
   C* twy = nullptr;
   std::vector<void*> allocs;
-  int n_big = 0;   // large allocations made (PDHG_STAGGER experiment)
-  int n_contig_fail = 0;   // PDHG_ALLOC=contig requests that fell back to hipMalloc
+  bool contig_alloc = [] { const char* e = getenv("PDHG_ALLOC"); return !(e && !strcmp(e, "none")); }();
+  int n_contig_fail = 0;   // contiguous requests that fell back to hipMalloc
   size_t dev_bytes = 0;
   int na = 0, n_dead = 0;
   bool two_sets = false;
@@ -194,20 +194,24 @@ struct Impl : ImplBase {
   int alloc(T** p, size_t n) {
     void* q = nullptr;
     const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
-    // large arrays: base offset (k mod 16) * stagger bytes (tuning experiments, PDHG_STAGGER; 0 = none)
-    const size_t stagger = [] { const char* e = getenv("PDHG_STAGGER"); return e ? (size_t)atoll(e) : (size_t)0; }();
-    const size_t off = (stagger && bytes >= ((size_t)64 << 20)) ? (size_t)(n_big++ % 16) * stagger : 0;
-    const char* am = getenv("PDHG_ALLOC");   // tuning experiments: "contig" = physically contiguous
+    // Large arrays physically contiguous: with the default allocator the physical placement of the ~13 GB
+    // planes differs from context to context, and so did the dual / update times (C3 dual 30.3 - 35.4 ms
+    // across contexts, stable to 0.05 ms within one); contiguous planes ran 30.0 - 30.2 (interleaved A/B,
+    // DESIGN.md section 4).  Falls back to hipMalloc (counted: path_info "contig_fail"); PDHG_ALLOC=none
+    // turns it off.
     hipError_t e = hipErrorOutOfMemory;
-    if (am && !strcmp(am, "contig") && bytes >= ((size_t)64 << 20)) {
-      e = hipExtMallocWithFlags(&q, bytes + (off ? 15 * stagger : 0), hipDeviceMallocContiguous);
-      if (e != hipSuccess) { (void)hipGetLastError(); n_contig_fail++; }
+    if (bytes >= ((size_t)64 << 20) && contig_alloc) {
+      e = hipExtMallocWithFlags(&q, bytes, hipDeviceMallocContiguous);
+      if (e != hipSuccess) {
+        (void)hipGetLastError();
+        n_contig_fail++;
+      }
     }
-    if (e != hipSuccess) e = hipMalloc(&q, bytes + (off ? 15 * stagger : 0));
+    if (e != hipSuccess) e = hipMalloc(&q, bytes);
     if (e != hipSuccess) return fail(PDHG_ERR_NOMEM, "hipMalloc(%zu bytes) failed: %s", bytes, hipGetErrorString(e));
     allocs.push_back(q);
     dev_bytes += bytes;
-    *p = reinterpret_cast<T*>(static_cast<char*>(q) + off);
+    *p = static_cast<T*>(q);
     return PDHG_OK;
   }
 

@@ -66,7 +66,7 @@ def run_variant(cfg, steps, overrides, k=1):
 
 def main():
     cfg, rounds, steps = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
-    variants = [dict(kv.split("=", 1) for kv in v.split()) for v in sys.argv[4:]] or [{}]
+    variants = [dict(kv.split("=", 1) for kv in v.replace("+", " ").split()) for v in sys.argv[4:]] or [{}]
     res = [[] for _ in variants]
     for r in range(rounds):
         for i, ov in enumerate(variants):
