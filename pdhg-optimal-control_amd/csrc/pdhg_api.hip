@@ -104,7 +104,11 @@ struct Impl : ImplBase {
   C* twx = nullptr;
   C* twy = nullptr;
   std::vector<void*> allocs;
-  bool contig_alloc = [] { const char* e = getenv("PDHG_ALLOC"); return !(e && !strcmp(e, "none")); }();
+  // PDHG_ALLOC: "contig" / "none" override the default (contiguous planes for fp32 2-D contexts only)
+  int alloc_mode = [] {
+    const char* e = getenv("PDHG_ALLOC");
+    return !e ? 0 : !strcmp(e, "contig") ? 1 : !strcmp(e, "none") ? -1 : 0;
+  }();
   int n_contig_fail = 0;   // contiguous requests that fell back to hipMalloc
   size_t dev_bytes = 0;
   int na = 0, n_dead = 0;
@@ -194,13 +198,15 @@ struct Impl : ImplBase {
   int alloc(T** p, size_t n) {
     void* q = nullptr;
     const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
-    // Large arrays physically contiguous: with the default allocator the physical placement of the ~13 GB
-    // planes differs from context to context, and so did the dual / update times (C3 dual 30.3 - 35.4 ms
-    // across contexts, stable to 0.05 ms within one); contiguous planes ran 30.0 - 30.2 (interleaved A/B,
-    // DESIGN.md section 4).  Falls back to hipMalloc (counted: path_info "contig_fail"); PDHG_ALLOC=none
-    // turns it off.
+    // Large arrays of fp32 2-D contexts physically contiguous: with the default allocator the physical
+    // placement of C3's 13 GB planes differs from context to context, and so did the dual / update times
+    // (dual 30.3 - 35.4 ms across contexts, stable to 0.05 ms within one); contiguous planes ran 29.5 - 30.5.
+    // The same placement made fp64 C3's generic residual 71 -> 91 ms and fp32 C1's update 0.12 -> 0.14 ms,
+    // and C2 was neutral (interleaved A/B), hence fp32 2-D only.  Falls back to
+    // hipMalloc (counted: path_info "contig_fail").
+    const bool contig = alloc_mode > 0 || (alloc_mode == 0 && sizeof(R) == 4 && pb.ndim == 2);
     hipError_t e = hipErrorOutOfMemory;
-    if (bytes >= ((size_t)64 << 20) && contig_alloc) {
+    if (bytes >= ((size_t)64 << 20) && contig) {
       e = hipExtMallocWithFlags(&q, bytes, hipDeviceMallocContiguous);
       if (e != hipSuccess) {
         (void)hipGetLastError();

@@ -5,6 +5,7 @@ variants are created, timed and destroyed in turn, ROUNDS times interleaved, so 
 alike.  Per kernel class: the median over rounds of the HIP-event average (pdhg_profile_query).
 
 usage: python scripts/ab_env.py <config> <rounds> <steps> "A=1 B=2" "A=2" ...   ("" = no overrides)
+AB_PREC=fp64: the contexts' precision (default fp32).
 AB_REPS=n: n timed segments per context (re-initialised state each), to separate per-context from per-run spread.
 """
 import json
@@ -32,7 +33,7 @@ def run_variant(cfg, steps, overrides, k=1):
         T = nt - 1
         xs, ys = bench.grid(ndim, nx, ny)
         ctx = PDHGContext(egno, ndim, nx, ny, T, 2.0 / nx, 2.0 / ny if ndim == 2 else 0.0, 1.0 / T, xs, ys,
-                          epsl=epsl, rho_alp_iters=k, device=0)
+                          epsl=epsl, rho_alp_iters=k, device=0, precision=os.environ.get("AB_PREC", "fp32"))
     finally:
         for n, v in saved.items():
             if v is None:
