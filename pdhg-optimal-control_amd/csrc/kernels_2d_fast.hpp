@@ -23,13 +23,55 @@ __device__ __forceinline__ void f4set(float4& v, int e, float x) {
 }
 __device__ __forceinline__ float4 z4() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
-template <int EGNO>
-__device__ __forceinline__ float m1f(float rho, float alp, float a) {   // (rho + 1e-4) f(alp)^+
-  return (rho + 1e-4f) * fpos<float>(fval<float, EGNO>(alp, a));
+// fp64 counterparts (4 consecutive y per lane as two 16-B accesses), for the kernels templated on R
+struct dbl4 {
+  double x, y, z, w;
+};
+template <typename R> struct V4s { using type = float4; };
+template <> struct V4s<double> { using type = dbl4; };
+template <typename R> using V4 = typename V4s<R>::type;
+__device__ __forceinline__ dbl4 ld4(const double* p) {
+  const double2 a = reinterpret_cast<const double2*>(p)[0], b = reinterpret_cast<const double2*>(p)[1];
+  return dbl4{a.x, a.y, b.x, b.y};
 }
-template <int EGNO>
-__device__ __forceinline__ float m2f(float rho, float alp, float a) {   // (rho + 1e-4) f(alp)^-
-  return (rho + 1e-4f) * fneg<float>(fval<float, EGNO>(alp, a));
+__device__ __forceinline__ void st4(double* p, dbl4 v) {
+  reinterpret_cast<double2*>(p)[0] = make_double2(v.x, v.y);
+  reinterpret_cast<double2*>(p)[1] = make_double2(v.z, v.w);
+}
+__device__ __forceinline__ double f4(const dbl4& v, int e) { return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w; }
+__device__ __forceinline__ void f4set(dbl4& v, int e, double x) {
+  if (e == 0) v.x = x; else if (e == 1) v.y = x; else if (e == 2) v.z = x; else v.w = x;
+}
+template <typename R> __device__ __forceinline__ V4<R> z4r() { return z4(); }
+template <> __device__ __forceinline__ dbl4 z4r<double>() { return dbl4{0.0, 0.0, 0.0, 0.0}; }
+__device__ __forceinline__ float4 mk4(float a, float b, float c, float d) { return make_float4(a, b, c, d); }
+__device__ __forceinline__ dbl4 mk4(double a, double b, double c, double d) { return dbl4{a, b, c, d}; }
+// the float lane shifts (common.hpp) on the two halves of a double
+__device__ __forceinline__ double lane_from_prev(double v, double edge) {
+  const long long vi = __builtin_bit_cast(long long, v), ei = __builtin_bit_cast(long long, edge);
+  const float lo = lane_from_prev(__builtin_bit_cast(float, (int)vi), __builtin_bit_cast(float, (int)ei));
+  const float hi = lane_from_prev(__builtin_bit_cast(float, (int)(vi >> 32)), __builtin_bit_cast(float, (int)(ei >> 32)));
+  return __builtin_bit_cast(double, (long long)(unsigned)__builtin_bit_cast(int, lo) |
+                                        ((long long)__builtin_bit_cast(int, hi) << 32));
+}
+__device__ __forceinline__ double lane_from_next(double v, double edge) {
+  const long long vi = __builtin_bit_cast(long long, v), ei = __builtin_bit_cast(long long, edge);
+  const float lo = lane_from_next(__builtin_bit_cast(float, (int)vi), __builtin_bit_cast(float, (int)ei));
+  const float hi = lane_from_next(__builtin_bit_cast(float, (int)(vi >> 32)), __builtin_bit_cast(float, (int)(ei >> 32)));
+  return __builtin_bit_cast(double, (long long)(unsigned)__builtin_bit_cast(int, lo) |
+                                        ((long long)__builtin_bit_cast(int, hi) << 32));
+}
+
+__device__ __forceinline__ float fmar(float a, float b, float c) { return fmaf(a, b, c); }
+__device__ __forceinline__ double fmar(double a, double b, double c) { return fma(a, b, c); }
+
+template <int EGNO, typename R = float>
+__device__ __forceinline__ R m1f(R rho, R alp, R a) {   // (rho + 1e-4) f(alp)^+
+  return (rho + (R)1e-4) * fpos<R>(fval<R, EGNO>(alp, a));
+}
+template <int EGNO, typename R = float>
+__device__ __forceinline__ R m2f(R rho, R alp, R a) {   // (rho + 1e-4) f(alp)^-
+  return (rho + (R)1e-4) * fneg<R>(fval<R, EGNO>(alp, a));
 }
 
 // grid: T * nx/RW row-group tasks (XCD-aware); block NT = min(1024, N/4); LDS RW/2 * (N + N/16) * 8 B.
@@ -37,33 +79,35 @@ __device__ __forceinline__ float m2f(float rho, float alp, float a) {   // (rho 
 // the task's RW/2 transformed lines in LDS (line l = rows 2l, 2l+1 as real / imaginary part, stride LINE).
 // B = 2: the float4 holds rows 2 part, 2 part + 1 at columns 2b, 2b + 1, i.e. the Hartley values of line
 // `part` at ky = 2b, 2b+1 -- two element pairs read once for both rows (the generic path reads them per row).
-template <int N, int LINE>
-__device__ __forceinline__ float4 unpack_chunk4(const float2* A, int b, int part, int B, int lB) {
+template <int N, int LINE, typename R = float>
+__device__ __forceinline__ V4<R> unpack_chunk4(const cplx<R>* A, int b, int part, int B, int lB) {
+  using C = cplx<R>;
   if (B == 2) {   // ky = 2b + 1 < N always (N even)
-    const float2* Z = A + part * LINE;
-    float a0, b0, a1, b1;
-    hartley_padded<float2, float>(Z, N, 2 * b, a0, b0);
-    hartley_padded<float2, float>(Z, N, 2 * b + 1, a1, b1);
-    return make_float4(a0, a1, b0, b1);
+    const C* Z = A + part * LINE;
+    R a0, b0, a1, b1;
+    hartley_padded<C, R>(Z, N, 2 * b, a0, b0);
+    hartley_padded<C, R>(Z, N, 2 * b + 1, a1, b1);
+    return mk4(a0, a1, b0, b1);
   }
-  float4 v;
+  V4<R> v;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int f = part * 4 + e;
     const int r = f >> lB, c = f & (B - 1);
     const int ky = b * B + c;
-    float ha = 0.f, hb = 0.f;
-    if (ky < N) hartley_padded<float2, float>(A + (r >> 1) * LINE, N, ky, ha, hb);
+    R ha = (R)0, hb = (R)0;
+    if (ky < N) hartley_padded<C, R>(A + (r >> 1) * LINE, N, ky, ha, hb);
     f4set(v, e, (r & 1) ? hb : ha);
   }
   return v;
 }
 
-template <int EGNO, int N, int RW, int NT>
-__global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const float2* __restrict__ twy) {
-  using C = float2;
+template <int EGNO, int N, int RW, int NT, typename R = float>
+__global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<R> p, const cplx<R>* __restrict__ twy) {
+  using C = cplx<R>;
+  using V = V4<R>;
   constexpr int NL = RW / 2;
-  constexpr int GPT = (N / 4) / NT;   // float4 y-groups per thread
+  constexpr int GPT = (N / 4) / NT;   // V y-groups per thread
   if (p.ctrl->done) return;
   extern __shared__ __align__(16) unsigned char smem_raw[];
   C* A = reinterpret_cast<C*>(smem_raw);
@@ -93,13 +137,13 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const floa
   j += p.row_base;
   const int x0 = gx * RW;
   const size_t plane = (size_t)nx * N;
-  const float* rj = p.rho[cur] + (size_t)j * plane;
-  const float* a1x = p.alp[cur][0] + (size_t)j * plane;
-  const float* a2x = p.alp[cur][1] + (size_t)j * plane;
-  const float* a1y = (EGNO == 3) ? nullptr : p.alp[cur][2] + (size_t)j * plane;
-  const float* a2y = (EGNO == 3) ? nullptr : p.alp[cur][3] + (size_t)j * plane;
-  const float cdt = (j == T - 1 && p.last_slab) ? p.c_over_dt : 0.f;   // +c/dt on the window's last row
-  const bool use_eps = p.epsl != 0.f;
+  const R* rj = p.rho[cur] + (size_t)j * plane;
+  const R* a1x = p.alp[cur][0] + (size_t)j * plane;
+  const R* a2x = p.alp[cur][1] + (size_t)j * plane;
+  const R* a1y = (EGNO == 3) ? nullptr : p.alp[cur][2] + (size_t)j * plane;
+  const R* a2y = (EGNO == 3) ? nullptr : p.alp[cur][3] + (size_t)j * plane;
+  const R cdt = (j == T - 1 && p.last_slab) ? p.c_over_dt : (R)0;   // +c/dt on the window's last row
+  const bool use_eps = p.epsl != (R)0;
 
   // Branch-free row loop: every load reads a valid address (rows/columns outside a Dirichlet edge
   // are clamped and zeroed by a select afterwards), so the loads of consecutive rows stay in
@@ -111,7 +155,7 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const floa
   // rho row j+1: local, or the next slab's first row (halo), or zero after the window's last row
   const bool halo_j = (j + 1 >= T) && !p.last_slab;
   const bool last_j = (j + 1 >= T) && p.last_slab;
-  const float* rnx = last_j ? rj : halo_j ? p.rho_halo : p.rho[cur] + (size_t)(j + 1) * plane;
+  const R* rnx = last_j ? rj : halo_j ? p.rho_halo : p.rho[cur] + (size_t)(j + 1) * plane;
   const int lane = threadIdx.x & (kWave - 1);
 #pragma unroll
   for (int gi = 0; gi < GPT; ++gi) {
@@ -121,35 +165,35 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const floa
     const int ywm = nb_index(yw0 - 1, N, p.bcy), ywp = nb_index(yw0 + 4 * kWave, N, p.bcy);
     const bool zym = ywm < 0, zyp = ywp < 0;
     const int ywmc = zym ? 0 : ywm, ywpc = zyp ? 0 : ywp;
-    float4 ay4 = z4();
-    float aym = 0.f, ayp = 0.f;
+    V ay4 = z4r<R>();
+    R aym = (R)0, ayp = (R)0;
     if constexpr (EGNO != 3) {
       ay4 = ld4(p.ay + y);
-      aym = lane_from_prev(ay4.w, zym ? 0.f : p.ay[ywmc]);
-      ayp = lane_from_next(ay4.x, zyp ? 0.f : p.ay[ywpc]);
+      aym = lane_from_prev(ay4.w, zym ? (R)0 : p.ay[ywmc]);
+      ayp = lane_from_next(ay4.x, zyp ? (R)0 : p.ay[ywpc]);
     }
-    float4 r_m = ld4(rj + (size_t)xm0c * N + y);
-    float4 a1_m = ld4(a1x + (size_t)xm0c * N + y);
-    float ax_m = p.ax[xm0c];
+    V r_m = ld4(rj + (size_t)xm0c * N + y);
+    V a1_m = ld4(a1x + (size_t)xm0c * N + y);
+    R ax_m = p.ax[xm0c];
     if (zm) {
-      r_m = z4();
-      a1_m = z4();
-      ax_m = 0.f;
+      r_m = z4r<R>();
+      a1_m = z4r<R>();
+      ax_m = (R)0;
     }
-    float4 r_c = ld4(rj + (size_t)x0 * N + y);
-    float4 a2_c = ld4(a2x + (size_t)x0 * N + y);
-    float ax_c = p.ax[x0];
+    V r_c = ld4(rj + (size_t)x0 * N + y);
+    V a2_c = ld4(a2x + (size_t)x0 * N + y);
+    R ax_c = p.ax[x0];
     // flux carries: m1x at the row above, m2x at the current row
-    float m1x_prev[4], m2x_cur[4];
+    R m1x_prev[4], m2x_cur[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      m1x_prev[e] = zm ? 0.f : m1f<EGNO>(f4(r_m, e), f4(a1_m, e), ax_m);
-      m2x_cur[e] = m2f<EGNO>(f4(r_c, e), f4(a2_c, e), ax_c);
+      m1x_prev[e] = zm ? (R)0 : m1f<EGNO, R>(f4(r_m, e), f4(a1_m, e), ax_m);
+      m2x_cur[e] = m2f<EGNO, R>(f4(r_c, e), f4(a2_c, e), ax_c);
     }
     // software pipeline: the loads of row r+1 are issued before row r is computed
     struct RowIn {
-      float4 r_p, a2_p, a1_c, rn4, a1y4, a2y4;
-      float ax_p, e_rm, e_rp, e_a1m, e_a2p;
+      V r_p, a2_p, a1_c, rn4, a1y4, a2y4;
+      R ax_p, e_rm, e_rp, e_a1m, e_a2p;
     };
     auto load_row = [&](int r) {
       RowIn in;
@@ -169,8 +213,8 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const floa
         in.e_a1m = a1y[ro + ywmc];
         in.e_a2p = a2y[ro + ywpc];
       } else {
-        in.a1y4 = in.a2y4 = z4();
-        in.e_a1m = in.e_a2p = 0.f;
+        in.a1y4 = in.a2y4 = z4r<R>();
+        in.e_a1m = in.e_a2p = (R)0;
       }
       return in;
     };
@@ -180,67 +224,67 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const floa
       const RowIn in = nxt;
       if (r + 1 < RW) nxt = load_row(r + 1);
       const bool zp = (r + 1 == RW) && zpl;
-      float4 r_p = in.r_p, a2_p = in.a2_p, rn4 = in.rn4;
-      float ax_p = in.ax_p;
-      const float4 a1_c = in.a1_c;
+      V r_p = in.r_p, a2_p = in.a2_p, rn4 = in.rn4;
+      R ax_p = in.ax_p;
+      const V a1_c = in.a1_c;
       if (zp) {
-        r_p = z4();
-        a2_p = z4();
-        ax_p = 0.f;
+        r_p = z4r<R>();
+        a2_p = z4r<R>();
+        ax_p = (R)0;
       }
-      if (last_j) rn4 = z4();
-      const float4 a1y4 = in.a1y4, a2y4 = in.a2y4;
-      float a1y_m = 0.f, a2y_p = 0.f;
+      if (last_j) rn4 = z4r<R>();
+      const V a1y4 = in.a1y4, a2y4 = in.a2y4;
+      R a1y_m = (R)0, a2y_p = (R)0;
       // y neighbours: from the adjacent lanes (DPP); the wave-edge values are uniform loads
       if constexpr (EGNO != 3) {
-        a1y_m = lane_from_prev(a1y4.w, zym ? 0.f : in.e_a1m);
-        a2y_p = lane_from_next(a2y4.x, zyp ? 0.f : in.e_a2p);
+        a1y_m = lane_from_prev(a1y4.w, zym ? (R)0 : in.e_a1m);
+        a2y_p = lane_from_next(a2y4.x, zyp ? (R)0 : in.e_a2p);
       }
-      const float r_ym = lane_from_prev(r_c.w, zym ? 0.f : in.e_rm);
-      const float r_yp = lane_from_next(r_c.x, zyp ? 0.f : in.e_rp);
+      const R r_ym = lane_from_prev(r_c.w, zym ? (R)0 : in.e_rm);
+      const R r_yp = lane_from_next(r_c.x, zyp ? (R)0 : in.e_rp);
       const bool edge_m = zym && lane == 0, edge_p = zyp && lane == kWave - 1;
-      float m1y[6], m2y[6], rr[6];   // index e+1 for e = -1..4
+      R m1y[6], m2y[6], rr[6];   // index e+1 for e = -1..4
       rr[0] = r_ym;
       rr[5] = r_yp;
 #pragma unroll
       for (int e = 0; e < 4; ++e) rr[e + 1] = f4(r_c, e);
       if constexpr (EGNO == 3) {
-        const float f1 = fpos<float>(ax_c), f2 = fneg<float>(ax_c);
+        const R f1 = fpos<R>(ax_c), f2 = fneg<R>(ax_c);
 #pragma unroll
         for (int e = 0; e < 6; ++e) {
-          m1y[e] = (rr[e] + 1e-4f) * f1;
-          m2y[e] = (rr[e] + 1e-4f) * f2;
+          m1y[e] = (rr[e] + (R)1e-4) * f1;
+          m2y[e] = (rr[e] + (R)1e-4) * f2;
         }
       } else {
-        m1y[0] = m1f<EGNO>(r_ym, a1y_m, aym);
-        m2y[5] = m2f<EGNO>(r_yp, a2y_p, ayp);
+        m1y[0] = m1f<EGNO, R>(r_ym, a1y_m, aym);
+        m2y[5] = m2f<EGNO, R>(r_yp, a2y_p, ayp);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          m1y[e + 1] = m1f<EGNO>(rr[e + 1], f4(a1y4, e), f4(ay4, e));
-          m2y[e + 1] = m2f<EGNO>(rr[e + 1], f4(a2y4, e), f4(ay4, e));
+          m1y[e + 1] = m1f<EGNO, R>(rr[e + 1], f4(a1y4, e), f4(ay4, e));
+          m2y[e + 1] = m2f<EGNO, R>(rr[e + 1], f4(a2y4, e), f4(ay4, e));
         }
       }
-      if (edge_m) m1y[0] = 0.f;   // zero flux outside a Dirichlet edge
-      if (edge_p) m2y[5] = 0.f;
-      float out[4];
+      if (edge_m) m1y[0] = (R)0;   // zero flux outside a Dirichlet edge
+      if (edge_p) m2y[5] = (R)0;
+      R out[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float r0 = rr[e + 1];
-        float res = (f4(rn4, e) - r0) * p.inv_dt;
+        const R r0 = rr[e + 1];
+        R res = (f4(rn4, e) - r0) * p.inv_dt;
         if (use_eps) {
-          res = res + p.epsl * ((f4(r_p, e) + f4(r_m, e) - 2.f * r0) * p.inv_dx2);
-          res = res + p.epsl * ((rr[e + 2] + rr[e] - 2.f * r0) * p.inv_dy2);
+          res = res + p.epsl * ((f4(r_p, e) + f4(r_m, e) - (R)2 * r0) * p.inv_dx2);
+          res = res + p.epsl * ((rr[e + 2] + rr[e] - (R)2 * r0) * p.inv_dy2);
         }
-        const float m1x_c = m1f<EGNO>(r0, f4(a1_c, e), ax_c);
-        const float m2x_p = zp ? 0.f : m2f<EGNO>(f4(r_p, e), f4(a2_p, e), ax_p);
-        const float div = (m1x_c - m1x_prev[e]) * p.inv_dx + (m2x_p - m2x_cur[e]) * p.inv_dx +
+        const R m1x_c = m1f<EGNO, R>(r0, f4(a1_c, e), ax_c);
+        const R m2x_p = zp ? (R)0 : m2f<EGNO, R>(f4(r_p, e), f4(a2_p, e), ax_p);
+        const R div = (m1x_c - m1x_prev[e]) * p.inv_dx + (m2x_p - m2x_cur[e]) * p.inv_dx +
                           (m1y[e + 1] - m1y[e]) * p.inv_dy + (m2y[e + 2] - m2y[e + 1]) * p.inv_dy;
         out[e] = res - div + cdt;
         m1x_prev[e] = m1x_c;
         m2x_cur[e] = m2x_p;
       }
       // residual row x -> line r/2, real (even r) or imaginary (odd r) part; 4 contiguous elements
-      float* Af = reinterpret_cast<float*>(A + (r >> 1) * Pad<N>::LINE + pix(y)) + (r & 1);
+      R* Af = reinterpret_cast<R*>(A + (r >> 1) * Pad<N>::LINE + pix(y)) + (r & 1);
 #pragma unroll
       for (int e = 0; e < 4; ++e) Af[2 * e] = out[e];
       // slide the window
@@ -253,13 +297,13 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<float> p, const floa
   if (!(p.dbg & 8)) lds_fft_inplace<C, N, NL, NT>(A, twy);
   // Hartley unpack -> blocked layout: chunk (j, b, x0..x0+RW-1, 0..B-1) = RW*B contiguous floats
   const int B = p.B;
-  const int CS4 = RW * B / 4;                 // float4 per chunk
+  const int CS4 = RW * B / 4;                 // V per chunk
   const int lCS4 = p.lB + (RW == 8 ? 1 : RW == 4 ? 0 : RW == 2 ? -1 : -2);   // log2(CS4), B power of two
   const int nb = p.nb;
-  float* wk = p.work + (size_t)j * nb * nx * B;
+  R* wk = p.work + (size_t)j * nb * nx * B;
   for (int t = threadIdx.x; t < nb * CS4; t += NT) {
     const int b = t >> lCS4, part = t & (CS4 - 1);
-    st4(wk + ((size_t)b * nx + x0) * B + part * 4, unpack_chunk4<N, Pad<N>::LINE>(A, b, part, B, p.lB));
+    st4(wk + ((size_t)b * nx + x0) * B + part * 4, unpack_chunk4<N, Pad<N>::LINE, R>(A, b, part, B, p.lB));
   }
 }
 
@@ -403,15 +447,16 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
 
 // G workgroups striding over the T * nx/RW row-group tasks; block NT; LDS RW/2 * (N + N/16) * 8 B.
 // sums: [0] sum (phi'-phi)^2, [1] sum phi^2 (old), [2] sum phi'^2
-template <int N, int RW, int NT, int PF = 1>
-__global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const float2* __restrict__ twy) {
-  using C = float2;
+template <int N, int RW, int NT, int PF = 1, typename R = float>
+__global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<R> p, const cplx<R>* __restrict__ twy) {
+  using C = cplx<R>;
+  using V = V4<R>;
   constexpr int NL = RW / 2;
   constexpr int GPT = (N / 4) / NT;
   if (p.ctrl->done) return;
   extern __shared__ __align__(16) unsigned char smem_raw[];
   C* A = reinterpret_cast<C*>(smem_raw);
-  float* Af = reinterpret_cast<float*>(A);
+  R* Af = reinterpret_cast<R*>(A);
   constexpr bool TWL = N <= 4096;   // twiddle seeds in LDS (see k_res_fwdy_fused_2d)
   C* twl = A + NL * Pad<N>::LINE;
   if constexpr (TWL) fill_twlds<C, N>(twl, twy);
@@ -419,7 +464,7 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
   const int ngx = nx / RW;
   const int ntask = ngx * p.T;
   const size_t plane = (size_t)nx * N;
-  const float scale = p.tau * p.inv_n;
+  const R scale = p.tau * p.inv_n;
   const int CS4 = RW * B / 4;
   const int lB = p.lB;
   const int lCS4 = lB + (RW == 8 ? 1 : RW == 4 ? 0 : RW == 2 ? -1 : -2);   // log2(CS4), B power of two
@@ -433,7 +478,7 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
     const int j = task / ngx;
     const int x0 = (task - j * ngx) * RW;
     if (x0 + RW <= p.xl0 || x0 >= p.xl1) continue;   // x-slab padding / ghost rows only (workgroup-uniform)
-    const float* wk = p.work + (size_t)j * nb * nx * B;
+    const R* wk = p.work + (size_t)j * nb * nx * B;
     // the task's spectrum (RW*B/4 float4 per block, N/B blocks = NLD per thread), in batches of up to 8
     // loads issued together: one memory round trip per batch, not per float4.  The thread index is
     // laundered per task so the 4*BATCH LDS addresses are not hoisted out of the task loop (registers).
@@ -441,7 +486,7 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
     asm volatile("" : "+v"(tl));
 #pragma unroll
     for (int i0 = 0; i0 < NLD; i0 += BATCH) {
-      float4 v[BATCH];
+      V v[BATCH];
 #pragma unroll
       for (int i = 0; i < BATCH; ++i) {
         const int t = tl + (i0 + i) * NT;
@@ -454,8 +499,8 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
         const int b = t >> lCS4, part = t & (CS4 - 1);
         if (B == 2) {   // the float4 holds rows r, r+1 (r = 2 part) at columns 2b, 2b+1: two complex elements
           C* Al = A + part * Pad<N>::LINE;
-          Al[pix(2 * b)] = make_float2(v[i].x, v[i].z);
-          Al[pix(2 * b + 1)] = make_float2(v[i].y, v[i].w);
+          Al[pix(2 * b)] = cmk<C>(v[i].x, v[i].z);
+          Al[pix(2 * b + 1)] = cmk<C>(v[i].y, v[i].w);
         } else {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -466,12 +511,12 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
         }
       }
     }
-    float* phi = p.phi + (size_t)(j + 1) * plane;
-    float* pbar = p.phibar + (size_t)(j + 1) * plane;
+    R* phi = p.phi + (size_t)(j + 1) * plane;
+    R* pbar = p.phibar + (size_t)(j + 1) * plane;
     // old-phi row pairs, one per step s = gi * NL + l; PF steps in flight ahead of the one being updated
     // (step 0 before the transform, steps 1 .. PF-1 right after it, when the FFT's registers are free)
     constexpr int NS = GPT * NL;
-    float4 op[NS][2];
+    V op[NS][2];
     auto ldstep = [&](int s) {
       const size_t idx = (size_t)(x0 + 2 * (s % NL)) * N + 4 * (tid + (s / NL) * NT);
       op[s][0] = ld4(phi + idx);
@@ -491,14 +536,14 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
 #pragma unroll
       for (int l = 0; l < NL; ++l) {   // rows 2l (real part) and 2l+1 (imaginary part) of line l
         const int st = gi * NL + l;
-        const float4 o4[2] = {op[st][0], op[st][1]};
+        const V o4[2] = {op[st][0], op[st][1]};
         if (st + PF < NS) ldstep(st + PF);
         const C* Z = A + l * Pad<N>::LINE;
-        float4 u[2];
+        V u[2];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          float a, b2;
-          hartley_padded<C, float>(Z, N, y + e, a, b2);
+          R a, b2;
+          hartley_padded<C, R>(Z, N, y + e, a, b2);
           f4set(u[0], e, a);
           f4set(u[1], e, b2);
         }
@@ -507,18 +552,18 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<float> p, const f
           const int xr = x0 + 2 * l + h;
           if (xr < p.xl0 || xr >= p.xl1) continue;   // x-slab ghost row (workgroup-uniform)
           const size_t idx = (size_t)xr * N + y;
-          float4 nw, pb;
-          float fs[3] = {0.f, 0.f, 0.f};   // the 4 points in fp32, then one fp64 add per sum
+          V nw, pb;
+          R fs[3] = {(R)0, (R)0, (R)0};   // the 4 points in R (fp32: then one fp64 add per sum)
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const float o = f4(o4[h], e);
-            const float n = o + scale * f4(u[h], e);
+            const R o = f4(o4[h], e);
+            const R n = o + scale * f4(u[h], e);
             f4set(nw, e, n);
-            f4set(pb, e, 2.f * n - o);
-            const float d = n - o;
-            fs[0] = fmaf(d, d, fs[0]);
-            fs[1] = fmaf(o, o, fs[1]);
-            fs[2] = fmaf(n, n, fs[2]);
+            f4set(pb, e, (R)2 * n - o);
+            const R d = n - o;
+            fs[0] = fmar(d, d, fs[0]);
+            fs[1] = fmar(o, o, fs[1]);
+            fs[2] = fmar(n, n, fs[2]);
           }
 #pragma unroll
           for (int i = 0; i < 3; ++i) s[i] += (double)fs[i];

@@ -153,6 +153,8 @@ struct Impl : ImplBase {
   size_t lds_fast_xt = 0;
   int RWf = 8, NTf = 1024, g_fast_upd = 1;
   size_t lds_fast = 0, lds_fast_tw = 0;
+  bool res64 = false;      // fp64 residual and update through the fast row kernels (4-row groups)
+  size_t lds_res64 = 0, lds_upd64 = 0;
   size_t partial_rows = 0;
   static constexpr int kFoldRows = 64;   // rows of the first fold level (k_fold_partials) after the table
   double* fold_out = nullptr;
@@ -374,6 +376,20 @@ struct Impl : ImplBase {
           // + the twiddle-seed table of the persistent kernels (fused residual, update; ny <= 4096)
           lds_fast_tw = lds_fast + (ny <= 4096 ? (size_t)twlds_size(ny) * sizeof(C) : 0);
           g_fast_upd = std::min((nx / RWf) * T, 2048);
+        }
+      }
+      // fp64 residual: the fast row kernel on 4-row groups (2 complex lines of 4096 doubles = 136 KiB of LDS),
+      // rows read once per group over the sliding 3-row window, instead of the generic row-pair kernel's
+      // per-point neighbour re-reads (fp64 C3: 204 GB moved against 80.5 GB algorithmic)
+      if (sizeof(R) == 8 && ply.pow2 && (ny == 2048 || ny == 4096) && nx % 4 == 0 && !xslab) {
+        res64 = true;
+        if (const char* e = getenv("PDHG_RES64")) res64 = atoi(e) != 0;   // tuning override
+        if (res64) {
+          p.tile_j = ((nx / 4) % 4 == 0) ? 8 : 1;
+          lds_res64 = (size_t)2 * (ny + ny / 16) * sizeof(C);
+          // the update through the fast row kernel too: + the twiddle-seed table (152 KiB at ny = 4096)
+          lds_upd64 = lds_res64 + (size_t)twlds_size(ny) * sizeof(C);
+          g_fast_upd = std::min((nx / 4) * T, 2048);
         }
       }
       // fused residual: fp32 fast kernels with 8-row tiles on both sides, rho_alp_iters = 1 (in place),
@@ -714,6 +730,37 @@ struct Impl : ImplBase {
       HIP_TRY(hipGetLastError());
       return PDHG_OK;
     }
+    if constexpr (sizeof(R) == 8) {
+      if (res64) {
+        ProfScope ps(this, "residual");
+        p.row_base = lo;
+        p.row_cnt = hi - lo;
+        auto go = [&](auto Nc) {
+          constexpr int N_ = decltype(Nc)::value, NT_ = 512;   // 1024 threads cap the fp64 rows at 128 VGPRs (spills)
+          const dim3 g((pb.nx / 4) * (hi - lo));
+          int r2;
+          switch (pb.egno) {
+            case 1:
+              if ((r2 = ensure_lds(k_res_fwdy_fast_2d<1, N_, 4, NT_, double>, lds_res64))) return r2;
+              hipLaunchKernelGGL((k_res_fwdy_fast_2d<1, N_, 4, NT_, double>), g, dim3(NT_), lds_res64, stream, p, twy);
+              break;
+            case 2:
+              if ((r2 = ensure_lds(k_res_fwdy_fast_2d<2, N_, 4, NT_, double>, lds_res64))) return r2;
+              hipLaunchKernelGGL((k_res_fwdy_fast_2d<2, N_, 4, NT_, double>), g, dim3(NT_), lds_res64, stream, p, twy);
+              break;
+            default:
+              if ((r2 = ensure_lds(k_res_fwdy_fast_2d<3, N_, 4, NT_, double>, lds_res64))) return r2;
+              hipLaunchKernelGGL((k_res_fwdy_fast_2d<3, N_, 4, NT_, double>), g, dim3(NT_), lds_res64, stream, p, twy);
+              break;
+          }
+          return (int)PDHG_OK;
+        };
+        rc = pb.ny == 4096 ? go(std::integral_constant<int, 4096>{}) : go(std::integral_constant<int, 2048>{});
+        if (rc) return rc;
+        HIP_TRY(hipGetLastError());
+        return PDHG_OK;
+      }
+    }
     if (fast_rows) {
       ProfScope ps(this, "residual");
       p.row_base = lo;
@@ -911,7 +958,25 @@ struct Impl : ImplBase {
         return PDHG_OK;
       }
       int upd_rows = gx4 * g4;
-      if (fast_rows) {
+      bool upd_done = false;
+      if constexpr (sizeof(R) == 8) {
+        if (res64) {
+          ProfScope ps(this, "update");
+          upd_rows = g_fast_upd;
+          auto go = [&](auto kern) {
+            int r3;
+            if ((r3 = ensure_lds(kern, lds_upd64))) return r3;
+            hipLaunchKernelGGL(kern, dim3(g_fast_upd), dim3(512), lds_upd64, stream, p, twy);
+            return (int)PDHG_OK;
+          };
+          rc = pb.ny == 4096 ? go(k_invy_update_fast_2d<4096, 4, 512, 4, double>)
+                             : go(k_invy_update_fast_2d<2048, 4, 512, 4, double>);
+          if (rc) return rc;
+          upd_done = true;
+        }
+      }
+      if (upd_done) {
+      } else if (fast_rows) {
         ProfScope ps(this, "update");
         upd_rows = g_fast_upd;
         rc = with_fast_rows([&](auto Nc, auto RWc, auto NTc) {
@@ -2032,6 +2097,7 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
     if (k == "fused_residual") *value = im.fuse_res ? 1 : 0;
     else if (k == "fast_rows") *value = im.fast_rows ? 1 : 0;
     else if (k == "contig_fail") *value = im.n_contig_fail;
+    else if (k == "res64") *value = im.res64 ? 1 : 0;
     else if (k == "fast_dual") *value = im.fast_dual ? im.dual_rx : -1;
     else if (k == "fast_xt")
       *value = im.fast_xt ? (im.batch_xt && !im.half_real ? (im.xt_dma && im.pb.nx == 4096 ? 4 : 3) : im.ws_xt ? 2 : 1) : 0;

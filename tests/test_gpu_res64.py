@@ -1,0 +1,82 @@
+"""fp64 residual and update through the fast row kernels (k_res_fwdy_fast_2d / k_invy_update_fast_2d <..., double>,
+4-row groups) at the row lengths
+that select it (ny = 2048, 4096; the reference's arithmetic at C2's / C3's ny): the primal update against the fp64
+oracle (update_fns_in_pdhg.py:72-96, 135-147), the generic row-pair kernels (PDHG_RES64=0) on the same state, and
+two full iterations.  Small nx keeps the oracle fast (column blocks of B = 16); one case at nx = 2048 has C3's
+B = 2 blocked layout."""
+import numpy as np
+import pytest
+
+from _problems import device_ctx, make_problem, oracle_fns, rel
+
+pytestmark = pytest.mark.gpu
+
+TAU, SIGMA = 0.1 / 1.5, 0.1 * 1.5
+CASES = [
+    # egno, ndim, nx, ny, T, epsl
+    (1, 2, 8, 2048, 3, 0.0),
+    (2, 2, 8, 4096, 3, 0.1),
+    (2, 2, 12, 2048, 2, 0.0),
+    (3, 2, 8, 2048, 2, 0.1),    # bc (1, 0): Neumann rows in x
+    (2, 2, 2048, 2048, 2, 0.1),  # nx >= 2048: column blocks of B = 2 (C3's layout, the paired-read unpack)
+]
+IDS = ["e{}_{}x{}_T{}_eps{}".format(c[0], c[2], c[3], c[4], c[5]) for c in CASES]
+
+
+def _primal(P):
+    primal, _ = oracle_fns(P)
+    return primal(P["phi"], P["rho"], 70.0, P["alp"], TAU, P["dt"], P["dsp"], P["fns"], P["fv"], P["epsl"],
+                  P["x_arr"], None)
+
+
+@pytest.mark.parametrize("case", CASES, ids=IDS)
+def test_res64_primal_matches_oracle_and_generic(native, case, monkeypatch, parity_log):
+    P = make_problem(*case)
+    ctx = device_ctx(P, "fp64")
+    try:
+        assert ctx.path_info("res64") == 1
+        ctx.set_state(P["phi"], P["rho"], P["alp"])
+        ctx.update_primal(TAU)
+        phi_d = ctx.get_state()[0]
+        pbar_d = ctx.get_phi_bar()
+    finally:
+        ctx.close()
+    monkeypatch.setenv("PDHG_RES64", "0")
+    gen = device_ctx(P, "fp64")
+    try:
+        assert gen.path_info("res64") == 0
+        gen.set_state(P["phi"], P["rho"], P["alp"])
+        gen.update_primal(TAU)
+        phi_g = gen.get_state()[0]
+    finally:
+        gen.close()
+    phi_o = _primal(P)
+    U_o, U_d, U_g = ((x - P["phi"]) / TAU for x in (phi_o, phi_d, phi_g))
+    parity_log("test_res64_primal", "_".join(map(str, case)), {"U_vs_oracle": rel(U_d, U_o), "U_vs_generic": rel(U_d, U_g)},
+               {"U_vs_oracle": 1e-10, "U_vs_generic": 1e-12})
+    assert rel(U_d, U_o) < 1e-10
+    assert rel(U_d, U_g) < 1e-12
+    assert rel(pbar_d, 2 * phi_o - P["phi"]) < 1e-12
+
+
+@pytest.mark.parametrize("case", CASES[:2], ids=IDS[:2])
+def test_res64_iterations_match_oracle(native, case):
+    P = make_problem(*case)
+    primal, dual = oracle_fns(P)
+    phi, rho, alp = P["phi"], P["rho"], P["alp"]
+    for _ in range(2):
+        phi_n = primal(phi, rho, 70.0, alp, TAU, P["dt"], P["dsp"], P["fns"], P["fv"], P["epsl"], P["x_arr"], None)
+        rho, alp = dual(2 * phi_n - phi, rho, 70.0, alp, SIGMA, P["dt"], P["dsp"], P["epsl"], P["fns"], P["x_arr"],
+                        None, 2, -1.0)
+        phi = phi_n
+    ctx = device_ctx(P, "fp64")
+    try:
+        ctx.set_state(P["phi"], P["rho"], P["alp"])
+        ctx.set_stop_rules(converge=False, nan=False)
+        st = ctx.iterate(2, TAU, SIGMA, -1.0, 1)
+        assert st["iters_run"] == 2
+        phi_d, rho_d, alp_d = ctx.get_state()
+    finally:
+        ctx.close()
+    assert rel(phi_d, phi) < 1e-10
+    assert rel(rho_d, rho) < 1e-10
