@@ -148,7 +148,10 @@ int pdhg_device_bytes(pdhg_ctx* ctx, unsigned long long* bytes);
  * RX rows through LDS), "fast_xt" (0 generic, 1 single-role, 2 warp-specialised, 3 row-batched,
  * 4 row-batched with LDS-DMA staging x-transform), "half_real", "fourstep", "fs16", "fs_wide",
  * "glb_line", "thomas_chunk", "rows_rw", "res_threads", "upd_threads",
- * "row_threads" (threads of the generic row kernels). */
+ * "row_threads" (threads of the generic row kernels), "res64" 1/0 (fp64 residual and update through the
+ * 4-row fast kernels, ny = 2048 / 4096), "contig_fail" (large arrays of an fp32 2-D context that fell back
+ * from a physically contiguous allocation to hipMalloc; environment PDHG_ALLOC=contig|none overrides the
+ * contiguous-for-fp32-2-D default). */
 int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value);
 
 /* Per-launch kernel timing for the benchmark: HIP events recorded on the
