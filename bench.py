@@ -529,6 +529,7 @@ def main():
                                    "t-slab x{} (RCCL point-to-point halos and carries, overlapped)".format(world))
                    if (world > 1 or xslab) else "single GPU",
                    "precision": args.precision,
+                   "contig_fail": ctx.path_info("contig_fail") if hasattr(ctx, "path_info") else None,
                    "iters_executed": iters, "stop_status": st["status"], "state_nonfinite": bool(st["nan_seen"]),
                    "dual_subiters_mean": (st.get("inner_total", 0) / max(iters, 1)) if k > 1 else 1,
                    "first_nonfinite_iter": first_nonfinite,
