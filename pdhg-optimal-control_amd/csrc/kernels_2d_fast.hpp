@@ -1129,8 +1129,9 @@ __global__ void __launch_bounds__(512) k_precond_xt_ws_2d(KP<float> p, const flo
 // computed; every load reads a valid address (rows outside a Dirichlet edge are clamped, then
 // zeroed by a select), so nothing drains the load queue.  y neighbours come from the adjacent
 // lanes (DPP), the wave-edge ones from uniform loads.  Sums as in k_dual_2d (double per point).
-template <int EGNO>
-__global__ void __launch_bounds__(256) k_dual_fast_2d(KP<float> p, int jchunk, int jbase, int jend, int zbase) {
+template <int EGNO, typename R = float>
+__global__ void __launch_bounds__(256) k_dual_fast_2d(KP<R> p, int jchunk, int jbase, int jend, int zbase) {
+  using V = V4<R>;
   if (p.ctrl->done || p.ctrl->inner_done) return;
   constexpr int NA = (EGNO == 3) ? 2 : 4;
   constexpr int NS = 3 + 3 * NA;
@@ -1156,24 +1157,24 @@ __global__ void __launch_bounds__(256) k_dual_fast_2d(KP<float> p, int jchunk, i
     const int xm = nb_index(x - 1, nx, p.bcx), xp = nb_index(x + 1, nx, p.bcx);
     const bool zxm = xm < 0, zxp = xp < 0;
     const size_t rxm = (size_t)(zxm ? x : xm) * ny, rxc = (size_t)x * ny, rxp = (size_t)(zxp ? x : xp) * ny;
-    const float4 ay4 = ld4(p.ay + y);
-    const float axc = p.ax[x];
-    const float* rs = p.rho[src_set];
-    float* rd = p.rho[dst_set];
-    const float* as[NA];
-    float* ad[NA];
+    const V ay4 = ld4(p.ay + y);
+    const R axc = p.ax[x];
+    const R* rs = p.rho[src_set];
+    R* rd = p.rho[dst_set];
+    const R* as[NA];
+    R* ad[NA];
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
       as[a] = p.alp[src_set][a];
       ad[a] = p.alp[dst_set][a];
     }
     struct In {
-      float4 pm, pc, pp, rho, al[NA];
-      float el, er;
+      V pm, pc, pp, rho, al[NA];
+      R el, er;
     };
     auto load = [&](int j) {
       In in;
-      const float* f1 = p.phibar + (size_t)(j + 1) * plane;
+      const R* f1 = p.phibar + (size_t)(j + 1) * plane;
       in.pm = ld4(f1 + rxm + y);
       in.pc = ld4(f1 + rxc + y);
       in.pp = ld4(f1 + rxp + y);
@@ -1185,26 +1186,26 @@ __global__ void __launch_bounds__(256) k_dual_fast_2d(KP<float> p, int jchunk, i
       for (int a = 0; a < NA; ++a) in.al[a] = ld4(as[a] + o);
       return in;
     };
-    float4 f0 = ld4(p.phibar + (size_t)j0 * plane + rxc + y);   // phi_bar row j
+    V f0 = ld4(p.phibar + (size_t)j0 * plane + rxc + y);   // phi_bar row j
     In nxt = load(j0);
 #pragma unroll 1
     for (int j = j0; j < j1; ++j) {
       const In in = nxt;
       nxt = load(min(j + 1, j1 - 1));   // (the last step reloads its own row: keeps the loop branch-free)
-      const float4 pm = zxm ? z4() : in.pm, pp = zxp ? z4() : in.pp, pc = in.pc;
-      const float pyl = lane_from_prev(pc.w, zym ? 0.f : in.el);
-      const float pyr = lane_from_next(pc.x, zyp ? 0.f : in.er);
-      float4 rn4, an4[NA];
+      const V pm = zxm ? z4r<R>() : in.pm, pp = zxp ? z4r<R>() : in.pp, pc = in.pc;
+      const R pyl = lane_from_prev(pc.w, zym ? (R)0 : in.el);
+      const R pyr = lane_from_next(pc.x, zyp ? (R)0 : in.er);
+      V rn4, an4[NA];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float c = f4(pc, e);
-        const float lft = e == 0 ? pyl : f4(pc, e - 1);
-        const float rgt = e == 3 ? pyr : f4(pc, e + 1);
-        float ao[4], an[4];
+        const R c = f4(pc, e);
+        const R lft = e == 0 ? pyl : f4(pc, e - 1);
+        const R rgt = e == 3 ? pyr : f4(pc, e + 1);
+        R ao[4], an[4];
 #pragma unroll
         for (int a = 0; a < NA; ++a) ao[a] = f4(in.al[a], e);
-        const float rho = f4(in.rho, e);
-        const float rn = dual_point<float, EGNO>(p, c, f4(pm, e), f4(pp, e), lft, rgt, f4(f0, e), rho, ao, axc,
+        const R rho = f4(in.rho, e);
+        const R rn = dual_point<R, EGNO>(p, c, f4(pm, e), f4(pp, e), lft, rgt, f4(f0, e), rho, ao, axc,
                                                  f4(ay4, e), an);
         f4set(rn4, e, rn);
 #pragma unroll

@@ -97,6 +97,7 @@ constexpr uint32_t kMultiMagic = 0x5044484du;  // "PDHM"
 template <typename R>
 struct Impl : ImplBase {
   using C = cplx<R>;
+  using Real = R;
   pdhg_problem pb{};
   hipStream_t stream = nullptr;
   KP<R> kp{};
@@ -337,15 +338,20 @@ struct Impl : ImplBase {
         lds_fast_xt = ws_xt ? (size_t)(2 * (4096 + 4096 / 16) + 816) * sizeof(C)
                             : (size_t)(4096 + 4096 / 16 + 3 * 4096 + 816) * sizeof(C);
       }
-      if (sizeof(R) == 4 && ny % 256 == 0) {
+      // fp64: the row-per-thread time-marching dual (k_dual_fast_2d<EGNO, double>) instead of the generic
+      // per-point kernel (PDHG_DUAL64=0 keeps the generic one); the LDS-row and fused variants are fp32
+      const bool dual64_ok = sizeof(R) == 8 && ny % 256 == 0 && !xslab;
+      bool dual64 = false;   // opt-in until measured (PDHG_DUAL64=1)
+      if (const char* e = getenv("PDHG_DUAL64")) dual64 = dual64_ok && atoi(e) != 0;
+      if ((sizeof(R) == 4 || dual64) && ny % 256 == 0) {
         fast_dual = true;
         // x rows through LDS (k_dual_lds_2d) for the fused-residual sweep; a context created for
         // rho_alp_iters > 1 (no fused residual) sweeps row-per-thread: measured at C3 with rho_alp_iters = 10,
         // k_dual_fast_2d 25.7 ms per sub-iteration against 38.1 for k_dual_lds_2d (2 waves per SIMD)
-        dual_rx = (nx % 8 == 0 && !short_dual && !two_sets) ? 8 : 0;
+        dual_rx = (sizeof(R) == 4 && nx % 8 == 0 && !short_dual && !two_sets) ? 8 : 0;
         if (const char* e = getenv("PDHG_DUAL_RX")) {   // tuning override: 0 = row-per-thread kernel
           const int v = atoi(e);
-          if (v == 0 || ((v == 4 || v == 8 || v == 16) && nx % v == 0)) dual_rx = v;
+          if (v == 0 || (sizeof(R) == 4 && (v == 4 || v == 8 || v == 16) && nx % v == 0)) dual_rx = v;
         }
         NTd = dual_rx ? dual_rx * 64 : std::min(256, ny / 4);
         gxd = dual_rx ? nx / dual_rx : nx;
@@ -1196,6 +1202,10 @@ struct Impl : ImplBase {
         case 16: hipLaunchKernelGGL((k_dual_lds_2d<EGNO, 16>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase); break;
         default: hipLaunchKernelGGL((k_dual_fast_2d<EGNO>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase);
       }
+    } else {
+      const dim3 g(gxd, gyd, gz);
+      res_valid = false;
+      hipLaunchKernelGGL((k_dual_fast_2d<EGNO, double>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase);
     }
   }
   int launch_dual_fast(const KP<R>& p, int lo = 0, int hi = -1, int zbase = 0) {
@@ -2098,6 +2108,7 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
     else if (k == "fast_rows") *value = im.fast_rows ? 1 : 0;
     else if (k == "contig_fail") *value = im.n_contig_fail;
     else if (k == "res64") *value = im.res64 ? 1 : 0;
+    else if (k == "dual64") *value = (sizeof(typename std::remove_reference<decltype(im)>::type::Real) == 8 && im.fast_dual) ? 1 : 0;
     else if (k == "fast_dual") *value = im.fast_dual ? im.dual_rx : -1;
     else if (k == "fast_xt")
       *value = im.fast_xt ? (im.batch_xt && !im.half_real ? (im.xt_dma && im.pb.nx == 4096 ? 4 : 3) : im.ws_xt ? 2 : 1) : 0;

@@ -80,3 +80,44 @@ def test_res64_iterations_match_oracle(native, case):
         ctx.close()
     assert rel(phi_d, phi) < 1e-10
     assert rel(rho_d, rho) < 1e-10
+
+
+DUAL_CASES = [
+    # egno, ndim, nx, ny, T, epsl
+    (1, 2, 6, 256, 3, 0.0),
+    (2, 2, 5, 512, 3, 0.1),
+    (3, 2, 4, 256, 2, 0.1),
+]
+
+
+@pytest.mark.parametrize("k", [1, 3])
+@pytest.mark.parametrize("case", DUAL_CASES, ids=["e{}_{}x{}_T{}_eps{}".format(c[0], c[2], c[3], c[4], c[5])
+                                                  for c in DUAL_CASES])
+def test_dual64_matches_oracle(native, case, k, monkeypatch):
+    """fp64 dual through the row-per-thread time-marching kernel (k_dual_fast_2d<EGNO, double>, ny % 256 == 0)
+    against the fp64 oracle (update_fns_in_pdhg.py:150-180) and the generic per-point kernel (PDHG_DUAL64=0)."""
+    P = make_problem(*case)
+    rng = np.random.default_rng(11)
+    phi_bar = P["phi"] + 0.05 * rng.standard_normal(P["phi"].shape)
+    _, dual = oracle_fns(P, rho_alp_iters=k)
+    rho_o, alp_o = dual(phi_bar, P["rho"], 70.0, P["alp"], SIGMA, P["dt"], P["dsp"], P["epsl"], P["fns"], P["x_arr"],
+                        None, 2, -1.0)
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("PDHG_DUAL64", flag)
+        ctx = device_ctx(P, "fp64", rho_alp_iters=k)
+        try:
+            assert ctx.path_info("dual64") == int(flag)
+            ctx.set_state(P["phi"], P["rho"], P["alp"])
+            ctx.set_phi_bar(phi_bar)
+            ctx.update_dual(SIGMA, -1.0, k)
+            _, rho_d, alp_d = ctx.get_state()
+        finally:
+            ctx.close()
+        out[flag] = (rho_d, alp_d)
+    rho_d, alp_d = out["1"]
+    assert rel(rho_d, rho_o) < 1e-10
+    for a_d, a_o in zip(alp_d, alp_o):
+        if np.linalg.norm(a_o) > 0:
+            assert rel(a_d, a_o) < 1e-10
+    assert rel(rho_d, out["0"][0]) < 1e-12
