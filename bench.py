@@ -121,7 +121,7 @@ def pmc_traffic(args):
         cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "run", "--",
                sys.executable, os.path.abspath(__file__), "--config", args.config, "--steps", "2", "--warmup", "1",
                "--rho-alp-iters", str(args.rho_alp_iters), "--precision", args.precision, "--no-cpu-baseline",
-               "--no-pmc", "--no-probe"]
+               "--no-pmc", "--no-probe", "--no-reference-precision"]
         try:
             subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=600,
                            env=dict(os.environ, TMPDIR="/tmp"))
@@ -255,6 +255,32 @@ def cpu_marching_baseline(config, k, total_iters, threads, reps=3):
                           reps, k, inner, total_iters)}
 
 
+def reference_precision_run(args):
+    """The same workload in the reference's arithmetic (float64 state and transforms, jaxsrc/update_fns_in_pdhg.py:10),
+    run as a child process BEFORE this process initialises the GPU (its own PMC passes are grandchildren started
+    before it touches the GPU).  Returns the child's JSON line (nested as "reference_precision") or an error note."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--config", args.config, "--steps", str(args.steps),
+           "--warmup", str(args.warmup), "--rho-alp-iters", str(args.rho_alp_iters), "--precision", "fp64",
+           "--no-cpu-baseline", "--no-reference-precision"]
+    if args.no_pmc:
+        cmd.append("--no-pmc")
+    try:
+        r = subprocess.run(cmd, check=True, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, timeout=900,
+                           env=dict(os.environ, TMPDIR="/tmp"))
+    except Exception as e:  # noqa: BLE001
+        return {"error": "fp64 child run failed: {}".format(e)}
+    lines = [ln for ln in r.stdout.decode().splitlines() if ln.startswith("{")]
+    if not lines:
+        return {"error": "fp64 child printed no JSON line"}
+    d = json.loads(lines[-1])
+    d.pop("metric", None)
+    d["parity"] = ("fp64 device path vs the float64 oracle: <= 1e-10 relative L2 on phi / rho / alp "
+                   "(tests/test_gpu_res64.py, tests/test_gpu_configs.py eps 0.1 fp64 cases, "
+                   "tests/test_gpu_divergence.py pointwise)")
+    return d
+
+
 def _free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
@@ -293,6 +319,8 @@ def main():
     ap.add_argument("--cpu-sample-T", type=int, default=1)
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
     ap.add_argument("--no-probe", action="store_true", help="skip the non-finite probe and the finite segment")
+    ap.add_argument("--no-reference-precision", action="store_true",
+                    help="skip the nested fp64 line (run by default next to an fp32 single-GPU line)")
     ap.add_argument("--decomp", default="tslab", choices=["tslab", "xslab"],
                     help="multi-GPU decomposition of the window (xslab also at N = 1: one slab through its phases)")
     ap.add_argument("--marching", action="store_true",
@@ -343,6 +371,9 @@ def main():
     pmc, pmc_err = None, "disabled"
     if world == 1 and not args.no_pmc and args.decomp == "tslab":
         pmc, pmc_err = pmc_traffic(args)   # before this process initialises the GPU
+    ref_prec = None
+    if world == 1 and args.precision == "fp32" and args.decomp == "tslab" and not args.no_reference_precision:
+        ref_prec = reference_precision_run(args)   # likewise before this process initialises the GPU
 
     from pdhg_amd.context import PDHGContext
 
@@ -562,6 +593,8 @@ def main():
         out["pmc_by_kernel"] = pmc.get("_by_kernel")
     elif world == 1:
         out["roofline"]["traffic_note"] = pmc_err
+    if ref_prec is not None:
+        out["reference_precision"] = ref_prec
     if world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
         sample_cfg = CONFIGS[args.config]

@@ -151,7 +151,11 @@ int pdhg_device_bytes(pdhg_ctx* ctx, unsigned long long* bytes);
  * "row_threads" (threads of the generic row kernels), "res64" 1/0 (fp64 residual and update through the
  * 4-row fast kernels, ny = 2048 / 4096), "contig_fail" (large arrays of an fp32 2-D context that fell back
  * from a physically contiguous allocation to hipMalloc; environment PDHG_ALLOC=contig|none overrides the
- * contiguous-for-fp32-2-D default). */
+ * contiguous-for-fp32-2-D default), "dual64" 1/0 (fp64 contexts: the row-per-thread time-marching dual
+ * k_dual_fast_2d<EGNO, double>; default on where ny % 256 == 0, environment PDHG_DUAL64=0 selects the generic
+ * per-point kernel), "f64_xt" 1/0 (fp64 nx = 4096: k_precond_xt_f64_2d), "graph" 1/0 (pdhg_iterate replays
+ * windows of iterations from a captured HIP graph; default on, environment PDHG_GRAPH=0 launches every
+ * iteration eagerly), "graph_window" (iterations per replayed graph). */
 int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value);
 
 /* Per-launch kernel timing for the benchmark: HIP events recorded on the

@@ -49,6 +49,7 @@ struct Ctrl {
   int first_nan;     // iteration (1-based, since the last reset) at which nan_seen was first set; 0: none
   double err1, err2, err_inner;
   double s_dphi, s_phi_old, s_phi_new;   // finalized primal sums
+  double row0_sq;                        // sum phi_0^2 of the fixed row 0 (written by set_state / init_state)
   double dual_sums[kNumSums];            // finalized sums of the last dual sub-iteration
   double outer_sums[kNumSums];           // finalized outer (initial vs final) dual sums
 };

@@ -88,8 +88,10 @@ __device__ __forceinline__ R cont_residual_2d(const KP<R>& p, const R* __restric
 // flat grid over (T x npairs) row-pair tasks; block nt_row (256..1024, by LDS occupancy); LDS 2 * ny complex.
 // The XCD-aware remap puts consecutive row pairs on one XCD at the same time, so the
 // 32/B row pairs that fill one 128-B line of the blocked layout merge in that XCD's L2.
-template <typename R, int EGNO, class F>
-__global__ void __launch_bounds__(1024) k_res_fwdy_2d(KP<R> p, F ply, const cplx<R>* __restrict__ twy) {
+// NTB: launch bound (256 for nt_row = 256, 1024 for the wider launches), so the 256-thread instantiations keep
+// their full register budget
+template <typename R, int EGNO, class F, int NTB>
+__global__ void __launch_bounds__(NTB) k_res_fwdy_2d(KP<R> p, F ply, const cplx<R>* __restrict__ twy) {
   using C = cplx<R>;
   if (p.ctrl->done) return;
   extern __shared__ __align__(16) unsigned char smem_raw[];
@@ -307,8 +309,8 @@ __global__ void __launch_bounds__(512) k_precond_xt_2d(KP<R> p, F plx, const cpl
 // G workgroups striding over the (T x npairs) row-pair tasks (XCD-aware, as k_res_fwdy_2d);
 // block nt_row (as k_res_fwdy_2d); LDS 2 * ny complex.
 // sums: [0] sum (phi'-phi)^2, [1] sum phi^2 (old), [2] sum phi'^2 (NaN detector)
-template <typename R, class F>
-__global__ void __launch_bounds__(1024) k_invy_update_2d(KP<R> p, F ply, const cplx<R>* __restrict__ twy) {
+template <typename R, class F, int NTB>
+__global__ void __launch_bounds__(NTB) k_invy_update_2d(KP<R> p, F ply, const cplx<R>* __restrict__ twy) {
   using C = cplx<R>;
   if (p.ctrl->done) return;
   extern __shared__ __align__(16) unsigned char smem_raw[];

@@ -55,13 +55,15 @@ __global__ void __launch_bounds__(1024) k_fold_partials(const double* __restrict
   if ((int)threadIdx.x < ns) out[(size_t)blockIdx.x * kNumSums + threadIdx.x] = o[threadIdx.x];
 }
 
-// After the primal update: err1 sums (utils_pdhg_solver.py:58).  row0_sq = sum phi_0^2
-// (row 0 never changes: utils_precond.py:139/177).
-__global__ void __launch_bounds__(1024) k_finalize_primal(const double* partials, int nrows, double row0_sq, Ctrl* ctrl) {
+// After the primal update: err1 sums (utils_pdhg_solver.py:58).  ctrl->row0_sq = sum phi_0^2
+// (row 0 never changes: utils_precond.py:139/177).  Read from the control block, not passed by value, so a
+// replayed graph sees the row 0 of the state set after the capture (window marching re-seeds it).
+__global__ void __launch_bounds__(1024) k_finalize_primal(const double* partials, int nrows, int add_row0, Ctrl* ctrl) {
   if (ctrl->done) return;
   __shared__ double out[3];
   reduce_partials(partials, nrows, 3, out);
   if (threadIdx.x == 0) {
+    const double row0_sq = add_row0 ? ctrl->row0_sq : 0.0;   // t-slab sums carry it already (k_reduce_vec)
     ctrl->s_dphi = out[0];
     ctrl->s_phi_old = out[1] + row0_sq;
     ctrl->s_phi_new = out[2] + row0_sq;

@@ -339,9 +339,11 @@ struct Impl : ImplBase {
                             : (size_t)(4096 + 4096 / 16 + 3 * 4096 + 816) * sizeof(C);
       }
       // fp64: the row-per-thread time-marching dual (k_dual_fast_2d<EGNO, double>) instead of the generic
-      // per-point kernel (PDHG_DUAL64=0 keeps the generic one); the LDS-row and fused variants are fp32
+      // per-point kernel, which re-reads every phi_bar neighbour (fp64 C3: 248 GB fetched for 161 GB of reads).
+      // Measured at fp64 C3 (same box, profiles/r04_ab_dual64_*.json): 52.7 vs 59.3 ms per dual, 6.61 vs 6.44
+      // it/s.  PDHG_DUAL64=0 keeps the generic kernel.  The LDS-row and fused variants are fp32.
       const bool dual64_ok = sizeof(R) == 8 && ny % 256 == 0 && !xslab;
-      bool dual64 = false;   // opt-in until measured (PDHG_DUAL64=1)
+      bool dual64 = dual64_ok;
       if (const char* e = getenv("PDHG_DUAL64")) dual64 = dual64_ok && atoi(e) != 0;
       if ((sizeof(R) == 4 || dual64) && ny % 256 == 0) {
         fast_dual = true;
@@ -799,22 +801,26 @@ struct Impl : ImplBase {
       dim3 g(gx1);
       rc = with_line_fft(ply, [&](auto f) {
         using F = decltype(f);
-        int r2;
-        switch (pb.egno) {
-          case 1:
-            if ((r2 = ensure_lds(k_res_fwdy_2d<R, 1, F>, lds_res))) return r2;
-            hipLaunchKernelGGL((k_res_fwdy_2d<R, 1, F>), g, dim3(nt_row), lds_res, stream, p, f, twy);
-            break;
-          case 2:
-            if ((r2 = ensure_lds(k_res_fwdy_2d<R, 2, F>, lds_res))) return r2;
-            hipLaunchKernelGGL((k_res_fwdy_2d<R, 2, F>), g, dim3(nt_row), lds_res, stream, p, f, twy);
-            break;
-          default:
-            if ((r2 = ensure_lds(k_res_fwdy_2d<R, 3, F>, lds_res))) return r2;
-            hipLaunchKernelGGL((k_res_fwdy_2d<R, 3, F>), g, dim3(nt_row), lds_res, stream, p, f, twy);
-            break;
-        }
-        return (int)PDHG_OK;
+        auto go = [&](auto ntb) {
+          constexpr int NTB = decltype(ntb)::value;
+          int r2;
+          switch (pb.egno) {
+            case 1:
+              if ((r2 = ensure_lds(k_res_fwdy_2d<R, 1, F, NTB>, lds_res))) return r2;
+              hipLaunchKernelGGL((k_res_fwdy_2d<R, 1, F, NTB>), g, dim3(nt_row), lds_res, stream, p, f, twy);
+              break;
+            case 2:
+              if ((r2 = ensure_lds(k_res_fwdy_2d<R, 2, F, NTB>, lds_res))) return r2;
+              hipLaunchKernelGGL((k_res_fwdy_2d<R, 2, F, NTB>), g, dim3(nt_row), lds_res, stream, p, f, twy);
+              break;
+            default:
+              if ((r2 = ensure_lds(k_res_fwdy_2d<R, 3, F, NTB>, lds_res))) return r2;
+              hipLaunchKernelGGL((k_res_fwdy_2d<R, 3, F, NTB>), g, dim3(nt_row), lds_res, stream, p, f, twy);
+              break;
+          }
+          return (int)PDHG_OK;
+        };
+        return nt_row <= 256 ? go(std::integral_constant<int, 256>{}) : go(std::integral_constant<int, 1024>{});
       });
     }
     if (rc) return rc;
@@ -1017,9 +1023,14 @@ struct Impl : ImplBase {
         rc = with_line_fft(ply, [&](auto f) {
           using F = decltype(f);
           int r2;
-          if ((r2 = ensure_lds(k_invy_update_2d<R, F>, lds_res))) return r2;
-          hipLaunchKernelGGL((k_invy_update_2d<R, F>), dim3(gx4), dim3(nt_row), lds_res, stream, p, f, twy);
-          return (int)PDHG_OK;
+          auto go = [&](auto kern) {
+            int r3;
+            if ((r3 = ensure_lds(kern, lds_res))) return r3;
+            hipLaunchKernelGGL(kern, dim3(gx4), dim3(nt_row), lds_res, stream, p, f, twy);
+            return (int)PDHG_OK;
+          };
+          (void)r2;
+          return nt_row <= 256 ? go(k_invy_update_2d<R, F, 256>) : go(k_invy_update_2d<R, F, 1024>);
         });
         if (rc) return rc;
       }
@@ -1027,7 +1038,7 @@ struct Impl : ImplBase {
         hipLaunchKernelGGL(k_reduce_vec, dim3(1), dim3(1024), 0, stream, p.partials, upd_rows, 3,
                            kp.j0 == 0 ? row0_sq : 0.0, sums_out);
       else
-        hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, p.partials, upd_rows, row0_sq, p.ctrl);
+        hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, p.partials, upd_rows, 1, p.ctrl);
     } else {
       int rc;
       if constexpr (sizeof(R) == 4) {
@@ -1064,7 +1075,7 @@ struct Impl : ImplBase {
         });
         if (rc) return rc;
       }
-      hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, p.partials, gx4, row0_sq, p.ctrl);
+      hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, p.partials, gx4, 1, p.ctrl);
     }
     HIP_TRY(hipGetLastError());
     return PDHG_OK;
@@ -1103,7 +1114,7 @@ struct Impl : ImplBase {
         if ((rc = ensure_lds(k_fs2_1d<1>, lds2))) return rc;
         hipLaunchKernelGGL((k_fs2_1d<1>), dim3(9, npairs), dim3(kFsNT), lds2, stream, p, tw256, Y);
       }
-      hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, p.partials, 9 * npairs, row0_sq, p.ctrl);
+      hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, p.partials, 9 * npairs, 1, p.ctrl);
       HIP_TRY(hipGetLastError());
     }
     return PDHG_OK;
@@ -1139,7 +1150,7 @@ struct Impl : ImplBase {
         if ((rc = ensure_lds(k_fs2w_1d<1>, lds))) return rc;
         hipLaunchKernelGGL((k_fs2w_1d<1>), dim3(5, npairs), dim3(1024), lds, stream, p, tw256, Y);
       }
-      hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, p.partials, 5 * npairs, row0_sq, p.ctrl);
+      hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, p.partials, 5 * npairs, 1, p.ctrl);
       HIP_TRY(hipGetLastError());
     }
     return PDHG_OK;
@@ -1177,7 +1188,7 @@ struct Impl : ImplBase {
         hipLaunchKernelGGL(k_f16b_inv_1d, dim3(8, npairs), dim3(512), ldsb, stream, p, twx, Y);
         hipLaunchKernelGGL(k_f16a_inv_1d, dim3(kF16N2 / 2 / 256, npairs), dim3(256), 0, stream, p, twx, Y);
       }
-      hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, p.partials, 8 * npairs, row0_sq, p.ctrl);
+      hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, p.partials, 8 * npairs, 1, p.ctrl);
       HIP_TRY(hipGetLastError());
     }
     return PDHG_OK;
@@ -1280,6 +1291,7 @@ struct Impl : ImplBase {
     HIP_TRY(hipMemcpyAsync(&cur, &kp.ctrl->cur, sizeof(int), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     h.cur = cur;
+    h.row0_sq = row0_sq;
     HIP_TRY(hipMemcpyAsync(kp.ctrl, &h, sizeof(Ctrl), hipMemcpyHostToDevice, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     return PDHG_OK;
@@ -1523,7 +1535,7 @@ struct Impl : ImplBase {
   }
   int slab_backward(R tau, double* sums) { return launch_primal(tau, 2 | 4, 2, sums); }
   int slab_primal_finalize(const double* sums) {
-    hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, sums, 1, 0.0, kp.ctrl);
+    hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, sums, 1, 0, kp.ctrl);
     HIP_TRY(hipGetLastError());
     return PDHG_OK;
   }
@@ -1749,6 +1761,7 @@ struct Impl : ImplBase {
     }
     Ctrl h{};
     h.cur = cur;
+    h.row0_sq = row0_sq;
     HIP_TRY(hipMemcpy(kp.ctrl, &h, sizeof(Ctrl), hipMemcpyHostToDevice));
     primal_done = false;
     return PDHG_OK;
@@ -1823,6 +1836,7 @@ struct Impl : ImplBase {
     HIP_TRY(hipStreamSynchronize(stream));
     hipFree(d_row);
     Ctrl h{};
+    h.row0_sq = row0_sq;
     HIP_TRY(hipMemcpy(kp.ctrl, &h, sizeof(Ctrl), hipMemcpyHostToDevice));
     (void)rc;
     primal_done = false;

@@ -87,6 +87,30 @@ def get_f_vals_2d(f_fn, alp, x_arr, t_arr):               # update_fns_in_pdhg.p
     return tuple(out)
 
 
+# ---- the preconditioner's symbol ----
+_FV_OK = [None]
+
+
+def check_fv(fv, ndim, space, dspatial, bc):
+    """The device kernels use the analytic Laplacian symbol of the reference's stencil (utils_precond.py:42-71;
+    pdhg_amd.utils_precond.compute_Dxx_fft_fv).  A caller's fv that is not that symbol (up to the FFT's roundoff)
+    would be silently replaced, where the reference would use it (update_fns_in_pdhg.py:139, 146): refuse it with
+    PDHGUnsupported (NotImplementedError).  fv = None selects the analytic symbol."""
+    if fv is None or _FV_OK[0] is fv:
+        return
+    from ._native import PDHGUnsupported
+    from .utils_precond import compute_Dxx_fft_fv
+    ref = compute_Dxx_fft_fv(ndim, tuple(space), tuple(dspatial), bc if ndim == 2 else 0)
+    f = np.asarray(fv)
+    if f.shape != ref.shape:
+        f = np.broadcast_to(f, ref.shape) if f.size == 1 else f
+    if f.shape != ref.shape or not np.all(np.abs(f - ref) <= 1e-9 * np.max(np.abs(ref)) + 1e-9):
+        raise PDHGUnsupported(-2, "fv differs from the Laplacian symbol of the reference stencil "
+                                  "(compute_Dxx_fft_fv, utils_precond.py:42-71); the device preconditioner "
+                                  "implements that symbol only")
+    _FV_OK[0] = fv
+
+
 # ---- primal ----
 def _primal(phi_prev, rho_prev, c_on_rho, alp_prev, tau, dt, dspatial, fns_dict, epsl, x_arr, bc, C, pow, Ct):
     spec = _spec(fns_dict)
@@ -100,13 +124,16 @@ def _primal(phi_prev, rho_prev, c_on_rho, alp_prev, tau, dt, dspatial, fns_dict,
 
 def update_primal_1d(phi_prev, rho_prev, c_on_rho, alp_prev, tau, dt, dspatial, fns_dict, fv, epsl, x_arr, t_arr, bc,
                      C=1.0, pow=1, Ct=1):
-    """phi + tau * H1^{-1} cont_residual (update_fns_in_pdhg.py:135-140); fv is recomputed analytically."""
+    """phi + tau * H1^{-1} cont_residual (update_fns_in_pdhg.py:135-140); fv must be the stencil's symbol
+    (check_fv), which the kernels form analytically."""
+    check_fv(fv, 1, np.shape(phi_prev)[1:], dspatial, bc)
     return _primal(phi_prev, rho_prev, c_on_rho, alp_prev, tau, dt, dspatial, fns_dict, epsl, x_arr, bc, C, pow, Ct)
 
 
 def update_primal_2d(phi_prev, rho_prev, c_on_rho, alp_prev, tau, dt, dspatial, fns_dict, fv, epsl, x_arr, t_arr, bc,
                      C=1.0, pow=1, Ct=1):
-    """update_fns_in_pdhg.py:142-147 (pow and Ct are ignored in 2-D, as in the reference)."""
+    """update_fns_in_pdhg.py:142-147 (pow and Ct are ignored in 2-D, as in the reference); fv as update_primal_1d."""
+    check_fv(fv, 2, np.shape(phi_prev)[1:], dspatial, bc)
     return _primal(phi_prev, rho_prev, c_on_rho, alp_prev, tau, dt, dspatial, fns_dict, epsl, x_arr, bc, C, 1.0, 1.0)
 
 

@@ -100,6 +100,7 @@ def PDHG_solver_oneiter(fn_update_primal, fn_update_dual, fns_dict, phi0, rho0, 
     """Outer PDHG loop (utils_pdhg_solver.py:9-94).  Returns (results_all, error_all)."""
     tag = _native_tag(fn_update_primal, fn_update_dual)
     if tag is not None:
+        U.check_fv(fv, ndim, np.shape(phi0)[1:], dspatial, tag["bc"])
         return _device_oneiter(tag, fns_dict, phi0, rho0, alp0, x_arr, ndim, dt, dspatial, c_on_rho, epsl,
                                stepsz_param, N_maxiter, print_freq, eps, verbose, stats)
     # generic callables: the reference's host loop, one device call per update
@@ -156,29 +157,43 @@ def PDHG_multi_step(fn_update_primal, fn_update_dual, fns_dict, g, x_arr, ndim, 
     phi_all, rho_all, alp_all, errs_all = [], [], [], []
     init_t = 0
     phi_end = None
+    # back-off schedule from the CALLER's step size (utils_pdhg_solver.py:160-161), fixed before a middle file
+    # restores a reduced one, so a resumed run steps down exactly as the uninterrupted run does
+    s_delta = stepsz_param / 10
+    s_min = stepsz_param / 10
     if load_middle_dir is not None and load_middle_prefix is not None:
         # middle results: [max_iters, phi_all, rho_all, alp_all, errs_all, phi0_next, stepsz_param]; phi_all keeps
         # phi_c[:-1] for every window but the last (utils_pdhg_solver.py:192-195), so the warm start the next
         # window begins from (phi0 + (phi_c[-1:] - phi0[0:1]), :201-203) is saved whole (phi0_next) and restored
-        # bit for bit.  The reference restarts from phi_all[-1:] (:146-150), which is the previous window's
-        # start, not its end.  Files of round 2 hold only the end row there (shape [1, ...]): it is repeated.
+        # bit for bit, with the step size the run had reached (after any back-off).  Files of round 2 hold only
+        # the end row there (shape [1, ...]): it is repeated.
+        # The reference's own 5-entry list (:211-212) holds no end row; it restarts from phi_all[-1:] (:145-147),
+        # the last saved window's entries.  Here that window is solved again: every window's phi0 repeats one row
+        # (:123, and the warm start adds the same row to every row, :201-203), and that row is phi_all[-1][0]
+        # (row 0 never changes, utils_precond.py:139/177), so its start state is known exactly -- rho / alp from
+        # the window before it (or the initial ones) -- and the run continues as the uninterrupted one.
         middle = load_middle_solution(load_middle_dir, load_middle_prefix)
-        max_iters, phi_all, rho_all, alp_all, errs_all = middle[:5]
+        max_iters, phi_all, rho_all, alp_all, errs_all = [middle[0]] + [list(m) for m in middle[1:5]]
         init_t = len(phi_all)
         assert init_t == len(rho_all) == len(alp_all) == len(errs_all)
         if 0 < init_t < nt_PDHG:
-            if len(middle) < 7:
-                raise ValueError("middle results {}/{} hold no end row of window {} (saved without phi_end); "
-                                 "cannot resume".format(load_middle_dir, load_middle_prefix, init_t - 1))
-            phi_end, stepsz_param = np.asarray(middle[5], dtype=np.float64), float(middle[6])
-            if phi_end.shape == phi0.shape:
-                phi0 = phi_end.copy()
+            if len(middle) >= 7:
+                phi_end, stepsz_param = np.asarray(middle[5], dtype=np.float64), float(middle[6])
+                if phi_end.shape == phi0.shape:
+                    phi0 = phi_end.copy()
+                else:
+                    phi0 = np.repeat(phi_end.reshape((1,) + phi0.shape[1:]), time_step_per_PDHG, axis=0)
+                rho0 = rho_all[-1]
+                alp0 = tuple(alp_all[-1][i] for i in range(n_alp))
             else:
-                phi0 = np.repeat(phi_end.reshape((1,) + phi0.shape[1:]), time_step_per_PDHG, axis=0)
-            rho0 = rho_all[-1]
-            alp0 = tuple(alp_all[-1][i] for i in range(n_alp))
-    s_delta = stepsz_param / 10
-    s_min = stepsz_param / 10
+                row = np.asarray(phi_all[-1], dtype=np.float64)[0:1]
+                phi0 = np.repeat(row, time_step_per_PDHG, axis=0)
+                for lst in (phi_all, rho_all, alp_all, errs_all):
+                    lst.pop()
+                init_t -= 1
+                if init_t > 0:
+                    rho0 = rho_all[-1]
+                    alp0 = tuple(alp_all[-1][i] for i in range(n_alp))
     sol_nan = False
     for i in range(init_t, nt_PDHG):
         t_arr = np.linspace(i * dt * T, (i + 1) * dt * T, num=time_step_per_PDHG)[1:]

@@ -8,7 +8,7 @@ IFS=: read -ra DS <<< "$DIRS"
 for d in "${DS[@]}"; do
   cd "$REPO/$d" || exit 1
   echo "== $d"
-  timeout -k 10 300 python bench.py --no-pmc --no-cpu-baseline --no-probe "$@" 2>/dev/null | python -c "
+  timeout -k 10 300 python bench.py --no-pmc --no-cpu-baseline --no-probe --no-reference-precision "$@" 2>/dev/null | python -c "
 import json,sys
 d=json.loads(sys.stdin.read().strip().splitlines()[-1])
 print('it/s %.3f ms %.2f' % (d['value'], d['ms_per_step']), {k: round(v['avg_ms'],2) for k,v in d['kernels'].items()})" || exit 1

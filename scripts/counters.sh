@@ -8,7 +8,7 @@ REPO=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$REPO/gpurun_out/cnt_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-ARGS="$REPO/bench.py --config $CFG --steps 2 --warmup 1 --no-cpu-baseline --no-pmc --no-probe"
+ARGS="$REPO/bench.py --config $CFG --steps 2 --warmup 1 --no-cpu-baseline --no-pmc --no-probe --no-reference-precision"
 timeout -s KILL 60 rocprofv3 -L > "$OUT/counters_available.txt" 2>&1 || true
 i=0
 for C in "$@"; do

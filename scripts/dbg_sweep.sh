@@ -9,6 +9,6 @@ CFG=$1; shift
 REPO=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$REPO"
 for D in "$@"; do
-  PDHG_DBG=$D timeout -k 10 300 python bench.py --config "$CFG" --steps 6 --warmup 2 --no-pmc --no-cpu-baseline --no-probe \
+  PDHG_DBG=$D timeout -k 10 300 python bench.py --config "$CFG" --steps 6 --warmup 2 --no-pmc --no-cpu-baseline --no-probe --no-reference-precision \
     2>/dev/null | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'dbg': $D, 'ms_per_step': round(d['ms_per_step'],2), 'kernels': {k: round(v['avg_ms'],3) for k, v in d['kernels'].items()}}))" || exit 1
 done

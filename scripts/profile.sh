@@ -8,7 +8,7 @@ OUT=$REPO/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 # the bench's own step counts (10 timed after 3 warm-up), so the trace's per-kernel averages are those of its line
-ARGS="$REPO/bench.py --config $CFG --steps 10 --warmup 3 --no-cpu-baseline --no-pmc --no-probe $EXTRA"
+ARGS="$REPO/bench.py --config $CFG --steps 10 --warmup 3 --no-cpu-baseline --no-pmc --no-probe --no-reference-precision $EXTRA"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $ARGS > "$OUT/trace.log" 2>&1 || exit 1
 for C in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
   N=$(echo $C | tr ' ' '_')

@@ -476,14 +476,24 @@ def test_graph_replay_matches_eager(native, monkeypatch, case):
             assert ctx.path_info("graph") == int(g)
             if g == "1":
                 assert ctx.path_info("graph_window") == 8
-            out.append((a, b, ctx.get_state()))
+            s_b = ctx.get_state()
+            # window marching re-seeds the same context (PDHG_multi_step's warm start, a new phi row 0) and
+            # iterates with unchanged (tau, sigma, eps, k): the replayed graph must use the new row 0 in err1
+            phi2 = P["phi"] * 1.7 + 0.3
+            ctx.set_state(phi2, P["rho"], P["alp"])
+            c1 = ctx.iterate(1, TAU, SIGMA, -1.0, 1)
+            c = ctx.iterate(16, TAU, SIGMA, -1.0, 1)
+            out.append((a, b, s_b, c1, c, ctx.get_state()))
         finally:
             ctx.close()
-    (a0, b0, s0), (a1, b1, s1) = out
+    (a0, b0, s0, c10, c0, t0), (a1, b1, s1, c11, c1, t1) = out
     assert a0["iters_run"] == a1["iters_run"] == 37
     assert b0["iters_run"] == b1["iters_run"] and b0["status"] == b1["status"], (b0, b1)
     assert b0["err1"] == b1["err1"] and b0["err2"] == b1["err2"]
     assert np.array_equal(s0[0], s1[0]) and np.array_equal(s0[1], s1[1])
+    assert c10["err1"] == c11["err1"] and c0["iters_run"] == c1["iters_run"] == 16
+    assert c0["err1"] == c1["err1"] and c0["err2"] == c1["err2"], (c0, c1)
+    assert np.array_equal(t0[0], t1[0]) and np.array_equal(t0[1], t1[1])
 
 
 @pytest.mark.parametrize("case", [(2, 2, 4096, 16, 6, 0.0), (1, 2, 4096, 32, 3, 0.0), (2, 2, 4096, 8, 1, 0.0)],

@@ -140,17 +140,73 @@ def test_resume_from_middle_matches_straight_run(tmp_path, monkeypatch):
     assert len(errs_r) == len(errs_s)
 
 
-def test_resume_without_end_row_raises(tmp_path):
-    """Middle results in the reference's 5-entry form hold no end row: resuming mid-run is refused."""
+def test_resume_from_reference_middle_list(tmp_path, monkeypatch):
+    """The reference's own middle file is the 5-entry list [max_iters, phi_all, rho_all, alp_all, errs_all]
+    (utils_pdhg_solver.py:211-212) with no end row; resuming from it (:139-147) solves the last saved window
+    again from its known start state and then matches the uninterrupted run."""
+    nx, nt = 12, 5
+    x, fns, g, fv = _setup(nx, nt)
+    primal, dual = O.make_update_fns(1, 0, rho_alp_iters=10)
+    kw = dict(time_step_per_PDHG=2, stepsz_param=0.1, n_ctrl=1, fv=fv, N_maxiter=3000, print_freq=400, eps=1e-6,
+              verbose=False)
+    real_save = S.save
+
+    def save_and_snapshot(d, prefix, results):
+        real_save(d, prefix, results)
+        if len(results[1]) == 2:
+            real_save(d, "ref5", list(results[:5]))        # the reference's layout
+    monkeypatch.setattr(S, "save", save_and_snapshot)
+    res_s, errs_s = S.PDHG_multi_step(primal, dual, fns, g, x, 1, nt, (nx,), 0.25, (2.0 / nx,), 70.0,
+                                      save_middle_dir=str(tmp_path), save_middle_prefix="mid", **kw)
+    assert len(solver.load_middle_solution(str(tmp_path), "ref5")) == 5
+    res_r, errs_r = S.PDHG_multi_step(primal, dual, fns, g, x, 1, nt, (nx,), 0.25, (2.0 / nx,), 70.0,
+                                      load_middle_dir=str(tmp_path), load_middle_prefix="ref5", **kw)
+    assert res_r[0][0] == res_s[0][0]
+    for a, b in zip(res_r[0][1:], res_s[0][1:]):
+        assert a.shape == b.shape and np.array_equal(a, b)
+    assert len(errs_r) == len(errs_s)
+    for a, b in zip(errs_r, errs_s):
+        assert np.array_equal(a, b)
+
+
+def test_resume_after_backoff_keeps_the_schedule(tmp_path, monkeypatch):
+    """A run that backed off its step size before the middle file was written steps down on the SAME schedule
+    after a resume: s_delta / s_min come from the caller's step size (utils_pdhg_solver.py:160-161), not from
+    the reduced one the file restores.  Window 0 blows up above 0.095 (0.1 -> 0.09), window 2 above 0.075
+    (0.09 -> 0.08 -> 0.07); resuming after window 1 with a schedule derived from 0.09 would try 0.081, 0.072."""
     nx, nt = 8, 5
     x, fns, g, fv = _setup(nx, nt)
     primal, dual = O.make_update_fns(1, 0, rho_alp_iters=1)
-    phi = np.zeros((1, nx))
-    solver.save(str(tmp_path), "old", [3, [phi], [np.zeros((1, nx))], [np.zeros((2, 1, nx, 1))], [np.zeros((1, 2))]])
-    with pytest.raises(ValueError, match="end row"):
-        S.PDHG_multi_step(primal, dual, fns, g, x, 1, nt, (nx,), 0.25, (2.0 / nx,), 70.0, time_step_per_PDHG=2,
-                          stepsz_param=0.1, n_ctrl=1, fv=fv, N_maxiter=10, print_freq=5, eps=1e-6, verbose=False,
-                          load_middle_dir=str(tmp_path), load_middle_prefix="old")
+    tried = {"s": [], "r": []}
+
+    def mk(key):
+        def p2(phi, rho, c, alp, tau, dt, ds, f, fv_, epsl, xa, t):
+            step = round(tau * 1.5, 12)
+            w = int(round(float(np.asarray(t).ravel()[0]) / dt)) - 1       # window index (T = 1 rows)
+            if not tried[key] or tried[key][-1] != (w, step):
+                tried[key].append((w, step))
+            out = primal(phi, rho, c, alp, tau, dt, ds, f, fv_, epsl, xa, t)
+            thr = {0: 0.095, 2: 0.075}.get(w, 1.0)
+            return out * np.nan if step > thr else out
+        return p2
+    kw = dict(time_step_per_PDHG=2, stepsz_param=0.1, n_ctrl=1, fv=fv, N_maxiter=40, print_freq=10, eps=1e-6,
+              verbose=False)
+    real_save = S.save
+
+    def save_and_snapshot(d, prefix, results):
+        real_save(d, prefix, results)
+        if len(results[1]) == 2:
+            real_save(d, "after2", results)
+    monkeypatch.setattr(S, "save", save_and_snapshot)
+    res_s, errs_s = S.PDHG_multi_step(mk("s"), dual, fns, g, x, 1, nt, (nx,), 0.25, (2.0 / nx,), 70.0,
+                                      save_middle_dir=str(tmp_path), save_middle_prefix="mid", **kw)
+    assert [s for w, s in tried["s"] if w == 2] == [0.09, 0.08, 0.07]
+    res_r, errs_r = S.PDHG_multi_step(mk("r"), dual, fns, g, x, 1, nt, (nx,), 0.25, (2.0 / nx,), 70.0,
+                                      load_middle_dir=str(tmp_path), load_middle_prefix="after2", **kw)
+    assert [e for e in tried["r"] if e[0] >= 2] == [e for e in tried["s"] if e[0] >= 2]
+    assert res_r[0][0] == res_s[0][0]
+    for a, b in zip(res_r[0][1:], res_s[0][1:]):
+        assert a.shape == b.shape and np.array_equal(a, b)
 
 
 def test_dropin_default_precision_is_fp64():
@@ -159,3 +215,26 @@ def test_dropin_default_precision_is_fp64():
     assert U.get_precision() == "fp64"
     fp, fd = S.make_update_fns(1, 0)
     assert fp._pdhg_native["precision"] is None   # resolved to the module default when the context is made
+
+
+@pytest.mark.parametrize("ndim,bc", [(1, 0), (2, (0, 0)), (2, (1, 0))])
+def test_dropin_refuses_a_foreign_fv(ndim, bc):
+    """The drop-ins' preconditioner is the reference stencil's symbol (utils_precond.py:42-71): the oracle's fv
+    (the reference's FFT of the stencil) is accepted, any other fv raises NotImplementedError before any device
+    work instead of being silently replaced (update_fns_in_pdhg.py:139, 146 would use it)."""
+    from pdhg_amd import update_fns_in_pdhg as U
+    space, dsp = ((16,), (0.125,)) if ndim == 1 else ((8, 6), (0.25, 1 / 3))
+    fv = O.compute_Dxx_fft_fv(ndim, space, dsp, bc)
+    U.check_fv(fv, ndim, space, dsp, bc)
+    U.check_fv(None, ndim, space, dsp, bc)
+    with pytest.raises(NotImplementedError, match="symbol"):
+        U.check_fv(fv * 1.01, ndim, space, dsp, bc)
+    T = 2
+    phi = np.zeros((T + 1,) + space)
+    rho = np.full((T,) + space, 70.0)
+    alp = tuple(np.zeros((T,) + space + (ndim,)) for _ in range(2 if ndim == 1 else 4))
+    fns = set_fns.set_up_example_fns(1, ndim, 0)
+    upd = U.update_primal_1d if ndim == 1 else U.update_primal_2d
+    with pytest.raises(NotImplementedError, match="symbol"):
+        upd(phi, rho, 70.0, alp, 0.1, 0.5, dsp, fns, fv + 3.0, 0.0, O.make_grid(ndim, *(space + (1,))[:2], 1), None,
+            bc)
