@@ -339,6 +339,25 @@ __device__ __forceinline__ void inplace_pass(C* __restrict__ a, const C* __restr
 #pragma unroll
       for (int r = 0; r < R; ++r) v[q][r] = s[r * (nR + nR / 16)];
       if (LS > 1 && k != 0) {
+        if constexpr (REG && R == 16 && sizeof(C) == 16) {
+          // fp64: W^r = (W^4k)^(r>>2 part) (W^k)^(r&3) applied row by row of the 4 x 4 split, so at most the three
+          // low powers and one high factor are live (the full w[16] table is 60 VGPRs next to 64 of values)
+          const C* t3 = twl + twlds_off(LS) + 3 * k;
+          const C w1 = t3[0], w2 = cmul(w1, w1), w3 = cmul(w2, w1);
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            C H;
+            if (h == 1) H = t3[1];
+            else if (h == 2) H = t3[2];
+            else if (h == 3) H = cmul(t3[1], t3[2]);
+            if (h > 0) v[q][4 * h] = cmul(v[q][4 * h], H);
+            v[q][4 * h + 1] = cmul(v[q][4 * h + 1], h > 0 ? cmul(H, w1) : w1);
+            v[q][4 * h + 2] = cmul(v[q][4 * h + 2], h > 0 ? cmul(H, w2) : w2);
+            v[q][4 * h + 3] = cmul(v[q][4 * h + 3], h > 0 ? cmul(H, w3) : w3);
+          }
+          base[q] = l * LINE + pix((j - k) * R + k);
+          continue;
+        }
         C w[R];
         if constexpr (REG) {
           const C* t3 = twl + twlds_off(LS) + 3 * k;

@@ -274,11 +274,13 @@ struct Impl : ImplBase {
       while (nyp < ny) nyp <<= 1;
       if (B > nyp) B = nyp;
       // fp32 nx = 8192 (C4): one real column per block, packed into a 4096-point FFT (half_real)
-      half_real = sizeof(R) == 4 && nxg == 8192 && pb.bc_x == 0;
+      // fp64 nx = 8192 (C4's grid in the reference's precision): the same half-real split in k_precond_xt_f64_2d<HR>
+      half_real = nxg == 8192 && pb.bc_x == 0 && (sizeof(R) == 4 || (!xslab && !slab));
       if (half_real) B = 1;
       // fp64 nx = 4096 (C3's grid in the reference's precision): k_precond_xt_f64_2d keeps the carries in
       // registers, so the column pair (B = 2) fits LDS although 5 M reals would not
-      f64_xt = sizeof(R) == 8 && nxg == 4096 && pb.bc_x == 0 && !xslab && !slab && B == 2;
+      f64_xt = sizeof(R) == 8 && pb.bc_x == 0 && !xslab && !slab &&
+               ((nxg == 4096 && B == 2) || (nxg == 8192 && half_real));
       if (!half_real && !f64_xt && (size_t)nxg * B > cap)
         return fail(PDHG_ERR_UNSUPPORTED, "nx=%d too large for the x-transform slab (max %zu in this precision)", nxg,
                     cap / 2);
@@ -315,7 +317,7 @@ struct Impl : ImplBase {
       if (const char* e = getenv("PDHG_SHORT_T_XT")) short_t_xt = atoi(e);   // tuning overrides (0: never)
       if (const char* e = getenv("PDHG_SHORT_T")) short_t_dual = atoi(e);
       const bool short_win = T < short_t_xt, short_dual = T < short_t_dual;
-      if (half_real) {
+      if (half_real && sizeof(R) == 4) {
         fast_xt = true;
         ws_xt = true;
         lds_fast_xt = (size_t)(2 * (4096 + 4096 / 16) + 816 + 4096) * sizeof(C);   // + split twiddles
@@ -873,6 +875,13 @@ struct Impl : ImplBase {
         ProfScope ps(this, "precond");
         if (p.xt_phase != 0 || p.b0 != 0 || nblk != p.nb)
           return fail(PDHG_ERR_UNSUPPORTED, "the fp64 nx = 4096 x transform runs whole windows only");
+        if (half_real) {   // nx = 8192: one real column per block + the split-twiddle tables
+          const size_t lds = (size_t)(Pad<4096>::LINE + TwLds<4096>::SIZE + 4096 + 128) * sizeof(C);
+          if ((rc = ensure_lds(k_precond_xt_f64_2d<4096, 512, true>, lds))) return rc;
+          hipLaunchKernelGGL((k_precond_xt_f64_2d<4096, 512, true>), dim3(nblk), dim3(512), lds, stream, p, twx);
+          HIP_TRY(hipGetLastError());
+          return PDHG_OK;
+        }
         const size_t lds = (size_t)(Pad<4096>::LINE + TwLds<4096>::SIZE + 4096) * sizeof(C);
         if ((rc = ensure_lds(k_precond_xt_f64_2d<4096, 512>, lds))) return rc;
         hipLaunchKernelGGL((k_precond_xt_f64_2d<4096, 512>), dim3(nblk), dim3(512), lds, stream, p, twx);

@@ -32,7 +32,7 @@ for step in "$@"; do
     info)  { timeout -k 5 60 rocm-smi --showproductname --showclocks --showpower --showtemp --showperflevel; hostname; } > "$OUT/info_$n.log" 2>&1
            grep -E "sclk|mclk|Power|Perf|Card SKU" "$OUT/info_$n.log" | head -12 || true ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { echo "smoke failed rc=$?"; tail -20 "$OUT/smoke.log"; exit 1; } ;;
-    tests) if [ -n "$arg" ]; then K=(-k "$arg"); else K=(); fi
+    tests) arg=${arg//+/ }; if [ -n "$arg" ]; then K=(-k "$arg"); else K=(); fi
            timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v -s --timeout 300 --timeout-method thread "${K[@]}" > "$OUT/tests_$n.log" 2>&1 || { echo "tests failed rc=$?"; tail -30 "$OUT/tests_$n.log"; exit 1; }
            tail -3 "$OUT/tests_$n.log" ;;
     bench) env "${ENVV[@]}" timeout -k 10 900 python -u bench.py $arg > "$OUT/bench_$n.json" 2> "$OUT/bench_$n.err" || { echo "bench failed rc=$?"; tail -20 "$OUT/bench_$n.err"; exit 1; }

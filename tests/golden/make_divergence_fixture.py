@@ -26,6 +26,12 @@ modes, which then grow ~3000-fold per iteration, so the float32 trajectory leave
 iterations and reaches a NaN long before float64 does.
 
 Run:  python tests/golden/make_divergence_fixture.py [T] [max_iters] [f32]   (~2.5 min per iteration at T = 4, 6 cores)
+
+Pointwise variant (argument "points"): the float64 oracle's phi' and rho' at NPTS fixed sample points of the plane
+(rows 1..T of phi', every row of rho'; indices from np.random.default_rng(20250117)) after each of the first
+max_iters iterations -> divergence_c3_plane_T{T}_points.npz.  tests/test_gpu_divergence.py compares the fp64
+device's values at the same points pointwise (relative L2 over the sample, per iteration), so the check covers
+the state itself, not only its norms.
 """
 import os
 import sys
@@ -58,8 +64,20 @@ def setup(nx, ny, T, dt, epsl, dtype=np.float64):
                 dt=dt, epsl=epsl)
 
 
+NPTS = 4096
+
+
+def sample_points(T, nx, ny, n=NPTS):
+    """Fixed sample of the plane: (t, x, y) for phi rows 1..T and for rho rows 0..T-1."""
+    rng = np.random.default_rng(20250117)
+    pt = rng.integers(1, T + 1, n), rng.integers(0, nx, n), rng.integers(0, ny, n)
+    rt = rng.integers(0, T, n), rng.integers(0, nx, n), rng.integers(0, ny, n)
+    return np.stack(pt), np.stack(rt)
+
+
 def run(S, max_iters, log=True):
     phi, rho, alp = S["phi"], S["rho"], S["alp"]
+    pts = S.get("points")
     rows = []
     first = 0
     t0 = time.time()
@@ -79,6 +97,9 @@ def run(S, max_iters, log=True):
             mphi = float(np.nanmax(np.abs(phi_n)))
             mrho = float(np.nanmax(np.abs(rho_n)))
         rows.append([it, nphi, nrho, nalp, e1, e2, 1.0 if fin else 0.0, mphi, mrho])
+        if pts is not None:
+            S["phi_pts"].append(phi_n[tuple(pts[0])].astype(np.float64))
+            S["rho_pts"].append(rho_n[tuple(pts[1])].astype(np.float64))
         if S.get("out"):
             save(S["out"], np.array(rows), 0, S)
         if log:
@@ -94,6 +115,11 @@ def run(S, max_iters, log=True):
 def save(out, rows, first, S):
     T = S["phi"].shape[0] - 1
     nx, ny = S["phi"].shape[1:]
+    if S.get("points") is not None:
+        np.savez_compressed(out, rows=rows, meta=np.array([2, 2, nx, ny, T]), dt=S["dt"], epsl=S["epsl"], tau=TAU,
+                            sigma=SIGMA, phi_idx=S["points"][0], rho_idx=S["points"][1],
+                            phi_pts=np.array(S["phi_pts"]), rho_pts=np.array(S["rho_pts"]))
+        return
     np.savez_compressed(out, rows=rows, first_nonfinite=first, meta=np.array([2, 2, nx, ny, T]), dt=S["dt"],
                         epsl=S["epsl"], tau=TAU, sigma=SIGMA,
                         columns=np.array(["iter", "phi_norm", "rho_norm", "alp_norm", "err1", "err2", "finite",
@@ -104,9 +130,12 @@ if __name__ == "__main__":
     T = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     max_iters = int(sys.argv[2]) if len(sys.argv) > 2 else 24
     f32 = len(sys.argv) > 3 and sys.argv[3] == "f32"   # the float32 oracle (until its first NaN)
+    points = len(sys.argv) > 3 and sys.argv[3] == "points"
     nx = ny = 4096
     S = setup(nx, ny, T, 1.0 / 200, 0.1, np.float32 if f32 else np.float64)
-    out = os.path.join(HERE, "divergence_c3_plane_T{}{}.npz".format(T, "_f32" if f32 else ""))
+    out = os.path.join(HERE, "divergence_c3_plane_T{}{}.npz".format(T, "_f32" if f32 else "_points" if points else ""))
+    if points:
+        S.update(points=sample_points(T, nx, ny), phi_pts=[], rho_pts=[])
     S["out"] = out            # rewritten after every iteration (a partial run is usable)
     rows, first = run(S, max_iters)
     save(out, rows, first, S)

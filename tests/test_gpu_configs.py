@@ -303,3 +303,58 @@ def test_chunked_thomas_matches_one_thread_per_mode(native, monkeypatch, nx, T, 
         finally:
             ctx.close()
     assert rel(out[1][0], out[0][0]) < 1e-6 and rel(out[1][1], out[0][1]) < 1e-6
+
+
+# The parity path: the same fixtures in the reference's arithmetic (fp64; jaxsrc/update_fns_in_pdhg.py:10).  Every
+# run of every fixture -- the epsl = 0.1 runs of C3 / C4 included -- at FIXED bounds with no float32 escape: the
+# north-star 1e-5 on phi, rho and every control, and the fp64 bar 1e-9 on phi / rho (the device and the oracle run
+# the same float64 algorithm from the same state; measured ~1e-13).  The fp64 kernels at each fixture's shape are
+# asserted through pdhg_path_info (k_precond_xt_f64_2d at nx = 4096 and its half-real form at C4's nx = 8192, the
+# 4-row fast row kernels at ny = 2048 / 4096, the time-marching dual).  C4's ny = 8192 rows are fp32-only so far.
+FP64_CASES = {
+    "c3_ws_T200": {"f64_xt": 1},
+    "c3_fr_4096x256": {"f64_xt": 1, "dual64": 1},
+    "c3_rows_ny4096": {"res64": 1, "dual64": 1},
+    "c2_x2048": {"dual64": 1},
+    "c2_rows_ny2048": {"res64": 1, "dual64": 1},
+    "c1_exact": {"glb_line": 1},
+    "c4_halfreal_x8192": {"f64_xt": 1, "half_real": 1, "dual64": 1},   # k_precond_xt_f64_2d<4096, 512, HR>
+}
+FP64_BAR = 1e-9
+
+
+@pytest.mark.parametrize("name", list(FP64_CASES))
+def test_config_fp64_fixed_bounds(native, name, parity_log):
+    F = _fixture(name)
+    egno, ndim, nx, ny, T = (int(v) for v in F["meta"])
+    failures = []
+    for tag in [str(t) for t in F["runs"]]:
+        g = lambda k: F[tag + "__" + k]  # noqa: E731
+        epsl, n, seeded = float(g("epsl")), int(g("iters")), bool(int(g("seeded")))
+        ip, ir = g("idx_phi"), g("idx_rho")
+        P = make_problem(egno, ndim, nx, ny, T, epsl, seeded=seeded)
+        phi0, rho0, alp0 = _f32_state(P)
+        ctx = device_ctx(P, "fp64")
+        try:
+            for key, val in FP64_CASES[name].items():
+                assert ctx.path_info(key) == val, (name, key, ctx.path_info(key), val)
+            ctx.set_state(phi0, rho0, alp0)
+            st = ctx.iterate(n, TAU, SIGMA, -1.0, 1)
+            phi, rho, alp = ctx.get_state()
+        finally:
+            ctx.close()
+        m = {"phi": rel(phi.reshape(-1)[ip], g("phi")), "rho": rel(rho.reshape(-1)[ir], g("rho"))}
+        for a, arr in enumerate(_live(ndim, egno, alp)):
+            ref = g("alp{}".format(a))
+            if np.linalg.norm(ref) > 0:
+                m["alp{}".format(a)] = rel(arr.reshape(-1)[ir], ref)
+        e1_o = float(g("err")[0])
+        m["err1"] = abs(st["err1"] - e1_o) / e1_o if e1_o > 0 else abs(st["err1"])
+        tol = {k: 1e-5 for k in m}
+        tol["phi"] = tol["rho"] = FP64_BAR
+        parity_log("test_config_fp64_fixed_bounds", "{}/{}".format(name, tag), m, tol, iters=n, epsl=epsl,
+                   seeded=seeded)
+        if not (st["iters_run"] == n and st["status"] == 0 and not st["nan_seen"]):
+            failures.append((tag, "run", st))
+        failures += [(tag, k, v, tol[k]) for k, v in m.items() if not v <= tol[k]]
+    assert not failures, failures
