@@ -1,4 +1,5 @@
-// Dual sweep (update_fns_in_pdhg.py:150-165) with the x neighbours staged through LDS.
+// Dual sweep (update_fns_in_pdhg.py:150-165) with the x neighbours staged through LDS (fp32, and fp64 without
+// the fused residual: R = double, 4 consecutive y per lane as dbl4).
 //
 // k_dual_fast_2d (kernels_2d_fast.hpp) gives every thread one x row and reads the x-1 / x+1 rows of
 // phi_bar straight from global memory, relying on L2 for the reuse between workgroups; the measured
@@ -24,17 +25,19 @@ namespace pdhg {
 // edge rows / columns contribute to the neighbouring tiles (p.ex: eps rho'/dx^2 + m1x/dx of row x0+RX-1
 // for the next tile's first row, eps rho'/dx^2 - m2x/dx of row x0 for the previous tile's last row;
 // p.ey: likewise per strip-edge column with m1y / m2y), and k_res_fwdy_fused_2d adds them.
-template <int EGNO, int RX, bool FR = false>
-__global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<float> p, int jchunk, int jbase, int jend,
+template <int EGNO, int RX, bool FR = false, typename R = float>
+__global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<R> p, int jchunk, int jbase, int jend,
                                                                      int zbase) {
+  using V = V4<R>;
   if (p.ctrl->done || p.ctrl->inner_done) return;
   constexpr int NA = (EGNO == 3) ? 2 : 4;
   constexpr int NS = 3 + 3 * NA;
   constexpr int YW = 256;                         // y strip per workgroup (64 lanes x float4)
   static_assert(!FR || EGNO != 3, "fused residual: egno 1/2 (four live controls)");
-  __shared__ __align__(16) float4 strip[2][RX + 2][YW / 4];
+  static_assert(!FR || sizeof(R) == 4, "fused residual: fp32 (the fp64 sweep runs the residual kernel)");
+  __shared__ __align__(16) V strip[2][RX + 2][YW / 4];
   // FR: [buffer][row][rho', m1x, m2x][lane]
-  __shared__ __align__(16) float4 flux[FR ? 2 : 1][FR ? RX : 1][3][YW / 4];
+  __shared__ __align__(16) V flux[FR ? 2 : 1][FR ? RX : 1][3][YW / 4];
   const int cur = p.ctrl->cur;
   const int src_set = (p.inplace || p.sub == 0) ? cur : 1 - cur;
   const int dst_set = p.inplace ? cur : 1 - cur;
@@ -61,26 +64,26 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<float> p, int jch
   const int ywm = nb_index(yw0 - 1, ny, p.bcy), ywp = nb_index(yw0 + 4 * kWave, ny, p.bcy);
   const bool zym = ywm < 0, zyp = ywp < 0;
   const int ywmc = zym ? 0 : ywm, ywpc = zyp ? 0 : ywp;
-  const float4 ay4 = ld4(p.ay + y);
-  const float axc = p.ax[x];
-  const float* rs = p.rho[src_set];
-  float* rd = p.rho[dst_set];
-  const float* as[NA];
-  float* ad[NA];
+  const V ay4 = ld4(p.ay + y);
+  const R axc = p.ax[x];
+  const R* rs = p.rho[src_set];
+  R* rd = p.rho[dst_set];
+  const R* as[NA];
+  R* ad[NA];
 #pragma unroll
   for (int a = 0; a < NA; ++a) {
     as[a] = p.alp[src_set][a];
     ad[a] = p.alp[dst_set][a];
   }
   struct In {
-    float4 pc, ph, rho, al[NA];
-    float el, er;
+    V pc, ph, rho, al[NA];
+    R el, er;
   };
   auto load = [&](int j) {
     In in;
-    const float* f1 = p.phibar + (size_t)(j + 1) * plane;
+    const R* f1 = p.phibar + (size_t)(j + 1) * plane;
     in.pc = ld4(f1 + rxc + y);
-    in.ph = has_h ? ld4(f1 + rxh + y) : z4();
+    in.ph = has_h ? ld4(f1 + rxh + y) : z4r<R>();
     in.el = f1[rxc + ywmc];
     in.er = f1[rxc + ywpc];
     const size_t o = (size_t)j * plane + rxc + y;
@@ -91,12 +94,12 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<float> p, int jch
   };
   auto stage = [&](const In& in, int buf) {
     strip[buf][r + 1][lane] = in.pc;
-    if (has_h) strip[buf][hslot][lane] = zh ? z4() : in.ph;
+    if (has_h) strip[buf][hslot][lane] = zh ? z4r<R>() : in.ph;
   };
   // FR state: the y part of row j-1's residual (eps*Dyy rho' and the y flux divergence), completed at
   // step j once rho'_j and the x neighbours' fluxes (LDS) are known
-  float yeps[4] = {0.f, 0.f, 0.f, 0.f}, ydiv[4] = {0.f, 0.f, 0.f, 0.f};
-  const bool use_eps = p.epsl != 0.f;
+  R yeps[4] = {(R)0, (R)0, (R)0, (R)0}, ydiv[4] = {(R)0, (R)0, (R)0, (R)0};
+  const bool use_eps = p.epsl != (R)0;
   const int nstrip = ny / YW;
   // R_{jr} (row jr of the next residual) = (rho'_{jr+1} - rho'_{jr})/dt + eps*Lap rho' - div m, from the
   // flux buffer fb (row jr's values) and rnext = rho'_{jr+1} at this thread's 4 points.  The time difference
@@ -104,61 +107,66 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<float> p, int jch
   // k_res_fwdy_fused_2d from the next slab's rho row 0 with the same fma -- rounds exactly as the row does
   // inside one window (with epsl > 0 the eps*Lap rho' terms are ~1e8 at dx = 2/8192, so any other order
   // differs by their ulp)
-  auto finish_res = [&](int jr, int fb, const float4& rnext, float cdt, bool tdiff = true) {
-    const float4 rc = flux[fb][r][0][lane], m1c = flux[fb][r][1][lane], m2c = flux[fb][r][2][lane];
+  auto finish_res = [&](int jr, int fb, const V& rnext, R cdt, bool tdiff = true) {
+    const V rc = flux[fb][r][0][lane], m1c = flux[fb][r][1][lane], m2c = flux[fb][r][2][lane];
     const int rmi = r > 0 ? r - 1 : r, rpi = r < RX - 1 ? r + 1 : r;   // wave-uniform
-    float4 rm = flux[fb][rmi][0][lane], m1m = flux[fb][rmi][1][lane];
-    float4 rp = flux[fb][rpi][0][lane], m2p = flux[fb][rpi][2][lane];
-    if (r == 0) rm = m1m = z4();            // row x0-1: added by the residual kernel
-    if (r == RX - 1) rp = m2p = z4();       // row x0+RX: likewise
-    float4 out;
+    V rm = flux[fb][rmi][0][lane], m1m = flux[fb][rmi][1][lane];
+    V rp = flux[fb][rpi][0][lane], m2p = flux[fb][rpi][2][lane];
+    if (r == 0) rm = m1m = z4r<R>();        // row x0-1: added by the residual kernel
+    if (r == RX - 1) rp = m2p = z4r<R>();   // row x0+RX: likewise
+    V out;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const float r0 = f4(rc, e);
-      float res = 0.f;
+      const R r0 = f4(rc, e);
+      R res = (R)0;
       if (use_eps) {
-        res = p.epsl * ((f4(rp, e) + f4(rm, e) - 2.f * r0) * p.inv_dx2);
+        res = p.epsl * ((f4(rp, e) + f4(rm, e) - (R)2 * r0) * p.inv_dx2);
         res = res + yeps[e];
       }
-      const float div = (f4(m1c, e) - f4(m1m, e)) * p.inv_dx + (f4(m2p, e) - f4(m2c, e)) * p.inv_dx + ydiv[e];
-      const float other = res - div + cdt;
-      f4set(out, e, tdiff ? __builtin_fmaf(f4(rnext, e) - r0, p.inv_dt, other) : other);
+      const R div = (f4(m1c, e) - f4(m1m, e)) * p.inv_dx + (f4(m2p, e) - f4(m2c, e)) * p.inv_dx + ydiv[e];
+      const R other = res - div + cdt;
+      f4set(out, e, tdiff ? fmar(f4(rnext, e) - r0, p.inv_dt, other) : other);
     }
     st4(p.res + (size_t)jr * plane + rxc + y, out);
   };
   if (j0 < j1) {
-    float4 f0 = ld4(p.phibar + (size_t)j0 * plane + rxc + y);   // phi_bar row j
+    V f0 = ld4(p.phibar + (size_t)j0 * plane + rxc + y);   // phi_bar row j
     // Two register sets, A and B, alternate between the rows (no copies: a register copy of a row still in
     // flight would wait for it).  Step j computes from cur (row j), re-fills cur with row j+2 and stages oth
     // (row j+1, loaded one step earlier) into LDS: the loads of a row are in flight across a whole step,
     // and no wait ever covers a store.
     auto step = [&](int j, In& cur, const In& oth) {
       const int buf = (j - j0) & 1;
-      const float4 pm = strip[buf][r][lane], pp = strip[buf][r + 2][lane], pc = cur.pc;
-      const float pyl = lane_from_prev(pc.w, zym ? 0.f : cur.el);
-      const float pyr = lane_from_next(pc.x, zyp ? 0.f : cur.er);
-      float4 rn4, an4[NA];
-      float4 m1x4, m2x4;
-      float m1y[4], m2y[4];
+      const V pm = strip[buf][r][lane], pp = strip[buf][r + 2][lane], pc = cur.pc;
+      const R pyl = lane_from_prev(pc.w, zym ? (R)0 : cur.el);
+      const R pyr = lane_from_next(pc.x, zyp ? (R)0 : cur.er);
+      V rn4, an4[NA];
+      V m1x4, m2x4;
+      R m1y[4], m2y[4];
       // this step's 4 points summed in fp32 (4 terms), then one fp64 add per sum: the fixed-order fp64
       // accumulation over t stays, with a quarter of the fp64 work
-      float fs[NS];
+      // (fp64: straight into the fixed-order fp64 sums, s)
+      R fsb[sizeof(R) == 4 ? NS : 1];
+      double* const fs_d = s;
+      auto fsr = [&](int i) -> R& { if constexpr (sizeof(R) == 4) return fsb[i]; else return fs_d[i]; };
+      if constexpr (sizeof(R) == 4) {
 #pragma unroll
-      for (int i = 0; i < NS; ++i) fs[i] = 0.f;
+        for (int i = 0; i < NS; ++i) fsb[i] = (R)0;
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float c = f4(pc, e);
-        const float lft = e == 0 ? pyl : f4(pc, e - 1);
-        const float rgt = e == 3 ? pyr : f4(pc, e + 1);
-        float ao[4], an[4], fo[4];
+        const R c = f4(pc, e);
+        const R lft = e == 0 ? pyl : f4(pc, e - 1);
+        const R rgt = e == 3 ? pyr : f4(pc, e + 1);
+        R ao[4], an[4], fo[4];
 #pragma unroll
         for (int a = 0; a < NA; ++a) ao[a] = f4(cur.al[a], e);
-        const float rho = f4(cur.rho, e);
-        const float rn = dual_point<float, EGNO>(p, c, f4(pm, e), f4(pp, e), lft, rgt, f4(f0, e), rho, ao, axc,
+        const R rho = f4(cur.rho, e);
+        const R rn = dual_point<R, EGNO>(p, c, f4(pm, e), f4(pp, e), lft, rgt, f4(f0, e), rho, ao, axc,
                                                  f4(ay4, e), an, FR ? fo : nullptr);
         f4set(rn4, e, rn);
         if constexpr (FR) {   // fluxes (rho'+1e-4) f(alp') of row j (m1f / m2f of the residual kernel)
-          const float rq = rn + 1e-4f;
+          const R rq = rn + (R)1e-4;
           f4set(m1x4, e, rq * fo[0]);
           f4set(m2x4, e, rq * fo[1]);
           m1y[e] = rq * fo[2];
@@ -166,25 +174,29 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<float> p, int jch
         }
 #pragma unroll
         for (int a = 0; a < NA; ++a) f4set(an4[a], e, an[a]);
-        const float dr = rn - rho;
-        fs[0] = fmaf(dr, dr, fs[0]);
-        fs[1] = fmaf(rn, rn, fs[1]);
-        fs[2] = fmaf(rho, rho, fs[2]);
+        if (sizeof(R) == 4 || live) {
+          const R dr = rn - rho;
+          fsr(0) = fmar(dr, dr, fsr(0));
+          fsr(1) = fmar(rn, rn, fsr(1));
+          fsr(2) = fmar(rho, rho, fsr(2));
 #pragma unroll
-        for (int a = 0; a < NA; ++a) {
-          const float da = an[a] - ao[a];
-          fs[3 + 3 * a] = fmaf(da, da, fs[3 + 3 * a]);
-          fs[4 + 3 * a] = fmaf(an[a], an[a], fs[4 + 3 * a]);
-          fs[5 + 3 * a] = fmaf(ao[a], ao[a], fs[5 + 3 * a]);
+          for (int a = 0; a < NA; ++a) {
+            const R da = an[a] - ao[a];
+            fsr(3 + 3 * a) = fmar(da, da, fsr(3 + 3 * a));
+            fsr(4 + 3 * a) = fmar(an[a], an[a], fsr(4 + 3 * a));
+            fsr(5 + 3 * a) = fmar(ao[a], ao[a], fsr(5 + 3 * a));
+          }
         }
       }
       // cur is consumed: the row after next goes into its registers now, ahead of this step's stores, so the
       // wait for the next row's loads (at the staging below) counts these 7 loads and never this step's stores
-      const float4 pcs = pc;
+      const V pcs = pc;
       cur = load(min(j + 2, j1 - 1));   // clamped: the last rows re-load row j1-1 (never used)
-      if (live) {
+      if constexpr (sizeof(R) == 4) {
+        if (live) {
 #pragma unroll
-        for (int i = 0; i < NS; ++i) s[i] += (double)fs[i];
+          for (int i = 0; i < NS; ++i) s[i] += (double)fsb[i];
+        }
       }
       const size_t o = (size_t)j * plane + rxc + y;
       if (live && !(p.dbg & 128)) {   // PDHG_DBG 128: no rho / alp stores (timing experiments only)
@@ -194,20 +206,20 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<float> p, int jch
       }
       f0 = pcs;
       if constexpr (FR) if (!(p.dbg & 256)) {   // PDHG_DBG 256: no residual / edge terms (timing only)
-        if (j > j0) finish_res(j - 1, buf ^ 1, rn4, 0.f);   // row j-1, with rho'_j
+        if (j > j0) finish_res(j - 1, buf ^ 1, rn4, (R)0);   // row j-1, with rho'_j
         flux[buf][r][0][lane] = rn4;
         flux[buf][r][1][lane] = m1x4;
         flux[buf][r][2][lane] = m2x4;
         // y part of row j: neighbours from the adjacent lanes; the strip's outer columns are left out
         // (0 here) and handed to the residual kernel through p.ey
-        const float rym = lane_from_prev(rn4.w, 0.f), ryp = lane_from_next(rn4.x, 0.f);
-        const float m1ym = lane_from_prev(m1y[3], 0.f), m2yp = lane_from_next(m2y[0], 0.f);
+        const R rym = lane_from_prev(rn4.w, (R)0), ryp = lane_from_next(rn4.x, (R)0);
+        const R m1ym = lane_from_prev(m1y[3], (R)0), m2yp = lane_from_next(m2y[0], (R)0);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float r0 = f4(rn4, e);
-          const float lo = e == 0 ? rym : f4(rn4, e - 1), hi = e == 3 ? ryp : f4(rn4, e + 1);
-          const float m1l = e == 0 ? m1ym : m1y[e - 1], m2h = e == 3 ? m2yp : m2y[e + 1];
-          yeps[e] = p.epsl * ((hi + lo - 2.f * r0) * p.inv_dy2);
+          const R r0 = f4(rn4, e);
+          const R lo = e == 0 ? rym : f4(rn4, e - 1), hi = e == 3 ? ryp : f4(rn4, e + 1);
+          const R m1l = e == 0 ? m1ym : m1y[e - 1], m2h = e == 3 ? m2yp : m2y[e + 1];
+          yeps[e] = p.epsl * ((hi + lo - (R)2 * r0) * p.inv_dy2);
           ydiv[e] = (m1y[e] - m1l) * p.inv_dy + (m2h - m2y[e]) * p.inv_dy;
         }
         // the neighbouring strips' outer-column terms that need this strip's edge column: lane 0 feeds the
@@ -215,7 +227,7 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<float> p, int jch
         // (eps rho'/dy^2 + m1y/dy); k_res_fwdy_fused_2d adds them (p.ey)
         if (lane == 0 || lane == kWave - 1) {
           const bool first = lane == 0;
-          float c = first ? -m2y[0] * p.inv_dy : m1y[3] * p.inv_dy;
+          R c = first ? -m2y[0] * p.inv_dy : m1y[3] * p.inv_dy;
           if (use_eps) c = c + p.epsl * ((first ? rn4.x : rn4.w) * p.inv_dy2);
           const int sy = first ? (blockIdx.y == 0 ? nstrip - 1 : blockIdx.y - 1)
                                : (blockIdx.y + 1 == nstrip ? 0 : blockIdx.y + 1);
@@ -227,10 +239,10 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<float> p, int jch
           const bool top = r == 0;
           const int ngx = nx / RX, tile = x0 / RX;
           const int tt = top ? (tile == 0 ? ngx - 1 : tile - 1) : (tile + 1 == ngx ? 0 : tile + 1);
-          float4 c;
+          V c;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            float v = top ? -f4(m2x4, e) * p.inv_dx : f4(m1x4, e) * p.inv_dx;
+            R v = top ? -f4(m2x4, e) * p.inv_dx : f4(m1x4, e) * p.inv_dx;
             if (use_eps) v = v + p.epsl * (f4(rn4, e) * p.inv_dx2);
             f4set(c, e, v);
           }
@@ -256,8 +268,8 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<float> p, int jch
       // the next slab's row 0: the time difference is left to k_res_fwdy_fused_2d (halo)
       __syncthreads();
       const bool inner = j1 < p.T;
-      const float4 rnx = inner ? ld4(rd + (size_t)j1 * plane + rxc + y) : z4();
-      finish_res(j1 - 1, (j1 - 1 - j0) & 1, rnx, (!inner && p.last_slab) ? p.c_over_dt : 0.f,
+      const V rnx = inner ? ld4(rd + (size_t)j1 * plane + rxc + y) : z4r<R>();
+      finish_res(j1 - 1, (j1 - 1 - j0) & 1, rnx, (!inner && p.last_slab) ? p.c_over_dt : (R)0,
                  inner || p.last_slab);
     }
   }

@@ -352,10 +352,12 @@ struct Impl : ImplBase {
         // x rows through LDS (k_dual_lds_2d) for the fused-residual sweep; a context created for
         // rho_alp_iters > 1 (no fused residual) sweeps row-per-thread: measured at C3 with rho_alp_iters = 10,
         // k_dual_fast_2d 25.7 ms per sub-iteration against 38.1 for k_dual_lds_2d (2 waves per SIMD)
-        dual_rx = (sizeof(R) == 4 && nx % 8 == 0 && !short_dual && !two_sets) ? 8 : 0;
+        // fp64 (k_dual_lds_2d<EGNO, 8, false, double>, 230 VGPRs, no spill): the phi_bar x neighbours through LDS
+        // instead of the row-per-thread kernel's 1.25x re-reads from L2 (fp64 C3: 200 GB fetched for 161 GB of reads)
+        dual_rx = (nx % 8 == 0 && !short_dual && !two_sets) ? 8 : 0;
         if (const char* e = getenv("PDHG_DUAL_RX")) {   // tuning override: 0 = row-per-thread kernel
           const int v = atoi(e);
-          if (v == 0 || (sizeof(R) == 4 && (v == 4 || v == 8 || v == 16) && nx % v == 0)) dual_rx = v;
+          if (v == 0 || (((sizeof(R) == 4 && (v == 4 || v == 16)) || v == 8) && nx % v == 0)) dual_rx = v;
         }
         NTd = dual_rx ? dual_rx * 64 : std::min(256, ny / 4);
         gxd = dual_rx ? nx / dual_rx : nx;
@@ -1225,7 +1227,10 @@ struct Impl : ImplBase {
     } else {
       const dim3 g(gxd, gyd, gz);
       res_valid = false;
-      hipLaunchKernelGGL((k_dual_fast_2d<EGNO, double>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase);
+      if (dual_rx == 8)
+        hipLaunchKernelGGL((k_dual_lds_2d<EGNO, 8, false, double>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase);
+      else
+        hipLaunchKernelGGL((k_dual_fast_2d<EGNO, double>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase);
     }
   }
   int launch_dual_fast(const KP<R>& p, int lo = 0, int hi = -1, int zbase = 0) {

@@ -12,9 +12,14 @@
 //     part q+1 sweeps forward (SlabRunner's schedule, pdhg_amd/slab.py);
 //   * waits are per neighbour (rho halo: r+1 -> r, phi_bar halo: r-1 -> r, D: r-1 -> r, S1: r+1 -> r), never
 //     all-to-all; only the long-range carry modes (few, pdhg_slab_long_modes) and the sums need every slab;
-//   * the 16-double sum vectors are gathered on slab 0's device (slab 0's stream waits each slab's event),
-//     folded in slab order by k_multi_sum, and copied back by every slab's main stream after one event, so
-//     every slab takes the same stop decisions in its own control block.
+//   * the 16-double sum vectors: with peer access between every pair of devices (xGMI), every slab's main
+//     stream waits for every slab's contribution event and one 64-thread kernel on its own device folds the P
+//     vectors in slab order straight from their owners' memory (peer pointers) -- the same order on every
+//     device, so every slab takes bitwise the same stop decisions in its own control block, with no copies
+//     and no device waiting for another's fold.  Contributions alternate between two buffers per slab: slab q
+//     rewrites a buffer two allreduces later, after its own fold of the allreduce in between, which waited for
+//     every slab's next contribution, recorded after that slab's fold of this one.  Without peer access the
+//     vectors are gathered on slab 0's device, folded there (k_multi_sum) and copied back.
 // Reuse of an exchange buffer is safe without extra events: every plane a receiver consumes is consumed
 // before that receiver's next sums contribution, and every producer overwrites its send buffer only after
 // the following sums fold, which waited for every slab's contribution.
@@ -24,6 +29,18 @@
 #include <vector>
 
 namespace pdhg {
+constexpr int kMultiMaxPeerFold = 16;
+struct SumPtrs {
+  const double* p[kMultiMaxPeerFold];
+};
+// fixed-order fold of P contribution vectors read in place (local or peer device memory)
+__global__ void k_multi_fold(SumPtrs in, int n, double* __restrict__ out) {
+  const int s = threadIdx.x;
+  if (s >= pdhg::kNumSums) return;
+  double t = 0.0;
+  for (int q = 0; q < n; ++q) t += in.p[q][s];
+  out[s] = t;
+}
 __global__ void k_multi_sum(const double* __restrict__ in, int n, double* __restrict__ out) {
   const int s = threadIdx.x;   // one thread per sum, slabs in order (fixed-order, deterministic)
   if (s >= pdhg::kNumSums) return;
@@ -50,15 +67,18 @@ struct pdhg_multi {
     float *rho_send = nullptr, *rho_recv = nullptr, *pb_send = nullptr, *pb_recv = nullptr;
     float *DS = nullptr, *GS = nullptr, *Dl = nullptr, *S1r = nullptr, *LONG = nullptr, *allLong = nullptr,
           *allGS = nullptr;
-    double* sums = nullptr;
+    double* sums = nullptr;      // the folded vector this slab's finalize kernels read
+    double* contrib = nullptr;   // peer fold: [2][16] contributions, alternating per allreduce
     // events: producer side (main stream) and receiver side (side stream)
     hipEvent_t rho = nullptr, rho_in = nullptr, longp = nullptr, long_in = nullptr, pb = nullptr, pb_in = nullptr,
                sum = nullptr;
     std::vector<hipEvent_t> ds, carry_in;   // per part
   };
   std::vector<Buf> b;
-  double* gather = nullptr;   // slab 0's device: [P][16] sums, then the folded [16]
+  double* gather = nullptr;   // slab 0's device: [P][16] sums, then the folded [16] (no peer access)
   hipEvent_t folded = nullptr;
+  bool peer_fold = false;     // every pair of devices has peer access: per-device folds of the contributions
+  unsigned round = 0;         // allreduces so far (peer fold: which contribution buffer)
   std::vector<void*> allocs;  // (device, pointer) freed at destroy
   std::vector<int> alloc_dev;
   std::vector<hipEvent_t> all_events;   // (created on the device of the slab that records them)
@@ -129,9 +149,25 @@ struct pdhg_multi {
     }
     return rec(marks[marks_used - 1][i], 0, st[0]);
   }
-  // sums of every slab -> fixed-order fold on slab 0 -> back to every slab
+  // where slab r writes its contribution to the next allreduce
+  double* cs(int r) { return peer_fold ? b[r].contrib + (size_t)(round & 1) * kNumSums : b[r].sums; }
+  // sums of every slab -> fixed-order fold -> every slab (b[r].sums)
   int allreduce() {
     int rc;
+    if (peer_fold) {
+      SumPtrs ptrs{};
+      for (int q = 0; q < P; ++q) ptrs.p[q] = cs(q);
+      for (int q = 0; q < P; ++q)
+        if ((rc = rec(b[q].sum, q, st[q]))) return rc;
+      for (int r = 0; r < P; ++r) {
+        for (int q = 0; q < P; ++q)
+          if (q != r && (rc = wait(r, st[r], b[q].sum))) return rc;
+        hipLaunchKernelGGL(pdhg::k_multi_fold, dim3(1), dim3(64), 0, st[r], ptrs, P, b[r].sums);
+        HIP_TRY(hipGetLastError());
+      }
+      ++round;
+      return PDHG_OK;
+    }
     for (int q = 0; q < P; ++q)
       if ((rc = rec(b[q].sum, q, st[q]))) return rc;
     for (int q = 1; q < P; ++q)
@@ -168,7 +204,10 @@ struct pdhg_multi {
       j1.push_back(j + n);
       j += n;
     }
-    // peer access where the runtime offers it (copies work either way)
+    // peer access where the runtime offers it (copies work either way; the sums fold reads peer memory only when
+    // every pair has it)
+    peer_fold = P <= pdhg::kMultiMaxPeerFold;
+    if (const char* e = getenv("PDHG_MULTI_PEER_FOLD")) peer_fold = peer_fold && atoi(e) != 0;   // tuning override
     for (int r = 0; r < P; ++r)
       for (int q = 0; q < P; ++q) {
         if (dev[r] == dev[q]) continue;
@@ -178,6 +217,8 @@ struct pdhg_multi {
           hipError_t e = hipDeviceEnablePeerAccess(dev[q], 0);
           if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return fail(PDHG_ERR_HIP, "peer access");
           (void)hipGetLastError();
+        } else {
+          peer_fold = false;
         }
       }
     s.assign(P, nullptr);
@@ -211,7 +252,7 @@ struct pdhg_multi {
       if ((rc = alloc(r, &x.rho_send, sp)) || (rc = alloc(r, &x.rho_recv, sp)) || (rc = alloc(r, &x.pb_send, sp)) ||
           (rc = alloc(r, &x.pb_recv, sp)) || (rc = alloc(r, &x.DS, 2 * spec)) || (rc = alloc(r, &x.GS, 2 * spec)) ||
           (rc = alloc(r, &x.Dl, spec)) || (rc = alloc(r, &x.S1r, spec)) || (rc = alloc(r, &x.allGS, 2 * spec * P)) ||
-          (rc = alloc(r, &x.sums, (size_t)kNumSums)))
+          (rc = alloc(r, &x.sums, (size_t)kNumSums)) || (rc = alloc(r, &x.contrib, (size_t)2 * kNumSums)))
         return rc;
       if ((rc = pdhg_slab_carry_gain(s[r], x.GS))) return rc;
     }
@@ -318,7 +359,7 @@ struct pdhg_multi {
           return rc;
       }
     for (int r = 0; r < P; ++r)
-      if ((rc = pdhg_slab_update(s[r], tau, b[r].sums))) return rc;
+      if ((rc = pdhg_slab_update(s[r], tau, cs(r)))) return rc;
     if ((rc = mark(3))) return rc;
     // phi_bar halo (row T of slab r-1 -> row 0 of slab r) || the primal sums and the interior dual rows
     for (int r = 0; r < P; ++r)
@@ -333,12 +374,12 @@ struct pdhg_multi {
     if ((rc = mark(4))) return rc;
     for (int sub = 0; sub < k; ++sub) {
       for (int r = 0; r < P; ++r)
-        if ((rc = pdhg_slab_dual(s[r], sigma, k, sub, b[r].sums, sub == 0 ? 1 : 3))) return rc;
+        if ((rc = pdhg_slab_dual(s[r], sigma, k, sub, cs(r), sub == 0 ? 1 : 3))) return rc;
       if (sub == 0)
         for (int r = 0; r < P; ++r) {
           if (r > 0 && ((rc = wait(r, st[r], b[r].pb_in)) || (rc = pdhg_slab_plane_in(s[r], 1, b[r].pb_recv))))
             return rc;
-          if ((rc = pdhg_slab_dual(s[r], sigma, k, sub, b[r].sums, 2))) return rc;
+          if ((rc = pdhg_slab_dual(s[r], sigma, k, sub, cs(r), 2))) return rc;
         }
       if ((rc = allreduce())) return rc;
       for (int r = 0; r < P; ++r)
@@ -346,7 +387,7 @@ struct pdhg_multi {
     }
     if ((rc = mark(5))) return rc;
     for (int r = 0; r < P; ++r)
-      if ((rc = pdhg_slab_outer(s[r], k, b[r].sums))) return rc;
+      if ((rc = pdhg_slab_outer(s[r], k, cs(r)))) return rc;
     if (k > 1 && (rc = allreduce())) return rc;
     for (int r = 0; r < P; ++r)
       if ((rc = pdhg_slab_outer_finalize(s[r], eps, k, b[r].sums))) return rc;
@@ -520,6 +561,7 @@ int pdhg_multi_info(pdhg_multi* m, const char* key, int* value) {
   if (k == "ndev") *value = m->P;
   else if (k == "long_modes") *value = m->K;
   else if (k == "parts") *value = m->parts;
+  else if (k == "peer_fold") *value = m->peer_fold ? 1 : 0;
   else if (k.rfind("rows:", 0) == 0) {
     const int r = atoi(k.c_str() + 5);
     if (r < 0 || r >= m->P) return fail(PDHG_ERR_ARG, "slab %d of %d", r, m->P);

@@ -20,10 +20,14 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("fold", ["1", "0"], ids=["peer_fold", "gather_fold"])
 @pytest.mark.parametrize("egno,nx,ny,T,nr,k", CASES, ids=[f"e{c[0]}_{c[1]}x{c[2]}_T{c[3]}_P{c[4]}_k{c[5]}"
                                                          for c in CASES])
-def test_multi_matches_single_context(native, egno, nx, ny, T, nr, k):
+def test_multi_matches_single_context(native, egno, nx, ny, T, nr, k, fold, monkeypatch):
+    """fold 1: every slab folds the P sum vectors itself from their owners' buffers (peer pointers; on one GPU
+    local ones), alternating contribution buffers; fold 0: gather on slab 0, fold, copy back."""
     import torch
+    monkeypatch.setenv("PDHG_MULTI_PEER_FOLD", fold)
     from pdhg_amd.context import PDHGContext
     from pdhg_amd.multi import MultiContext
     from pdhg_amd.slab import LocalComm, SlabContext, SlabRunner, join_state, slab_bounds, split_state
@@ -39,6 +43,7 @@ def test_multi_matches_single_context(native, egno, nx, ny, T, nr, k):
     m = MultiContext(egno, nx, ny, T, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"], devices=[0] * nr,
                      epsl=0.0, rho_alp_iters=k)
     assert m.info("ndev") == nr
+    assert m.info("peer_fold") == int(fold)
     assert [m.info("rows:%d" % i) for i in range(nr)] == [j1 - j0 for j0, j1 in slab_bounds(T, nr)]
     m.set_state(P["phi"], P["rho"], P["alp"])
     st = m.iterate(n, tau, sigma, -1.0, k)

@@ -87,6 +87,10 @@ DUAL_CASES = [
     (1, 2, 6, 256, 3, 0.0),
     (2, 2, 5, 512, 3, 0.1),
     (3, 2, 4, 256, 2, 0.1),
+    # nx % 8 == 0: with rho_alp_iters = 1 the x rows go through LDS (k_dual_lds_2d<EGNO, 8, false, double>)
+    (1, 2, 16, 256, 3, 0.0),
+    (2, 2, 24, 512, 4, 0.1),
+    (3, 2, 16, 256, 2, 0.1),
 ]
 
 
@@ -94,8 +98,9 @@ DUAL_CASES = [
 @pytest.mark.parametrize("case", DUAL_CASES, ids=["e{}_{}x{}_T{}_eps{}".format(c[0], c[2], c[3], c[4], c[5])
                                                   for c in DUAL_CASES])
 def test_dual64_matches_oracle(native, case, k, monkeypatch):
-    """fp64 dual through the row-per-thread time-marching kernel (k_dual_fast_2d<EGNO, double>, ny % 256 == 0)
-    against the fp64 oracle (update_fns_in_pdhg.py:150-180) and the generic per-point kernel (PDHG_DUAL64=0)."""
+    """fp64 dual through the time-marching kernels (ny % 256 == 0): x rows through LDS (k_dual_lds_2d<EGNO, 8, false,
+    double>, k = 1 and nx % 8 == 0) or row-per-thread (k_dual_fast_2d<EGNO, double>), against the fp64 oracle
+    (update_fns_in_pdhg.py:150-180) and the generic per-point kernel (PDHG_DUAL64=0)."""
     P = make_problem(*case)
     rng = np.random.default_rng(11)
     phi_bar = P["phi"] + 0.05 * rng.standard_normal(P["phi"].shape)
@@ -108,6 +113,8 @@ def test_dual64_matches_oracle(native, case, k, monkeypatch):
         ctx = device_ctx(P, "fp64", rho_alp_iters=k)
         try:
             assert ctx.path_info("dual64") == int(flag)
+            if flag == "1":   # LDS x rows (8 per workgroup) for k = 1 and nx % 8 == 0, else row-per-thread
+                assert ctx.path_info("fast_dual") == (8 if (k == 1 and case[2] % 8 == 0) else 0)
             ctx.set_state(P["phi"], P["rho"], P["alp"])
             ctx.set_phi_bar(phi_bar)
             ctx.update_dual(SIGMA, -1.0, k)
