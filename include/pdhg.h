@@ -196,7 +196,9 @@ int pdhg_algorithmic_bytes(pdhg_ctx* ctx, int k, const char* kernel_class, doubl
  * (pdhg_slab_carry_gain, iteration-invariant, gather once).  Planes are device pointers (float; D/S1 and
  * G/S2 are pairs of spectral planes, see pdhg_slab_plane_size); sums are device vectors of 16 doubles.
  * All calls enqueue on the context's stream (pdhg_set_stream to share the caller's).
- * fp32, ndim 2, power-of-two nx in [512, 8192], bc (0,0). */
+ * fp32, ndim 2, a power-of-two ny in [256, 8192] (the residual's halo-row split runs the fast row kernels); any nx
+ * the single context supports: the fast DHT x kernels, or the generic runtime-radix kernel (other nx, and egno 3's
+ * bc (1,0) DCT along x, jaxsrc/utils/utils_precond.py:159-174). */
 int pdhg_create_slab(const pdhg_problem* p, int j0, int T_total, int device, pdhg_ctx** out);
 int pdhg_set_stream(pdhg_ctx* ctx, void* hip_stream);
 int pdhg_slab_plane_size(pdhg_ctx* ctx, unsigned long long* spatial, unsigned long long* spectral);
@@ -271,8 +273,10 @@ int pdhg_xslab_update(pdhg_ctx* ctx, double tau, double* sums);            /* in
  * sums folded in slab order on the first device, so a C / Go / Java caller gets the multi-GPU window without
  * re-implementing pdhg_amd/slab.py or linking RCCL.  The window's rows [0, p->T) are split near-equally
  * (the first T % ndev slabs get one more row).  State arrays are the WHOLE window in the reference layouts
- * (as pdhg_set_state / pdhg_get_state).  Same support as the t-slab: fp32, ndim 2, bc (0,0), power-of-two nx
- * in [512, 8192].  Keys of pdhg_multi_info: "ndev", "long_modes", "rows:<i>" (rows of slab i). */
+ * (as pdhg_set_state / pdhg_get_state).  Same support as the t-slab (fp32, ndim 2, bc (0,0) or egno 3's (1,0)).
+ * The stop-test sums are folded on every device from its peers' buffers when all device pairs have peer
+ * access (environment PDHG_MULTI_PEER_FOLD=0: gathered on the first device and copied back).
+ * Keys of pdhg_multi_info: "ndev", "long_modes", "rows:<i>" (rows of slab i), "peer_fold". */
 typedef struct pdhg_multi pdhg_multi;
 int pdhg_create_multi(const pdhg_problem* p, const int* devices, int ndev, pdhg_multi** out);
 int pdhg_multi_destroy(pdhg_multi* m);

@@ -131,6 +131,10 @@ __global__ void __launch_bounds__(NTB) k_res_fwdy_2d(KP<R> p, F ply, const cplx<
 //      = 5 M * sizeof(R)  (M = 8192 fp32 / 4096 fp64 -> 160 KiB).
 // Each workgroup owns its M modes for all t: forward (DHT_x, elimination) for k = 0..T-1,
 // then backward (substitution, inverse DHT_x) for k = T-1..0.  b' of rows < T-1 goes through HBM.
+// t-slab (p.slab; any transform, so egno 3's DCT slabs too): the pivots are the closed form at the GLOBAL row
+// j0 + k, the forward sweep starts from a zero carry and stores every row (the Neumann end only on the last
+// slab), xt_phase 1 stops after it, xt_phase 2 runs only the backward sweep from the right carry (carry_y) over
+// the fixed-up rows -- the phases of k_precond_xt_fast_2d (oracle/slab_oracle.py).
 template <typename R, class F>
 __global__ void __launch_bounds__(512) k_precond_xt_2d(KP<R> p, F plx, const cplx<R>* __restrict__ twx) {
   using C = cplx<R>;
@@ -154,15 +158,17 @@ __global__ void __launch_bounds__(512) k_precond_xt_2d(KP<R> p, F plx, const cpl
   const R inv_ae = (R)1 / ae;
 
   const bool dct = p.dctw != nullptr;   // bc_x = 1: DCT-II along x (egno 3)
+  const int j0 = p.j0, Tg = p.Tg;       // global row of local row 0, window length (single context: 0, T)
   for (int pos = tid; pos < M; pos += NT) {
     const int kx = pos >> p.lB, c = pos & (B - 1);
     const R d0 = p.C - p.lamx[kx] - p.cx[kx] * p.lamy[b * B + c];
     const R delta = d0 / ((R)2 * ae);
     const R th = log1p(delta + sqrt(delta * (delta + (R)2)));   // cosh(th) = 1 + d0/(2 ae)
     sth[pos] = th;
-    sE[pos] = expm1((R)-2 * th);                                 // E_1, E_m = expm1(-2 th m)
+    sE[pos] = expm1((R)-2 * th * (R)(j0 + 1));                   // E_{j0+1}, E_m = expm1(-2 th m)
     sbp[pos] = (R)0;
   }
+  if (p.xt_phase != 2) {
   C pf[PF];
   {
     const C* s0 = reinterpret_cast<const C*>(wb);
@@ -208,36 +214,47 @@ __global__ void __launch_bounds__(512) k_precond_xt_2d(KP<R> p, F plx, const cpl
       const R h = (c & 1) ? hb : ha;
       const R th = sth[pos];
       const R prev = sbp[pos];
-      if (k < T - 1) {
+      const int kg = j0 + k;   // global row
+      if (k < T - 1 || !p.last_slab) {
         // 1/u_k = e^-th E_{k+1} / (ae E_{k+2})   (closed form of the Thomas pivots)
-        const R E2 = expm1((R)-2 * th * (R)(k + 2));
-        const R g = (th > (R)0) ? exp(-th) * sE[pos] / E2 : (R)(k + 1) / (R)(k + 2);
+        const R E2 = expm1((R)-2 * th * (R)(kg + 2));
+        const R g = (th > (R)0) ? exp(-th) * sE[pos] / E2 : (R)(kg + 1) / (R)(kg + 2);
         const R v = (h * inv_ae + prev) * g;
         sE[pos] = E2;
         sbp[pos] = v;
         dst[pos] = v;
       } else {
-        // Neumann last row: u_{T-1} = d0 + ae expm1(-th)(1 + e^{-th(2T-1)}) / E_T
+        // Neumann last row: u_{Tg-1} = d0 + ae expm1(-th)(1 + e^{-th(2Tg-1)}) / E_Tg
         const R d0 = p.C - p.lamx[kx] - p.cx[kx] * p.lamy[b * B + c];
         R u;
         if (th > (R)0) {
-          const R ET = expm1((R)-2 * th * (R)T);
-          u = d0 + ae * expm1(-th) * ((R)1 + exp(-th * (R)(2 * T - 1))) / ET;
+          const R ET = expm1((R)-2 * th * (R)Tg);
+          u = d0 + ae * expm1(-th) * ((R)1 + exp(-th * (R)(2 * Tg - 1))) / ET;
         } else {
-          u = d0 + ae / (R)T;
+          u = d0 + ae / (R)Tg;
         }
         sbp[pos] = (h + ae * prev) / u;
+        if (p.slab) dst[pos] = sbp[pos];   // re-read (after the carry fix-up) by the backward sweep
       }
     }
     __syncthreads();
   }
+  }   // xt_phase != 2
+  if (p.xt_phase == 1) return;   // forward sweep only (t-slab: the carry fix-up runs in between)
   // ---------------- backward: substitution + inverse DHT_x, k = T-1..0 ----------------
   // x_k = b'_k + g_k x_{k+1},  g_k = ae/u_k = e^-th E_{k+1}/E_{k+2}
+  // single context: from x_{T-1} (the forward's Neumann row, in LDS); t-slab: from the right carry x_{j0+T}
+  // over every local row of the fixed-up b' in HBM
   R* Ar = reinterpret_cast<R*>(A);
-  for (int pos = tid; pos < M; pos += NT) sE[pos] = expm1((R)-2 * sth[pos] * (R)T);   // E_{(T-2)+2}
+  const int ks = p.slab ? T - 1 : T - 2;   // first substituted local row
+  for (int pos = tid; pos < M; pos += NT) {
+    sE[pos] = expm1((R)-2 * sth[pos] * (R)(j0 + ks + 2));   // E_{k+2} of row ks
+    if (p.slab) sbp[pos] = p.carry_y ? p.carry_y[(size_t)b * M + pos] : (R)0;
+  }
+  __syncthreads();
   R pb[PB];
-  if (T >= 2) {
-    const R* s0 = wb + (size_t)(T - 2) * kstride;
+  if (ks >= 0) {
+    const R* s0 = wb + (size_t)ks * kstride;
 #pragma unroll
     for (int i = 0; i < PB; ++i) {
       const int pos = tid + i * NT;
@@ -251,10 +268,11 @@ __global__ void __launch_bounds__(512) k_precond_xt_2d(KP<R> p, F plx, const cpl
       const int pos = tid + i * NT;
       if (pos < M) {
         R x = sbp[pos];
-        if (k < T - 1) {
+        if (k <= ks) {
           const R th = sth[pos];
-          const R E1 = expm1((R)-2 * th * (R)(k + 1));
-          const R g = (th > (R)0) ? exp(-th) * E1 / sE[pos] : (R)(k + 1) / (R)(k + 2);
+          const int kg = j0 + k;
+          const R E1 = expm1((R)-2 * th * (R)(kg + 1));
+          const R g = (th > (R)0) ? exp(-th) * E1 / sE[pos] : (R)(kg + 1) / (R)(kg + 2);
           x = pb[i] + g * x;
           sE[pos] = E1;
           sbp[pos] = x;
@@ -262,7 +280,7 @@ __global__ void __launch_bounds__(512) k_precond_xt_2d(KP<R> p, F plx, const cpl
         Ar[pos] = x;
       }
     }
-    if (k >= 1 && k - 1 < T - 1) {
+    if (k >= 1 && k - 1 <= ks) {
       const R* sn = wb + (size_t)(k - 1) * kstride;
 #pragma unroll
       for (int i = 0; i < PB; ++i) {

@@ -464,9 +464,11 @@ struct Impl : ImplBase {
       if (p.nb % xs_P) return fail(PDHG_ERR_UNSUPPORTED, "%d column blocks do not split over %d ranks", p.nb, xs_P);
       xs_nbs = p.nb / xs_P;
     }
-    if (slab && !(is2d && fast_xt))
-      return fail(PDHG_ERR_UNSUPPORTED, "t-slab decomposition needs ndim 2, fp32 and a power-of-two nx in "
-                                        "[512, 4096] (fast x-transform kernels)");
+    // t-slab phases: the fast DHT x kernels (power-of-two nx 512 - 8192) or the generic runtime-radix kernel (any
+    // nx, the DCT of egno 3's bc (1, 0)); the halo row split of the residual needs the fast row kernels
+    if (slab && !(is2d && sizeof(R) == 4 && fast_rows))
+      return fail(PDHG_ERR_UNSUPPORTED, "t-slab decomposition needs ndim 2, fp32 and a power-of-two ny in [256, 8192] "
+                                        "(fast row kernels)");
 
     // ---- device buffers ----
     const size_t npl = plane();
@@ -950,7 +952,6 @@ struct Impl : ImplBase {
     } else {
       ProfScope ps(this, "precond");
       dim3 g(nblk);
-      if (p.xt_phase != 0) return fail(PDHG_ERR_UNSUPPORTED, "t-slab sweeps need the fp32 power-of-two x kernels");
       rc = with_xt_fft([&](auto f) {
         using F = decltype(f);
         int r2;

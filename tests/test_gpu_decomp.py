@@ -140,13 +140,15 @@ def test_multi_handle_is_not_a_context(native):
         m.close()
 
 
-def test_slab_eps_one_step_vs_oracle(native, parity_log):
+@pytest.mark.parametrize("egno", [2, 3])
+def test_slab_eps_one_step_vs_oracle(native, parity_log, egno):
     """epsl = 0.1 through the t-slab phases (4 slabs of 4 rows, fused residual off / on as selected, seeded
     rough state) for one iteration against the fp64 oracle: bounds as test_gpu_configs.test_one_step_eps --
-    the larger of the seeded-state bounds and K32 x the float32 oracle's own distance."""
+    the larger of the seeded-state bounds and K32 x the float32 oracle's own distance.  egno 3: bc (1, 0), the
+    DCT x transform's slab phases (jaxsrc/set_fns.py:96-111, utils/utils_precond.py:159-174)."""
     import torch
     from pdhg_amd.slab import LocalComm, SlabContext, SlabRunner, join_state, slab_bounds, split_state
-    egno, nx, ny, T, nr = 2, 512, 512, 16, 4
+    nx, ny, T, nr = 512, 512, 16, 4
     P = make_problem(egno, 2, nx, ny, T, 0.1, seeded=True)
     f = np.float32
     phi0, rho0 = P["phi"].astype(f).astype(np.float64), P["rho"].astype(f).astype(np.float64)
@@ -176,7 +178,7 @@ def test_slab_eps_one_step_vs_oracle(native, parity_log):
     for a in range(4):
         m["alp%d" % a] = rel(got[2][a], o[2][a])
         b["alp%d" % a] = max(1e-3, K32 * rel(p32[2][a], o[2][a]))
-    parity_log("test_slab_eps_one_step_vs_oracle", "512x512_T16_P4", m, b)
+    parity_log("test_slab_eps_one_step_vs_oracle", "e{}_512x512_T16_P4".format(egno), m, b)
     assert all(m[k] <= b[k] for k in m), (m, b)
 
 

@@ -17,6 +17,7 @@ CASES = [
     (2, 512, 256, 40, 4, 1),     # 10-row slabs: neighbour-only carries for the short-range modes
     (1, 512, 256, 5, 5, 3),      # one-row slabs, dual sub-iterations with early exit
     (2, 4096, 256, 50, 2, 1),    # 25-row slabs: the LDS-DMA x transform
+    (3, 512, 256, 9, 3, 1),      # egno 3: bc (1, 0), the generic DCT x kernel's slab phases
 ]
 
 

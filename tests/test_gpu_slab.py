@@ -26,6 +26,10 @@ CASES = [
     (1, 512, 256, 3, 3, 1),     # one-row slabs: the halo row is the whole slab
     (2, 512, 256, 19, 2, 1),    # residual tiles of 8 rows + untiled remainder rows
     (2, 512, 256, 40, 4, 1),    # 10-row slabs: short-range modes take the neighbour-only carries
+    # egno 3 (bc (1, 0): DCT-II along x, utils_precond.py:159-174): the generic x kernel's slab phases
+    (3, 512, 256, 9, 3, 1),
+    (3, 384, 256, 12, 2, 2),    # non-power-of-two nx (runtime-radix plan), dual sub-iterations
+    (3, 4096, 256, 8, 2, 1),    # C3's x extent (B = 2 column blocks)
 ]
 
 
@@ -53,7 +57,9 @@ def test_slabs_match_single_context(native, egno, nx, ny, T, nr, k, overlap, exc
 
     slabs = _slabs(P, nr, k)
     for s in slabs:   # the x kernel the slab runs (see CASES)
-        if nx == 4096:
+        if egno == 3:
+            assert s.path_info("fast_xt") == 0   # the generic runtime-radix DCT kernel
+        elif nx == 4096:
             assert s.path_info("fast_xt") == (4 if s.T >= 4 else 1), (s.T, s.path_info("fast_xt"))
     for s, part in zip(slabs, split_state(P["phi"], P["rho"], P["alp"], slab_bounds(T, nr))):
         s.set_state(*part)
@@ -111,7 +117,7 @@ def test_slab_rejects_unsupported(native):
     from pdhg_amd import _native as N
     from pdhg_amd.slab import SlabContext
     P = make_problem(1, 2, 48, 40, 4, 0.0)
-    with pytest.raises(N.PDHGError):      # nx = 48: no fast x-transform kernel
+    with pytest.raises(N.PDHGError):      # ny = 40: no fast row kernel (the halo row split of the residual)
         SlabContext(0, 2, 4, 1, 48, 40, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"])
 
 
