@@ -199,8 +199,9 @@ def marching(args):
     fv = utils_precond.compute_Dxx_fft_fv(ndim, nsp, dsp, bc)
     fp, fd = S.make_update_fns(ndim, bc, rho_alp_iters=k, precision=args.precision)
     stats = []
+    nt_run = nt if not args.windows else min(nt, args.windows + 1)   # the first W windows (same dt)
     t0 = time.perf_counter()
-    results, errs = S.PDHG_multi_step(fp, fd, fns, g, x_arr, ndim, nt, nsp, dt, dsp, 70.0, time_step_per_PDHG=2,
+    results, errs = S.PDHG_multi_step(fp, fd, fns, g, x_arr, ndim, nt_run, nsp, dt, dsp, 70.0, time_step_per_PDHG=2,
                                       epsl=epsl, stepsz_param=0.1, fv=fv, n_ctrl=n_ctrl, N_maxiter=1000000,
                                       print_freq=10000, eps=1e-6, verbose=True, stats=stats)   # per-window progress lines
     wall = time.perf_counter() - t0
@@ -209,9 +210,11 @@ def marching(args):
     out = {"metric": "time to solution, window marching (T = 1 windows to eps 1e-6)", "value": wall, "unit": "s",
            "higher_is_better": False, "n_gpus": 1, "dtype": {"fp32": "f32", "fp64": "f64"}.get(args.precision),
            "config": {"workload": "egno{} ndim{} epsl{} nx={} ny={} nt={}: {} windows of T = 1, rho_alp_iters={}, "
-                                  "stepsz 0.1, eps 1e-6".format(egno, ndim, epsl, nx, ny, nt, nt - 1, k)},
+                                  "stepsz 0.1, eps 1e-6".format(egno, ndim, epsl, nx, ny, nt, nt_run - 1, k),
+                      "precision": args.precision},
            "windows": len(errs), "total_outer_iters": total, "max_iters_per_window": int(results[0][0]),
-           "iters_per_window_first10": per_window[:10], "ms_per_outer_iter": wall / max(1, total) * 1e3,
+           "iters_per_window_first10": per_window[:10], "iters_per_window": per_window,
+           "ms_per_outer_iter": wall / max(1, total) * 1e3,
            "stop_status_last_window": int(stats[-1]["status"]) if stats else None}
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_marching_baseline(args.config, k, total, min(16, os.cpu_count() or 1))
@@ -325,6 +328,8 @@ def main():
                     help="multi-GPU decomposition of the window (xslab also at N = 1: one slab through its phases)")
     ap.add_argument("--marching", action="store_true",
                     help="time to solution of the T = 1 window-marching default on the config's grid (one GPU)")
+    ap.add_argument("--windows", type=int, default=0,
+                    help="--marching: only the first W windows (0: all nt - 1)")
     ap.add_argument("--selftest", action="store_true",
                     help="launcher / process-group check only: no GPU work, prints the world size")
     args = ap.parse_args()

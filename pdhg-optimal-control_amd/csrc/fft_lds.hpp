@@ -541,8 +541,10 @@ __device__ __forceinline__ void hartley_padded(const C* Z, int n, int k, T& ha, 
   hb = (T)0.5 * ((z.y + w.y) - (w.x - z.x));
 }
 
-// FFT policies used as kernel template arguments.
+// FFT policies used as kernel template arguments.  kPadded: the line lives in LDS in the padded in-place layout
+// (element e at pix(e)) instead of linearly.
 struct FFTRt {              // any n (mixed radix, runtime plan), nl interleaved lines
+  static constexpr bool kPadded = false;
   FFTPlan pl;
   int nl;
   template <typename C>
@@ -553,6 +555,7 @@ struct FFTRt {              // any n (mixed radix, runtime plan), nl interleaved
   __device__ __forceinline__ int lines() const { return nl; }
 };
 struct FFTGlb {             // any n, line buffers in global scratch (slot per workgroup): lines beyond LDS
+  static constexpr bool kPadded = false;
   FFTPlan pl;
   int nl;
   template <typename C>
@@ -567,6 +570,7 @@ struct FFTGlb {             // any n, line buffers in global scratch (slot per w
 
 template <int N, int NL>
 struct FFTFx {              // compile-time power-of-two n, NL lines
+  static constexpr bool kPadded = false;
   template <typename C>
   __device__ __forceinline__ C* buffer(C* lds, C*, int) const { return lds; }
   template <typename C>
@@ -576,6 +580,25 @@ struct FFTFx {              // compile-time power-of-two n, NL lines
   __device__ __forceinline__ int n() const { return N; }
   __device__ __forceinline__ int lines() const { return NL; }
 };
+
+// compile-time power-of-two N, ONE line transformed in place in the padded layout with NT threads (global twiddle
+// table): rows whose Stockham ping-pong (2 lines) does not fit LDS -- fp64 ny = 8192 (C4's y extent), 136 KiB
+template <int N, int NT>
+struct FFTIp {
+  static constexpr bool kPadded = true;
+  template <typename C>
+  __device__ __forceinline__ C* buffer(C* lds, C*, int) const { return lds; }
+  template <typename C>
+  __device__ __forceinline__ C* run(C* a, C*, const C* __restrict__ tw) const {
+    lds_fft_inplace<C, N, 1, NT>(a, tw);
+    return a;
+  }
+  __device__ __forceinline__ int n() const { return N; }
+  __device__ __forceinline__ int lines() const { return 1; }
+};
+// position of element e of a one-line buffer under policy F, and the Hartley pair of its transform
+template <class F>
+__device__ __forceinline__ int fpos(int e) { return F::kPadded ? pix(e) : e; }
 
 // Hartley unpack of line l at frequency k from the FFT Z of z = a + i b.
 // DCT-II (scipy norm=None: y_k = 2 sum x_n cos(pi k (2n+1) / 2n)) of two real columns a, b that were
@@ -601,6 +624,12 @@ __device__ __forceinline__ void hartley_pair(const C* Z, int n, int nl, int k, i
   const C w = Z[(size_t)km * nl + l];
   ha = (T)0.5 * ((z.x + w.x) - (z.y - w.y));
   hb = (T)0.5 * ((z.y + w.y) - (w.x - z.x));
+}
+// the Hartley pair of a one-line buffer under policy F (linear or padded)
+template <class F, typename C, typename T>
+__device__ __forceinline__ void hartley_line(const C* Z, int n, int k, T& ha, T& hb) {
+  if constexpr (F::kPadded) hartley_padded<C, T>(Z, n, k, ha, hb);
+  else hartley_pair<C, T>(Z, n, 1, k, 0, ha, hb);
 }
 
 }  // namespace pdhg

@@ -111,14 +111,14 @@ __global__ void __launch_bounds__(NTB) k_res_fwdy_2d(KP<R> p, F ply, const cplx<
   for (int y = threadIdx.x; y < ny; y += blockDim.x) {
     const R r0 = cont_residual_2d<R, EGNO>(p, rho, alp, j, x0, y);
     const R r1 = has2 ? cont_residual_2d<R, EGNO>(p, rho, alp, j, x0 + 1, y) : (R)0;
-    A[y] = cmk<C>(r0, r1);
+    A[fpos<F>(y)] = cmk<C>(r0, r1);
   }
   __syncthreads();
   const C* Z = ply.template run<C>(A, Bf, twy);
   const int ncol = nb * B;
   for (int ky = threadIdx.x; ky < ncol; ky += blockDim.x) {
     R ha = (R)0, hb = (R)0;
-    if (ky < ny) hartley_pair<C, R>(Z, ny, 1, ky, 0, ha, hb);
+    if (ky < ny) hartley_line<F, C, R>(Z, ny, ky, ha, hb);
     const int b = ky >> p.lB, c = ky & (B - 1);
     R* dst = wk + ((size_t)b * nx + x0) * B + c;
     dst[0] = ha;
@@ -350,13 +350,13 @@ __global__ void __launch_bounds__(NTB) k_invy_update_2d(KP<R> p, F ply, const cp
     for (int ky = threadIdx.x; ky < ny; ky += blockDim.x) {
       const int b = ky >> p.lB, c = ky & (B - 1);
       const R* srcp = wk + ((size_t)b * nx + x0) * B + c;
-      A[ky] = cmk<C>(srcp[0], has2 ? srcp[B] : (R)0);
+      A[fpos<F>(ky)] = cmk<C>(srcp[0], has2 ? srcp[B] : (R)0);
     }
     __syncthreads();
     const C* Z = ply.template run<C>(A, Bf, twy);
     for (int y = threadIdx.x; y < ny; y += blockDim.x) {
       R u0, u1;
-      hartley_pair<C, R>(Z, ny, 1, y, 0, u0, u1);
+      hartley_line<F, C, R>(Z, ny, y, u0, u1);
       for (int r = 0; r < 2; ++r) {
         if (r == 1 && !has2) break;
         const size_t idx = (size_t)(x0 + r) * ny + y;

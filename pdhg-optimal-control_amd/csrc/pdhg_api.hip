@@ -134,6 +134,7 @@ struct Impl : ImplBase {
   // fast row kernels (fp32, power-of-two ny): RW rows per workgroup, NTf threads
   bool fast_rows = false;
   bool glb_line = false;          // 1-D line FFTs over global scratch (nx beyond LDS)
+  bool ip_rows = false;           // fp64 ny = 8192: generic row kernels on one padded in-place line (FFTIp)
   bool fourstep = false;          // fp32 1-D nx = 65536: four-step DHT over 16 + 9 workgroups per row pair
   bool t1_xt = true;              // T = 1 windows: carry-free x transform (k_precond_x_t1_2d; env PDHG_T1_XT=0 off)
   C* tw256 = nullptr;             // W_256 table of the four-step stages
@@ -293,6 +294,10 @@ struct Impl : ImplBase {
       lds_res = 2 * (size_t)ny * csz;
       const int nmodes = nxg * B;
       lds_xt = (size_t)5 * nmodes * sizeof(R);
+      // fp64 ny = 8192 (C4's y extent in the reference's precision): the generic row kernels transform the row pair
+      // in place in one padded line (FFTIp, 136 KiB) instead of a Stockham ping-pong of two (256 KiB)
+      ip_rows = sizeof(R) == 8 && ny == 8192 && lds_res > kLdsBytes && !xslab && !slab;
+      if (ip_rows) lds_res = (size_t)Pad<8192>::LINE * csz;
       if (lds_res > kLdsBytes) return fail(PDHG_ERR_UNSUPPORTED, "ny=%d exceeds the LDS row transform", ny);
       {   // generic row kernels: when the LDS admits few workgroups per CU (fp64 ny = 4096: one), wider
           // workgroups keep >= 16 waves per CU in flight for the residual's scattered loads
@@ -623,6 +628,9 @@ struct Impl : ImplBase {
   template <typename Fn>
   int with_line_fft(const FFTPlan& pl, Fn&& fn) {
     if (glb_line) return fn(FFTGlb{pl, 1});   // 1-D lines beyond LDS
+    if constexpr (sizeof(R) == 8) {
+      if (ip_rows && &pl == &ply) return fn(FFTIp<8192, 1024>{});   // the row kernels' 1024 threads (nt_row)
+    }
     if constexpr (sizeof(R) == 4) {
       if (pl.pow2) {
         switch (pl.n) {
@@ -2144,6 +2152,7 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
     else if (k == "half_real") *value = im.half_real ? 1 : 0;
     else if (k == "fourstep") *value = im.fourstep ? 1 : 0;
     else if (k == "glb_line") *value = im.glb_line ? 1 : 0;
+    else if (k == "ip_rows") *value = im.ip_rows ? 1 : 0;   // fp64 ny = 8192 row pairs in one padded line
     else if (k == "thomas_chunk") *value = im.thomas_chunk ? 1 : 0;
     else if (k == "fs_wide") *value = (im.fourstep && im.fs_wide && !im.fs16) ? 1 : 0;
     else if (k == "fs16") *value = im.fs16 ? 1 : 0;

@@ -27,6 +27,11 @@ iterations and reaches a NaN long before float64 does.
 
 Run:  python tests/golden/make_divergence_fixture.py [T] [max_iters] [f32]   (~2.5 min per iteration at T = 4, 6 cores)
 
+Perturbed pointwise variant (argument "points_ulp"): the same run from phi_0 multiplied by (1 + u), u = +-2^-52 with
+random signs (np.random.default_rng(7)), at the same sample points -> divergence_c3_plane_T4_points_ulp.npz.  Its
+distance to the "points" fixture is how far two float64 runs of the reference algorithm that differ by one rounding
+drift apart through the instability: the spread any float64 implementation has against the oracle pointwise.
+
 Pointwise variant (argument "points"): the float64 oracle's phi' and rho' at NPTS fixed sample points of the plane
 (rows 1..T of phi', every row of rho'; indices from np.random.default_rng(20250117)) after each of the first
 max_iters iterations -> divergence_c3_plane_T{T}_points.npz.  tests/test_gpu_divergence.py compares the fp64
@@ -130,12 +135,17 @@ if __name__ == "__main__":
     T = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     max_iters = int(sys.argv[2]) if len(sys.argv) > 2 else 24
     f32 = len(sys.argv) > 3 and sys.argv[3] == "f32"   # the float32 oracle (until its first NaN)
-    points = len(sys.argv) > 3 and sys.argv[3] == "points"
+    points = len(sys.argv) > 3 and sys.argv[3] in ("points", "points_ulp")
+    ulp = len(sys.argv) > 3 and sys.argv[3] == "points_ulp"
     nx = ny = 4096
     S = setup(nx, ny, T, 1.0 / 200, 0.1, np.float32 if f32 else np.float64)
-    out = os.path.join(HERE, "divergence_c3_plane_T{}{}.npz".format(T, "_f32" if f32 else "_points" if points else ""))
+    out = os.path.join(HERE, "divergence_c3_plane_T{}{}.npz".format(
+        T, "_f32" if f32 else "_points_ulp" if ulp else "_points" if points else ""))
     if points:
         S.update(points=sample_points(T, nx, ny), phi_pts=[], rho_pts=[])
+    if ulp:
+        sgn = np.where(np.random.default_rng(7).random(S["phi"].shape) < 0.5, -1.0, 1.0)
+        S["phi"] = S["phi"] * (1.0 + sgn * 2.0 ** -52)
     S["out"] = out            # rewritten after every iteration (a partial run is usable)
     rows, first = run(S, max_iters)
     save(out, rows, first, S)

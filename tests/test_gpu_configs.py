@@ -310,7 +310,8 @@ def test_chunked_thomas_matches_one_thread_per_mode(native, monkeypatch, nx, T, 
 # north-star 1e-5 on phi, rho and every control, and the fp64 bar 1e-9 on phi / rho (the device and the oracle run
 # the same float64 algorithm from the same state; measured ~1e-13).  The fp64 kernels at each fixture's shape are
 # asserted through pdhg_path_info (k_precond_xt_f64_2d at nx = 4096 and its half-real form at C4's nx = 8192, the
-# 4-row fast row kernels at ny = 2048 / 4096, the time-marching dual).  C4's ny = 8192 rows are fp32-only so far.
+# 4-row fast row kernels at ny = 2048 / 4096, the generic row kernels on one padded in-place line at C4's ny = 8192,
+# the time-marching dual).
 FP64_CASES = {
     "c3_ws_T200": {"f64_xt": 1},
     "c3_fr_4096x256": {"f64_xt": 1, "dual64": 1},
@@ -319,6 +320,7 @@ FP64_CASES = {
     "c2_rows_ny2048": {"res64": 1, "dual64": 1},
     "c1_exact": {"glb_line": 1},
     "c4_halfreal_x8192": {"f64_xt": 1, "half_real": 1, "dual64": 1},   # k_precond_xt_f64_2d<4096, 512, HR>
+    "c4_rows_ny8192": {"ip_rows": 1, "dual64": 1},   # row pairs transformed in one padded in-place line (FFTIp)
 }
 FP64_BAR = 1e-9
 
