@@ -81,6 +81,7 @@ __global__ void __launch_bounds__(1024) k_precond_xt_dma_2d(KP<float> p, const f
   __shared__ float lxs[N];                   // lamx per item: dd is recomputed per row (8 VGPRs fewer)
   fill_twlds<C, N>(twl, twx);
   for (int i = threadIdx.x; i < N; i += NT) lxs[i] = p.lamx[i];
+  __syncthreads();   // lxs (read by the converged-pivot rows below)
   const int T = p.T, tid = threadIdx.x;
   // the wave index in an SGPR and the lane from mbcnt: the laundered thread index costs no VGPR between uses
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -118,7 +119,23 @@ __global__ void __launch_bounds__(1024) k_precond_xt_dma_2d(KP<float> p, const f
                                          16, 0, 0);
     }
   };
-  C c1[IT], c2[IT], c3[IT];     // theta (backward),  h | E,  b' | x
+  C c1[IT], c2[IT], c3[IT];     // theta (backward),  h | e^-th once converged (forward) | E | e^-th (backward),  b' | x
+  // Converged pivots (kernels_xt_f64.hpp): g_k = e^-th E_{k+1}/E_{k+2} is e^-th to within 2^-26 once th (k+1) > 9
+  // in every lane of the wave; kf[i] = the first such global row for item i (wave-uniform, SGPRs).  From it on the
+  // forward step multiplies by e^-th (no reciprocal) and the backward step needs no expm1 / exp / reciprocal.
+  int kf[IT];
+  launder();
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const float2 dd = dd_of(item_of(i));
+    const float dl0 = 0.5f * dd.x, dl1 = 0.5f * dd.y;
+    float tm = fminf(log1pf(dl0 + sqrtf(dl0 * (dl0 + 2.f))), log1pf(dl1 + sqrtf(dl1 * (dl1 + 2.f))));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tm = fminf(tm, __shfl_xor(tm, o, kWave));
+    const float q = 9.f / fmaxf(tm, 1e-20f);
+    kf[i] = __builtin_amdgcn_readfirstlane(q < 1e9f ? (int)q : 1000000000);
+  }
+  auto eth = [](float d) { return 1.f / (1.f + 0.5f * d + sqrtf(d * (1.f + 0.25f * d))); };   // e^-th
 
   // Waits.  A batch with both rows stored ("full") issues exactly 4 stores after the DMA of the next rows,
   // so vmcnt(4) retires that DMA; an edge batch waits vmcnt(0).  The waits are builtins, so the compiler's
@@ -170,16 +187,25 @@ __global__ void __launch_bounds__(1024) k_precond_xt_dma_2d(KP<float> p, const f
         const int k = k0 + r;
         if (!FULL && k >= T) break;
         C* dst = row_ptr(k);
+        const int kg = p.j0 + k;   // global row
         if (FULL || k < T - 1 || !p.last_slab) {
 #pragma unroll
           for (int i = 0; i < IT; ++i) {
             float ha, hb;
             hartley_padded<C, float>(A + r * LINE, N, item_of(i), ha, hb);
-            const float2 dd = dd_of(item_of(i));
-            const float s0 = dd.x + c2[i].x, s1 = dd.y + c2[i].y;
-            const float g0 = rcp_fast(1.f + s0), g1 = rcp_fast(1.f + s1);
-            c3[i] = make_float2((ha * inv_ae + c3[i].x) * g0, (hb * inv_ae + c3[i].y) * g1);
-            c2[i] = make_float2(s0 * g0, s1 * g1);
+            if (kg >= kf[i]) {   // converged: g = e^-th (in c2 from row kf on: h is no longer needed)
+              if (kg == max(kf[i], p.j0)) {   // the first converged row of this sweep (a slab may start past kf)
+                const float2 dd = dd_of(item_of(i));
+                c2[i] = make_float2(eth(dd.x), eth(dd.y));
+              }
+              c3[i] = make_float2((ha * inv_ae + c3[i].x) * c2[i].x, (hb * inv_ae + c3[i].y) * c2[i].y);
+            } else {
+              const float2 dd = dd_of(item_of(i));
+              const float s0 = dd.x + c2[i].x, s1 = dd.y + c2[i].y;
+              const float g0 = rcp_fast(1.f + s0), g1 = rcp_fast(1.f + s1);
+              c3[i] = make_float2((ha * inv_ae + c3[i].x) * g0, (hb * inv_ae + c3[i].y) * g1);
+              c2[i] = make_float2(s0 * g0, s1 * g1);
+            }
           }
 #pragma unroll
           for (int j = 0; j < IT / 2; ++j) st_pair(dst, j, c3[2 * j], c3[2 * j + 1]);
@@ -189,7 +215,12 @@ __global__ void __launch_bounds__(1024) k_precond_xt_dma_2d(KP<float> p, const f
             float ha, hb;
             hartley_padded<C, float>(A + r * LINE, N, item_of(i), ha, hb);
             const float2 dd = dd_of(item_of(i));
-            c3[i] = make_float2((ha * inv_ae + c3[i].x) / (dd.x + c2[i].x), (hb * inv_ae + c3[i].y) / (dd.y + c2[i].y));
+            if (max(kf[i], p.j0) < kg) {   // converged on an earlier row: dd + h = (1 - g) / g
+              const float2 g = c2[i];
+              c3[i] = make_float2((ha * inv_ae + c3[i].x) * g.x / (1.f - g.x), (hb * inv_ae + c3[i].y) * g.y / (1.f - g.y));
+            } else {
+              c3[i] = make_float2((ha * inv_ae + c3[i].x) / (dd.x + c2[i].x), (hb * inv_ae + c3[i].y) / (dd.y + c2[i].y));
+            }
           }
           if (p.slab) {   // re-read (after the carry fix-up) by the backward sweep
 #pragma unroll
@@ -232,9 +263,11 @@ __global__ void __launch_bounds__(1024) k_precond_xt_dma_2d(KP<float> p, const f
     const float dl0 = 0.5f * dd.x, dl1 = 0.5f * dd.y;
     c1[i] = make_float2(fmaxf(log1pf(dl0 + sqrtf(dl0 * (dl0 + 2.f))), 1e-20f),
                         fmaxf(log1pf(dl1 + sqrtf(dl1 * (dl1 + 2.f))), 1e-20f));
-    // E_{k+2} for the first substituted row: k = T-2 (single context) or T-1 (slab, from the right carry)
+    // E_{k+2} for the first substituted row: k = T-2 (single context) or T-1 (slab, from the right carry);
+    // e^-th instead when that row is already converged
     const float e0 = (float)(p.j0 + T + (p.slab ? 1 : 0));
-    c2[i] = make_float2(expm1f(-2.f * c1[i].x * e0), expm1f(-2.f * c1[i].y * e0));
+    if (p.j0 + T - (p.slab ? 1 : 2) >= kf[i]) c2[i] = make_float2(__expf(-c1[i].x), __expf(-c1[i].y));
+    else c2[i] = make_float2(expm1f(-2.f * c1[i].x * e0), expm1f(-2.f * c1[i].y * e0));
     if (p.slab)
       c3[i] = p.carry_y ? reinterpret_cast<const C*>(p.carry_y + (size_t)b * M)[item_of(i)] : make_float2(0.f, 0.f);
   }
@@ -253,11 +286,18 @@ __global__ void __launch_bounds__(1024) k_precond_xt_dma_2d(KP<float> p, const f
       const int k = kt - r;
       if (k < 0) break;
       if ((k < T - 1 || p.slab) && !(p.dbg & 4)) {
-        const float kk1 = (float)(p.j0 + k + 1);   // global row index + 1
+        const int kg = p.j0 + k;
+        const float kk1 = (float)(kg + 1);   // global row index + 1
 #pragma unroll
         for (int i = 0; i < IT; ++i) {
-          // theta >= 1e-20 (clamped above): the closed form tends to (k+1)/(k+2) as theta -> 0
           const C bp = bpv[r][i];
+          if (kg >= kf[i]) {   // converged: g = e^-th (c2)
+            c3[i] = make_float2(bp.x + c2[i].x * c3[i].x, bp.y + c2[i].y * c3[i].y);
+            continue;
+          }
+          if (kg + 1 == kf[i])   // first unconverged row below the converged ones: E_{k+2} from theta
+            c2[i] = make_float2(expm1f(-2.f * c1[i].x * (kk1 + 1.f)), expm1f(-2.f * c1[i].y * (kk1 + 1.f)));
+          // theta >= 1e-20 (clamped above): the closed form tends to (k+1)/(k+2) as theta -> 0
           const float2 E1 = expm1_neg2(-2.f * c1[i].x * kk1, -2.f * c1[i].y * kk1);
           const float g0 = __expf(-c1[i].x) * E1.x * rcp_fast(c2[i].x);
           const float g1 = __expf(-c1[i].y) * E1.y * rcp_fast(c2[i].y);
