@@ -145,7 +145,8 @@ int pdhg_device_bytes(pdhg_ctx* ctx, unsigned long long* bytes);
 /* Which kernel variant a context selected (no reference counterpart; tests and benches assert the fast
  * paths engaged): "fused_residual" 1/0 (the dual sweep forms the next residual, k_dual_lds_2d FR),
  * "fast_rows" 1/0 (fp32 8/4-row y-transform kernels), "fast_dual" (-1 generic, 0 row-per-thread,
- * RX rows through LDS), "fast_xt" (0 generic, 1 single-role, 2 warp-specialised, 3 row-batched,
+ * RX rows through LDS), "dual_ypl" (y per lane of the LDS dual: 4, or 2 for fp64 with PDHG_DUAL_YPL=2;
+ * 0 without it), "fast_xt" (0 generic, 1 single-role, 2 warp-specialised, 3 row-batched,
  * 4 row-batched with LDS-DMA staging x-transform), "half_real", "fourstep", "fs16", "fs_wide",
  * "glb_line", "thomas_chunk", "rows_rw", "res_threads", "upd_threads",
  * "row_threads" (threads of the generic row kernels), "res64" 1/0 (fp64 residual and update through the

@@ -44,6 +44,26 @@ __device__ __forceinline__ void f4set(dbl4& v, int e, double x) {
 }
 template <typename R> __device__ __forceinline__ V4<R> z4r() { return z4(); }
 template <> __device__ __forceinline__ dbl4 z4r<double>() { return dbl4{0.0, 0.0, 0.0, 0.0}; }
+// YPL consecutive y per lane: 4 (float4 / dbl4) or 2 (float2 / double2, one 16-B access per lane in fp64)
+template <typename R, int YPL> struct VYs { using type = V4<R>; };
+template <typename R> struct VYs<R, 2> { using type = cplx<R>; };
+template <typename R, int YPL> using VY = typename VYs<R, YPL>::type;
+__device__ __forceinline__ float f4(const float2& v, int e) { return e == 0 ? v.x : v.y; }
+__device__ __forceinline__ double f4(const double2& v, int e) { return e == 0 ? v.x : v.y; }
+__device__ __forceinline__ void f4set(float2& v, int e, float x) { if (e == 0) v.x = x; else v.y = x; }
+__device__ __forceinline__ void f4set(double2& v, int e, double x) { if (e == 0) v.x = x; else v.y = x; }
+template <int YPL, typename R> __device__ __forceinline__ VY<R, YPL> ldy(const R* p) {
+  if constexpr (YPL == 4) return ld4(p);
+  else return *reinterpret_cast<const cplx<R>*>(p);
+}
+template <int YPL, typename R> __device__ __forceinline__ void sty(R* p, VY<R, YPL> v) {
+  if constexpr (YPL == 4) st4(p, v);
+  else *reinterpret_cast<cplx<R>*>(p) = v;
+}
+template <typename R, int YPL> __device__ __forceinline__ VY<R, YPL> zy() {
+  if constexpr (YPL == 4) return z4r<R>();
+  else return cmk<cplx<R>>((R)0, (R)0);
+}
 __device__ __forceinline__ float4 mk4(float a, float b, float c, float d) { return make_float4(a, b, c, d); }
 __device__ __forceinline__ dbl4 mk4(double a, double b, double c, double d) { return dbl4{a, b, c, d}; }
 // the float lane shifts (common.hpp) on the two halves of a double
@@ -318,20 +338,27 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<R> p, const cplx<R>*
 // row-group tasks.  The next task's rows are loaded into registers before the current FFT and its edge rows
 // after it, so the CU's memory pipe is not idle during the transform; its strip-edge terms (RW * ny/256 * 2
 // floats) go through a small LDS double buffer, so only the edge lanes read them.
-// grid: G <= T * nx/RW; block NT (N/4 % NT == 0); LDS RW/2 * (N + N/16) * 8 B (+ 2 * RW * ny/128 floats).
-template <int EGNO, int N, int RW, int NT>
-__global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const float2* __restrict__ twy) {
-  using C = float2;
+// fp64 (R = double): the sweep's strips are 128 columns wide (k_dual_lds_2d<.., double, YPL = 2>) and 4 rows of
+// complex double fill the LDS, so a task is half a sweep tile (RW = 4, NH = 2): the first half adds row x0's
+// p.ex term, the second row x0+RW-1's.
+// grid: G <= T * nx/RW; block NT (N/4 % NT == 0); LDS RW/2 * (N + N/16) * sizeof(C) (+ 2 * RW * N/YW reals).
+template <int EGNO, int N, int RW, int NT, typename R = float>
+__global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<R> p, const cplx<R>* __restrict__ twy) {
+  using C = cplx<R>;
+  using V = V4<R>;
+  constexpr int TH = 8;                  // tile height of the sweep (k_dual_lds_2d RX)
+  constexpr int NH = TH / RW;            // tasks per sweep tile
   constexpr int NL = RW / 2;
   constexpr int LN = Pad<N>::LINE;
   constexpr int GPT = (N / 4) / NT;
-  constexpr int YW = 256, NSTRIP = N / YW;
+  constexpr int YW = sizeof(R) == 4 ? 256 : 128, NSTRIP = N / YW;
   constexpr int NEY = RW * NSTRIP * 2;   // strip-edge terms of one task
-  static_assert(RW == 8 && N % YW == 0 && (N / 4) % NT == 0, "fused residual tiles are 8 rows x 256 columns");
+  static_assert((sizeof(R) == 4 ? RW == 8 : RW == 4) && N % YW == 0 && (N / 4) % NT == 0,
+                "fused residual tasks: 8 (fp32) / 4 (fp64) rows of the sweep's 8-row x YW-column tiles");
   static_assert(NEY <= NT, "one strip-edge term per thread");
   if (p.ctrl->done) return;
   extern __shared__ __align__(16) unsigned char smem_raw[];
-  __shared__ float eyl[2][NEY];
+  __shared__ R eyl[2][NEY];
   C* A = reinterpret_cast<C*>(smem_raw);
   // twiddle seeds in LDS behind the lines (N <= 4096): the passes then issue no global loads, so the next
   // task's rows stay in flight across the whole transform (vmcnt drains in order)
@@ -347,15 +374,15 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
   const int lCS4 = p.lB + (RW == 8 ? 1 : RW == 4 ? 0 : RW == 2 ? -1 : -2);   // log2(CS4), B power of two
   const int nb = p.nb;
   const int tid = threadIdx.x;
-  float4 rows[GPT][RW];        // next task's residual rows x0 .. x0+RW-1
-  float4 e0[GPT], e1[GPT];     // next task's edge-row terms (row x0, row x0+RW-1)
-  float ev = 0.f;              // next task's strip-edge term number tid
+  V rows[GPT][RW];             // next task's residual rows x0 .. x0+RW-1
+  V e0[GPT], e1[NH == 1 ? GPT : 1];   // next task's edge-row terms (row x0, row x0+RW-1; NH = 2: the half's one)
+  R ev = (R)0;                 // next task's strip-edge term number tid
   // rows [r0, r1) of a task (NT = 1024: half before the transform, half after, so that only 4 rows of
   // loads are live across the FFT's registers)
   auto load_rows = [&](int task, int r0, int r1) {
     const int jt = task / ngx, j = p.row_base + jt, x0 = (task - jt * ngx) * RW;
     if (r0 == 0 && tid < NEY) ev = p.ey[((size_t)j * nx + x0) * NSTRIP * 2 + tid];   // first: waited for alone
-    const float* R0 = p.res + (size_t)j * plane + (size_t)x0 * N;
+    const R* R0 = p.res + (size_t)j * plane + (size_t)x0 * N;
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
       const int y = 4 * (tid + gi * NT);
@@ -366,13 +393,17 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
   };
   constexpr int RSPLIT = (NT >= 1024) ? RW / 2 : RW;
   auto load_edges = [&](int task) {
-    const int jt = task / ngx, j = p.row_base + jt, tile = task - jt * ngx;
-    const float* E = p.ex + ((size_t)j * ngx + tile) * 2 * N;
+    const int jt = task / ngx, j = p.row_base + jt, tk = task - jt * ngx, tile = tk / NH;
+    const R* E = p.ex + ((size_t)j * (ngx / NH) + tile) * 2 * N;
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
       const int y = 4 * (tid + gi * NT);
-      e0[gi] = ld4(E + y);
-      e1[gi] = ld4(E + N + y);
+      if constexpr (NH == 1) {
+        e0[gi] = ld4(E + y);
+        e1[gi] = ld4(E + N + y);
+      } else {
+        e0[gi] = ld4(E + ((tk & 1) ? N : 0) + y);
+      }
     }
   };
   int task = blockIdx.x, buf = 0;
@@ -390,22 +421,30 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
       const int y = 4 * (tid + gi * NT);
-      float4 v[RW];
+      V v[RW];
 #pragma unroll
       for (int r = 0; r < RW; ++r) v[r] = rows[gi][r];
       if (hal) {
-        const float* rl = p.rho[p.ctrl->cur] + (size_t)j * plane + (size_t)x0 * N;
+        const R* rl = p.rho[p.ctrl->cur] + (size_t)j * plane + (size_t)x0 * N;
 #pragma unroll
         for (int r = 0; r < RW; ++r) {
-          const float4 hv = ld4(p.rho_halo + (size_t)(x0 + r) * N + y), rv = ld4(rl + (size_t)r * N + y);
+          const V hv = ld4(p.rho_halo + (size_t)(x0 + r) * N + y), rv = ld4(rl + (size_t)r * N + y);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) f4set(v[r], e, __builtin_fmaf(f4(hv, e) - f4(rv, e), p.inv_dt, f4(v[r], e)));
+          for (int e = 0; e < 4; ++e) f4set(v[r], e, fmar(f4(hv, e) - f4(rv, e), p.inv_dt, f4(v[r], e)));
         }
       }
+      if constexpr (NH == 1) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        f4set(v[0], e, f4(v[0], e) + f4(e0[gi], e));
-        f4set(v[RW - 1], e, f4(v[RW - 1], e) + f4(e1[gi], e));
+        for (int e = 0; e < 4; ++e) {
+          f4set(v[0], e, f4(v[0], e) + f4(e0[gi], e));
+          f4set(v[RW - 1], e, f4(v[RW - 1], e) + f4(e1[gi], e));
+        }
+      } else if (((task - jt * ngx) & 1) == 0) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) f4set(v[0], e, f4(v[0], e) + f4(e0[gi], e));
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) f4set(v[RW - 1], e, f4(v[RW - 1], e) + f4(e0[gi], e));
       }
       const int s = y / YW, yo = y - s * YW;
       if (yo == 0) {
@@ -419,7 +458,7 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
       for (int l = 0; l < RW / 2; ++l) {   // rows 2l, 2l+1 -> line l (real, imaginary): one 8-B LDS store each
         C* Al = A + l * LN + pix(y);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) Al[e] = make_float2(f4(v[2 * l], e), f4(v[2 * l + 1], e));
+        for (int e = 0; e < 4; ++e) Al[e] = cmk<C>(f4(v[2 * l], e), f4(v[2 * l + 1], e));
       }
     }
     // the next task's loads are unconditional (the last task re-loads its own rows): a conditional load
@@ -434,10 +473,10 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<float> p, const flo
     if (tid < NEY) eyl[buf ^ 1][tid] = ev;   // read one barrier after its last use two tasks ago
     if constexpr (RSPLIT < RW) load_rows(nxt, RSPLIT, RW);
     load_edges(nxt);
-    float* wk = p.work + (size_t)j * nb * nx * B;
+    R* wk = p.work + (size_t)j * nb * nx * B;
     for (int t = tid; t < nb * CS4 && !(p.dbg & 32); t += NT) {   // PDHG_DBG 32: no unpack / stores (timing)
       const int b = t >> lCS4, part = t & (CS4 - 1);
-      const float4 v = unpack_chunk4<N, LN>(A, b, part, B, p.lB);
+      const V v = unpack_chunk4<N, LN, R>(A, b, part, B, p.lB);
       if (p.dbg & 512) st4(wk + (size_t)x0 * N + 4 * t, v);   // PDHG_DBG 512: task-contiguous stores (timing)
       else st4(wk + ((size_t)b * nx + x0) * B + part * 4, v);
     }

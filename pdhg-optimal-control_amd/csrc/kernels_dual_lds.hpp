@@ -25,19 +25,19 @@ namespace pdhg {
 // edge rows / columns contribute to the neighbouring tiles (p.ex: eps rho'/dx^2 + m1x/dx of row x0+RX-1
 // for the next tile's first row, eps rho'/dx^2 - m2x/dx of row x0 for the previous tile's last row;
 // p.ey: likewise per strip-edge column with m1y / m2y), and k_res_fwdy_fused_2d adds them.
-template <int EGNO, int RX, bool FR = false, typename R = float>
+template <int EGNO, int RX, bool FR = false, typename R = float, int YPL = 4>
 __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<R> p, int jchunk, int jbase, int jend,
                                                                      int zbase) {
-  using V = V4<R>;
+  using V = VY<R, YPL>;   // YPL consecutive y per lane
   if (p.ctrl->done || p.ctrl->inner_done) return;
   constexpr int NA = (EGNO == 3) ? 2 : 4;
   constexpr int NS = 3 + 3 * NA;
-  constexpr int YW = 256;                         // y strip per workgroup (64 lanes x float4)
+  constexpr int YW = 64 * YPL;                    // y strip per workgroup (64 lanes x YPL)
   static_assert(!FR || EGNO != 3, "fused residual: egno 1/2 (four live controls)");
-  static_assert(!FR || sizeof(R) == 4, "fused residual: fp32 (the fp64 sweep runs the residual kernel)");
-  __shared__ __align__(16) V strip[2][RX + 2][YW / 4];
+  static_assert(YPL == 4 || YPL == 2, "4 or 2 y per lane");
+  __shared__ __align__(16) V strip[2][RX + 2][64];
   // FR: [buffer][row][rho', m1x, m2x][lane]
-  __shared__ __align__(16) V flux[FR ? 2 : 1][FR ? RX : 1][3][YW / 4];
+  __shared__ __align__(16) V flux[FR ? 2 : 1][FR ? RX : 1][3][64];
   const int cur = p.ctrl->cur;
   const int src_set = (p.inplace || p.sub == 0) ? cur : 1 - cur;
   const int dst_set = p.inplace ? cur : 1 - cur;
@@ -47,7 +47,7 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<R> p, int jchunk,
   const int x0 = xcd_remap(blockIdx.x, gridDim.x) * RX;
   const int x = x0 + r;
   const bool live = x >= p.xl0 && x < p.xl1;   // wave-uniform (x-slab ghost / padding rows: neither stored nor summed)
-  const int y = blockIdx.y * YW + 4 * lane;
+  const int y = blockIdx.y * YW + YPL * lane;
   const int j0 = jbase + blockIdx.z * jchunk;
   const int j1 = min(jend, j0 + jchunk);
   double s[NS];
@@ -61,10 +61,10 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<R> p, int jchunk,
   const size_t rxh = (size_t)(zh ? x : xh) * ny, rxc = (size_t)x * ny;
   const int hslot = (r == 0) ? 0 : RX + 1;
   const int yw0 = __builtin_amdgcn_readfirstlane(y);
-  const int ywm = nb_index(yw0 - 1, ny, p.bcy), ywp = nb_index(yw0 + 4 * kWave, ny, p.bcy);
+  const int ywm = nb_index(yw0 - 1, ny, p.bcy), ywp = nb_index(yw0 + YPL * kWave, ny, p.bcy);
   const bool zym = ywm < 0, zyp = ywp < 0;
   const int ywmc = zym ? 0 : ywm, ywpc = zyp ? 0 : ywp;
-  const V ay4 = ld4(p.ay + y);
+  const V ay4 = ldy<YPL>(p.ay + y);
   const R axc = p.ax[x];
   const R* rs = p.rho[src_set];
   R* rd = p.rho[dst_set];
@@ -82,23 +82,25 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<R> p, int jchunk,
   auto load = [&](int j) {
     In in;
     const R* f1 = p.phibar + (size_t)(j + 1) * plane;
-    in.pc = ld4(f1 + rxc + y);
-    in.ph = has_h ? ld4(f1 + rxh + y) : z4r<R>();
+    in.pc = ldy<YPL>(f1 + rxc + y);
+    in.ph = has_h ? ldy<YPL>(f1 + rxh + y) : zy<R, YPL>();
     in.el = f1[rxc + ywmc];
     in.er = f1[rxc + ywpc];
     const size_t o = (size_t)j * plane + rxc + y;
-    in.rho = ld4(rs + o);
+    in.rho = ldy<YPL>(rs + o);
 #pragma unroll
-    for (int a = 0; a < NA; ++a) in.al[a] = ld4(as[a] + o);
+    for (int a = 0; a < NA; ++a) in.al[a] = ldy<YPL>(as[a] + o);
     return in;
   };
   auto stage = [&](const In& in, int buf) {
     strip[buf][r + 1][lane] = in.pc;
-    if (has_h) strip[buf][hslot][lane] = zh ? z4r<R>() : in.ph;
+    if (has_h) strip[buf][hslot][lane] = zh ? zy<R, YPL>() : in.ph;
   };
   // FR state: the y part of row j-1's residual (eps*Dyy rho' and the y flux divergence), completed at
   // step j once rho'_j and the x neighbours' fluxes (LDS) are known
-  R yeps[4] = {(R)0, (R)0, (R)0, (R)0}, ydiv[4] = {(R)0, (R)0, (R)0, (R)0};
+  R yeps[YPL], ydiv[YPL];
+#pragma unroll
+  for (int e = 0; e < YPL; ++e) yeps[e] = ydiv[e] = (R)0;
   const bool use_eps = p.epsl != (R)0;
   const int nstrip = ny / YW;
   // R_{jr} (row jr of the next residual) = (rho'_{jr+1} - rho'_{jr})/dt + eps*Lap rho' - div m, from the
@@ -112,11 +114,11 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<R> p, int jchunk,
     const int rmi = r > 0 ? r - 1 : r, rpi = r < RX - 1 ? r + 1 : r;   // wave-uniform
     V rm = flux[fb][rmi][0][lane], m1m = flux[fb][rmi][1][lane];
     V rp = flux[fb][rpi][0][lane], m2p = flux[fb][rpi][2][lane];
-    if (r == 0) rm = m1m = z4r<R>();        // row x0-1: added by the residual kernel
-    if (r == RX - 1) rp = m2p = z4r<R>();   // row x0+RX: likewise
+    if (r == 0) rm = m1m = zy<R, YPL>();        // row x0-1: added by the residual kernel
+    if (r == RX - 1) rp = m2p = zy<R, YPL>();   // row x0+RX: likewise
     V out;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
+    for (int e = 0; e < YPL; ++e) {
       const R r0 = f4(rc, e);
       R res = (R)0;
       if (use_eps) {
@@ -127,10 +129,10 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<R> p, int jchunk,
       const R other = res - div + cdt;
       f4set(out, e, tdiff ? fmar(f4(rnext, e) - r0, p.inv_dt, other) : other);
     }
-    st4(p.res + (size_t)jr * plane + rxc + y, out);
+    sty<YPL>(p.res + (size_t)jr * plane + rxc + y, out);
   };
   if (j0 < j1) {
-    V f0 = ld4(p.phibar + (size_t)j0 * plane + rxc + y);   // phi_bar row j
+    V f0 = ldy<YPL>(p.phibar + (size_t)j0 * plane + rxc + y);   // phi_bar row j
     // Two register sets, A and B, alternate between the rows (no copies: a register copy of a row still in
     // flight would wait for it).  Step j computes from cur (row j), re-fills cur with row j+2 and stages oth
     // (row j+1, loaded one step earlier) into LDS: the loads of a row are in flight across a whole step,
@@ -138,11 +140,11 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<R> p, int jchunk,
     auto step = [&](int j, In& cur, const In& oth) {
       const int buf = (j - j0) & 1;
       const V pm = strip[buf][r][lane], pp = strip[buf][r + 2][lane], pc = cur.pc;
-      const R pyl = lane_from_prev(pc.w, zym ? (R)0 : cur.el);
-      const R pyr = lane_from_next(pc.x, zyp ? (R)0 : cur.er);
+      const R pyl = lane_from_prev(f4(pc, YPL - 1), zym ? (R)0 : cur.el);
+      const R pyr = lane_from_next(f4(pc, 0), zyp ? (R)0 : cur.er);
       V rn4, an4[NA];
       V m1x4, m2x4;
-      R m1y[4], m2y[4];
+      R m1y[YPL], m2y[YPL];
       // this step's 4 points summed in fp32 (4 terms), then one fp64 add per sum: the fixed-order fp64
       // accumulation over t stays, with a quarter of the fp64 work
       // (fp64: straight into the fixed-order fp64 sums, s)
@@ -154,10 +156,10 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<R> p, int jchunk,
         for (int i = 0; i < NS; ++i) fsb[i] = (R)0;
       }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
+      for (int e = 0; e < YPL; ++e) {
         const R c = f4(pc, e);
         const R lft = e == 0 ? pyl : f4(pc, e - 1);
-        const R rgt = e == 3 ? pyr : f4(pc, e + 1);
+        const R rgt = e == YPL - 1 ? pyr : f4(pc, e + 1);
         R ao[4], an[4], fo[4];
 #pragma unroll
         for (int a = 0; a < NA; ++a) ao[a] = f4(cur.al[a], e);
@@ -200,9 +202,9 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<R> p, int jchunk,
       }
       const size_t o = (size_t)j * plane + rxc + y;
       if (live && !(p.dbg & 128)) {   // PDHG_DBG 128: no rho / alp stores (timing experiments only)
-        st4(rd + o, rn4);
+        sty<YPL>(rd + o, rn4);
 #pragma unroll
-        for (int a = 0; a < NA; ++a) st4(ad[a] + o, an4[a]);
+        for (int a = 0; a < NA; ++a) sty<YPL>(ad[a] + o, an4[a]);
       }
       f0 = pcs;
       if constexpr (FR) if (!(p.dbg & 256)) {   // PDHG_DBG 256: no residual / edge terms (timing only)
@@ -212,13 +214,13 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<R> p, int jchunk,
         flux[buf][r][2][lane] = m2x4;
         // y part of row j: neighbours from the adjacent lanes; the strip's outer columns are left out
         // (0 here) and handed to the residual kernel through p.ey
-        const R rym = lane_from_prev(rn4.w, (R)0), ryp = lane_from_next(rn4.x, (R)0);
-        const R m1ym = lane_from_prev(m1y[3], (R)0), m2yp = lane_from_next(m2y[0], (R)0);
+        const R rym = lane_from_prev(f4(rn4, YPL - 1), (R)0), ryp = lane_from_next(f4(rn4, 0), (R)0);
+        const R m1ym = lane_from_prev(m1y[YPL - 1], (R)0), m2yp = lane_from_next(m2y[0], (R)0);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int e = 0; e < YPL; ++e) {
           const R r0 = f4(rn4, e);
-          const R lo = e == 0 ? rym : f4(rn4, e - 1), hi = e == 3 ? ryp : f4(rn4, e + 1);
-          const R m1l = e == 0 ? m1ym : m1y[e - 1], m2h = e == 3 ? m2yp : m2y[e + 1];
+          const R lo = e == 0 ? rym : f4(rn4, e - 1), hi = e == YPL - 1 ? ryp : f4(rn4, e + 1);
+          const R m1l = e == 0 ? m1ym : m1y[e - 1], m2h = e == YPL - 1 ? m2yp : m2y[e + 1];
           yeps[e] = p.epsl * ((hi + lo - (R)2 * r0) * p.inv_dy2);
           ydiv[e] = (m1y[e] - m1l) * p.inv_dy + (m2h - m2y[e]) * p.inv_dy;
         }
@@ -227,8 +229,8 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<R> p, int jchunk,
         // (eps rho'/dy^2 + m1y/dy); k_res_fwdy_fused_2d adds them (p.ey)
         if (lane == 0 || lane == kWave - 1) {
           const bool first = lane == 0;
-          R c = first ? -m2y[0] * p.inv_dy : m1y[3] * p.inv_dy;
-          if (use_eps) c = c + p.epsl * ((first ? rn4.x : rn4.w) * p.inv_dy2);
+          R c = first ? -m2y[0] * p.inv_dy : m1y[YPL - 1] * p.inv_dy;
+          if (use_eps) c = c + p.epsl * ((first ? f4(rn4, 0) : f4(rn4, YPL - 1)) * p.inv_dy2);
           const int sy = first ? (blockIdx.y == 0 ? nstrip - 1 : blockIdx.y - 1)
                                : (blockIdx.y + 1 == nstrip ? 0 : blockIdx.y + 1);
           p.ey[(((size_t)j * nx + x) * nstrip + sy) * 2 + (first ? 1 : 0)] = c;
@@ -241,12 +243,12 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<R> p, int jchunk,
           const int tt = top ? (tile == 0 ? ngx - 1 : tile - 1) : (tile + 1 == ngx ? 0 : tile + 1);
           V c;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
+          for (int e = 0; e < YPL; ++e) {
             R v = top ? -f4(m2x4, e) * p.inv_dx : f4(m1x4, e) * p.inv_dx;
             if (use_eps) v = v + p.epsl * (f4(rn4, e) * p.inv_dx2);
             f4set(c, e, v);
           }
-          st4(p.ex + (((size_t)j * ngx + tt) * 2 + (top ? 1 : 0)) * ny + y, c);
+          sty<YPL>(p.ex + (((size_t)j * ngx + tt) * 2 + (top ? 1 : 0)) * ny + y, c);
         }
       }
       if (j + 1 < j1) {     // uniform over the workgroup
@@ -268,7 +270,7 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<R> p, int jchunk,
       // the next slab's row 0: the time difference is left to k_res_fwdy_fused_2d (halo)
       __syncthreads();
       const bool inner = j1 < p.T;
-      const V rnx = inner ? ld4(rd + (size_t)j1 * plane + rxc + y) : z4r<R>();
+      const V rnx = inner ? ldy<YPL>(rd + (size_t)j1 * plane + rxc + y) : zy<R, YPL>();
       finish_res(j1 - 1, (j1 - 1 - j0) & 1, rnx, (!inner && p.last_slab) ? p.c_over_dt : (R)0,
                  inner || p.last_slab);
     }

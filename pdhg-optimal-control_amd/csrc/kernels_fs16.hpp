@@ -1,4 +1,4 @@
-// 65536-point DHT of row pairs as 16 x 4096 (fp32, nx = 65536: C1, BASELINE configs[1]) with a permuted
+// 65536-point DHT of row pairs as 16 x 4096 (nx = 65536: C1, BASELINE configs[1]; fp32 and fp64) with a permuted
 // spectrum.
 //
 // Same preconditioner as the four-step kernels (H1_precond_1d, utils_precond.py:105-140: DHT_x of the
@@ -17,7 +17,9 @@
 // k1 = 0; of x = 4096 n1 + n2 it is 4096 (15 - n1) + 4096 - n2 (column 4096 - n2) for n2 != 0.
 // HBM per iteration: A reads the residual inputs and writes Y (8 B/point), B reads Y and writes the spectrum
 // rows, B' / A' the same the other way round; every access is a whole 128-B line.
+// fp64 (R = double): the same stages on complex doubles; stage B's 2 lines + twiddle seeds take 152 KiB of LDS.
 #pragma once
+#include "kernels_2d_fast.hpp"
 #include "kernels_fs_wide.hpp"
 
 namespace pdhg {
@@ -26,16 +28,33 @@ constexpr int kF16N2 = 4096;
 constexpr int kF16Line = Pad<kF16N2>::LINE;
 
 // Hartley values of rows a, b at k and N - k from Z_k = z, Z_{N-k} = w (fft_lds.hpp header)
+template <typename R>
 struct HPair {
-  float ha, hb, ma, mb;
+  R ha, hb, ma, mb;
 };
-__device__ __forceinline__ HPair hunpack(float2 z, float2 w) {
-  HPair h;
-  h.ha = 0.5f * ((z.x + w.x) - (z.y - w.y));
-  h.hb = 0.5f * ((z.y + w.y) - (w.x - z.x));
-  h.ma = 0.5f * ((w.x + z.x) - (w.y - z.y));
-  h.mb = 0.5f * ((w.y + z.y) - (z.x - w.x));
-  return h;
+template <typename C>
+__device__ __forceinline__ HPair<decltype(C::x)> hunpack(C z, C w) {
+  using R = decltype(C::x);
+  const R h = (R)0.5;
+  HPair<R> q;
+  q.ha = h * ((z.x + w.x) - (z.y - w.y));
+  q.hb = h * ((z.y + w.y) - (w.x - z.x));
+  q.ma = h * ((w.x + z.x) - (w.y - z.y));
+  q.mb = h * ((w.y + z.y) - (z.x - w.x));
+  return q;
+}
+
+// value of v in lane l (wave-uniform result)
+template <typename R>
+__device__ __forceinline__ R lane_value(R v, int l) {
+  if constexpr (sizeof(R) == 4) {
+    return __builtin_bit_cast(R, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+  } else {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+    return __builtin_bit_cast(R, ((unsigned long long)hi << 32) | lo);
+  }
 }
 
 // Stage A (forward).  grid (4096/256, pairs); block 256: thread = column n2; 16 residual values per row,
@@ -43,10 +62,10 @@ __device__ __forceinline__ HPair hunpack(float2 z, float2 w) {
 // The x -+ 1 neighbours come from the neighbouring lanes (DPP); the values beyond the wave's 64 columns for
 // all 16 rows n1 are fetched by ONE load per array (lane l < 16: column cw - 1 of row n1 = l, lane 16 + l:
 // column cw + 64) and picked per row with readlane.
-template <int EGNO, int G = 16>
-__global__ void __launch_bounds__(256, G == 16 ? 1 : 4) k_f16a_fwd_1d(KP<float> p, const float2* __restrict__ twN,
-                                                     float2* __restrict__ Y) {
-  using C = float2;
+template <int EGNO, int G = 16, typename R = float>
+__global__ void __launch_bounds__(256, G == 16 ? 1 : 4) k_f16a_fwd_1d(KP<R> p, const cplx<R>* __restrict__ twN,
+                                                     cplx<R>* __restrict__ Y) {
+  using C = cplx<R>;
   if (p.ctrl->done) return;
   const int nx = p.nx, T = p.T;
   const int c = blockIdx.x * 256 + threadIdx.x;
@@ -54,18 +73,18 @@ __global__ void __launch_bounds__(256, G == 16 ? 1 : 4) k_f16a_fwd_1d(KP<float> 
   const int pair = blockIdx.y, j = 2 * pair;
   const bool has2 = (j + 1) < T;
   const int cur = p.ctrl->cur;
-  const float* rho = p.rho[cur];
-  const float* a1 = p.alp[cur][0];
-  const float* a2 = p.alp[cur][1];
+  const R* rho = p.rho[cur];
+  const R* a1 = p.alp[cur][0];
+  const R* a2 = p.alp[cur][1];
   const int j1c = has2 ? j + 1 : j, j2 = min(j + 2, T - 1);
   const size_t o0 = (size_t)j * nx, o1 = (size_t)j1c * nx;
-  const float* r_j = rho + o0;
-  const float* r_j1 = rho + o1;
-  const float* r_j2 = rho + (size_t)j2 * nx;
+  const R* r_j = rho + o0;
+  const R* r_j1 = rho + o1;
+  const R* r_j2 = rho + (size_t)j2 * nx;
   const int ex = (kF16N2 * (lane & 15) + cw + ((lane & 16) ? 64 : -1)) & (nx - 1);
-  const float e_ax = p.ax[ex], e_r0 = r_j[ex], e_r1 = r_j1[ex];
-  const float e_b10 = a1[o0 + ex], e_b20 = a2[o0 + ex], e_b11 = a1[o1 + ex], e_b21 = a2[o1 + ex];
-  auto edge = [](float v, int l) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l)); };
+  const R e_ax = p.ax[ex], e_r0 = r_j[ex], e_r1 = r_j1[ex];
+  const R e_b10 = a1[o0 + ex], e_b20 = a2[o0 + ex], e_b11 = a1[o1 + ex], e_b21 = a2[o1 + ex];
+  auto edge = [](R v, int l) { return lane_value(v, l); };
   C v[16];
   int cl = c;   // laundered at every group: the group's addresses are formed there, not hoisted to the top
 #pragma unroll
@@ -76,18 +95,18 @@ __global__ void __launch_bounds__(256, G == 16 ? 1 : 4) k_f16a_fwd_1d(KP<float> 
       asm volatile("" : "+v"(cl));
     }
     const int x = kF16N2 * n1 + cl;
-    const float ac = p.ax[x];
-    const float am = lane_from_prev(ac, edge(e_ax, n1)), ap = lane_from_next(ac, edge(e_ax, 16 + n1));
+    const R ac = p.ax[x];
+    const R am = lane_from_prev(ac, edge(e_ax, n1)), ap = lane_from_next(ac, edge(e_ax, 16 + n1));
     // every load unconditional (rows clamped into [0, T)), the missing row's terms selected away
-    const float c0 = r_j[x], c1 = r_j1[x], c2 = r_j2[x];
-    const float b10 = a1[o0 + x], b20 = a2[o0 + x], b11 = a1[o1 + x], b21 = a2[o1 + x];
-    const float r0 = res1d<EGNO>(p, c0, lane_from_prev(c0, edge(e_r0, n1)), lane_from_next(c0, edge(e_r0, 16 + n1)),
-                                 has2 ? c1 : 0.f, b10, lane_from_prev(b10, edge(e_b10, n1)), b20,
-                                 lane_from_next(b20, edge(e_b20, 16 + n1)), ac, am, ap, j == T - 1);
-    const float r1 = res1d<EGNO>(p, c1, lane_from_prev(c1, edge(e_r1, n1)), lane_from_next(c1, edge(e_r1, 16 + n1)),
-                                 (j + 2 < T) ? c2 : 0.f, b11, lane_from_prev(b11, edge(e_b11, n1)), b21,
-                                 lane_from_next(b21, edge(e_b21, 16 + n1)), ac, am, ap, j + 1 == T - 1);
-    v[n1] = make_float2(r0, has2 ? r1 : 0.f);
+    const R c0 = r_j[x], c1 = r_j1[x], c2 = r_j2[x];
+    const R b10 = a1[o0 + x], b20 = a2[o0 + x], b11 = a1[o1 + x], b21 = a2[o1 + x];
+    const R r0 = res1d<EGNO>(p, c0, lane_from_prev(c0, edge(e_r0, n1)), lane_from_next(c0, edge(e_r0, 16 + n1)),
+                             has2 ? c1 : (R)0, b10, lane_from_prev(b10, edge(e_b10, n1)), b20,
+                             lane_from_next(b20, edge(e_b20, 16 + n1)), ac, am, ap, j == T - 1);
+    const R r1 = res1d<EGNO>(p, c1, lane_from_prev(c1, edge(e_r1, n1)), lane_from_next(c1, edge(e_r1, 16 + n1)),
+                             (j + 2 < T) ? c2 : (R)0, b11, lane_from_prev(b11, edge(e_b11, n1)), b21,
+                             lane_from_next(b21, edge(e_b21, 16 + n1)), ac, am, ap, j + 1 == T - 1);
+    v[n1] = cmk<C>(r0, has2 ? r1 : (R)0);
   }
   dft_any<C, 16>(v);
   C w[16];
@@ -101,9 +120,10 @@ __global__ void __launch_bounds__(256, G == 16 ? 1 : 4) k_f16a_fwd_1d(KP<float> 
 // Stage B (forward).  grid (8, pairs); block 512; LDS 2 lines of 4096 + TwLds<4096>.
 // Workgroup g transforms chunks {g, 16 - g} (g = 0: the self-partnered chunks {0, 8}) and writes the
 // Hartley rows j, j+1 of both to p.work at chunk-major positions.
-__global__ void __launch_bounds__(512) k_f16b_fwd_1d(KP<float> p, const float2* __restrict__ twN,
-                                                     const float2* __restrict__ Y) {
-  using C = float2;
+template <typename R = float>
+__global__ void __launch_bounds__(512) k_f16b_fwd_1d(KP<R> p, const cplx<R>* __restrict__ twN,
+                                                     const cplx<R>* __restrict__ Y) {
+  using C = cplx<R>;
   constexpr int NT = 512, L = kF16Line;
   if (p.ctrl->done) return;
   extern __shared__ __align__(16) unsigned char smem_raw[];
@@ -116,22 +136,22 @@ __global__ void __launch_bounds__(512) k_f16b_fwd_1d(KP<float> p, const float2* 
   const C* Yp = Y + (size_t)pair * nx;
   const int tid = threadIdx.x;
 #pragma unroll 4
-  for (int i = tid; i < 2 * (kF16N2 / 2); i += NT) {   // two complex per 16-B load
+  for (int i = tid; i < 2 * (kF16N2 / 2); i += NT) {   // two complex per load (16 B fp32, 32 B fp64)
     const int ln = i >> 11, e = 2 * (i & 2047);
-    const float4 q = *reinterpret_cast<const float4*>(Yp + (size_t)(ln ? kb : ka) * kF16N2 + e);
+    const V4<R> q = ld4(reinterpret_cast<const R*>(Yp + (size_t)(ln ? kb : ka) * kF16N2 + e));
     C* d = A + ln * L;
-    d[pix(e)] = make_float2(q.x, q.y);
-    d[pix(e + 1)] = make_float2(q.z, q.w);
+    d[pix(e)] = cmk<C>(q.x, q.y);
+    d[pix(e + 1)] = cmk<C>(q.z, q.w);
   }
   lds_sync();
   lds_fft_inplace_tl<C, kF16N2, 2, NT>(A, twl);
-  float* w0 = p.work + (size_t)j * nx;
-  float* w1 = w0 + nx;
+  R* w0 = p.work + (size_t)j * nx;
+  R* w1 = w0 + nx;
   if (g == 0) {   // chunk 0: partner (4096 - k2) mod 4096; chunk 8: partner 4095 - k2 (one output each)
 #pragma unroll 2
     for (int i = tid; i < kF16N2; i += NT) {
-      const HPair h0 = hunpack(A[pix(i)], A[pix((kF16N2 - i) & (kF16N2 - 1))]);
-      const HPair h8 = hunpack(A[L + pix(i)], A[L + pix(kF16N2 - 1 - i)]);
+      const HPair<R> h0 = hunpack(A[pix(i)], A[pix((kF16N2 - i) & (kF16N2 - 1))]);
+      const HPair<R> h8 = hunpack(A[L + pix(i)], A[L + pix(kF16N2 - 1 - i)]);
       w0[i] = h0.ha;
       w0[8 * kF16N2 + i] = h8.ha;
       if (has2) {
@@ -142,7 +162,7 @@ __global__ void __launch_bounds__(512) k_f16b_fwd_1d(KP<float> p, const float2* 
   } else {        // chunk ka element i pairs with chunk kb element 4095 - i: both outputs
 #pragma unroll 2
     for (int i = tid; i < kF16N2; i += NT) {
-      const HPair h = hunpack(A[pix(i)], A[L + pix(kF16N2 - 1 - i)]);
+      const HPair<R> h = hunpack(A[pix(i)], A[L + pix(kF16N2 - 1 - i)]);
       const int P = ka * kF16N2 + i, Pm = kb * kF16N2 + (kF16N2 - 1 - i);
       w0[P] = h.ha;
       w0[Pm] = h.ma;
@@ -156,9 +176,10 @@ __global__ void __launch_bounds__(512) k_f16b_fwd_1d(KP<float> p, const float2* 
 
 // Stage B' (inverse).  grid (8, pairs); block 512: chunks {2g, 2g+1} of spectrum rows j, j+1 packed as
 // z = H_j + i H_{j+1}, 4096-point FFT, to Y[k1][n2].
-__global__ void __launch_bounds__(512) k_f16b_inv_1d(KP<float> p, const float2* __restrict__ twN,
-                                                     float2* __restrict__ Y) {
-  using C = float2;
+template <typename R = float>
+__global__ void __launch_bounds__(512) k_f16b_inv_1d(KP<R> p, const cplx<R>* __restrict__ twN,
+                                                     cplx<R>* __restrict__ Y) {
+  using C = cplx<R>;
   constexpr int NT = 512, L = kF16Line;
   if (p.ctrl->done) return;
   extern __shared__ __align__(16) unsigned char smem_raw[];
@@ -167,39 +188,45 @@ __global__ void __launch_bounds__(512) k_f16b_inv_1d(KP<float> p, const float2* 
   fill_twlds<C, kF16N2>(twl, twN, 16);
   const int nx = p.nx, g = blockIdx.x, pair = blockIdx.y, j = 2 * pair;
   const bool has2 = (j + 1) < p.T;
-  const float* w0 = p.work + (size_t)j * nx + 2 * g * kF16N2;   // chunks 2g, 2g+1 are contiguous
-  const float* w1 = w0 + nx;
+  const R* w0 = p.work + (size_t)j * nx + 2 * g * kF16N2;   // chunks 2g, 2g+1 are contiguous
+  const R* w1 = w0 + nx;
   const int tid = threadIdx.x;
 #pragma unroll 4
-  for (int i = tid; i < 2 * kF16N2 / 4; i += NT) {   // four points per 16-B load of each row
+  for (int i = tid; i < 2 * kF16N2 / 4; i += NT) {   // four points per load of each row
     const int e = 4 * i;
-    const float4 a = *reinterpret_cast<const float4*>(w0 + e);
-    const float4 b = has2 ? *reinterpret_cast<const float4*>(w1 + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const V4<R> a = ld4(w0 + e);
+    const V4<R> b = has2 ? ld4(w1 + e) : z4r<R>();
     C* d = A + (e >> 12) * L;
     const int el = e & (kF16N2 - 1);
-    d[pix(el)] = make_float2(a.x, b.x);
-    d[pix(el + 1)] = make_float2(a.y, b.y);
-    d[pix(el + 2)] = make_float2(a.z, b.z);
-    d[pix(el + 3)] = make_float2(a.w, b.w);
+    d[pix(el)] = cmk<C>(a.x, b.x);
+    d[pix(el + 1)] = cmk<C>(a.y, b.y);
+    d[pix(el + 2)] = cmk<C>(a.z, b.z);
+    d[pix(el + 3)] = cmk<C>(a.w, b.w);
   }
   lds_sync();
   lds_fft_inplace_tl<C, kF16N2, 2, NT>(A, twl);
-  float2* Yp = Y + (size_t)pair * nx + 2 * g * kF16N2;
+  C* Yp = Y + (size_t)pair * nx + 2 * g * kF16N2;
 #pragma unroll 4
-  for (int i = tid; i < kF16N2; i += NT) {   // two complex per 16-B store
+  for (int i = tid; i < kF16N2; i += NT) {   // two complex per store
     const int e = 2 * i;
     const C* s = A + (e >> 12) * L;
     const int el = e & (kF16N2 - 1);
     const C u0 = s[pix(el)], u1 = s[pix(el + 1)];
-    *reinterpret_cast<float4*>(Yp + e) = make_float4(u0.x, u0.y, u1.x, u1.y);
+    V4<R> o;
+    o.x = u0.x;
+    o.y = u0.y;
+    o.z = u1.x;
+    o.w = u1.y;
+    st4(reinterpret_cast<R*>(Yp + e), o);
   }
 }
 
 // Stage A' (inverse) + primal update.  grid (2048/256, pairs); block 256: thread t owns columns t and
 // 4096 - t (t = 0: the self-partnered columns 0 and 2048).  One partial row of err1 sums per workgroup.
-__global__ void __launch_bounds__(256) k_f16a_inv_1d(KP<float> p, const float2* __restrict__ twN,
-                                                     const float2* __restrict__ Y) {
-  using C = float2;
+template <typename R = float>
+__global__ void __launch_bounds__(256) k_f16a_inv_1d(KP<R> p, const cplx<R>* __restrict__ twN,
+                                                     const cplx<R>* __restrict__ Y) {
+  using C = cplx<R>;
   double s[3] = {0.0, 0.0, 0.0};
   const int row = blockIdx.y * gridDim.x + blockIdx.x;
   if (p.ctrl->done) {
@@ -223,13 +250,13 @@ __global__ void __launch_bounds__(256) k_f16a_inv_1d(KP<float> p, const float2* 
   C fa[16], fb[16];
   column(ca, fa);
   column(cb, fb);
-  const float scale = p.tau * p.inv_n;
-  float* phi1 = p.phi + (size_t)(j + 1) * nx;   // phi rows j+1, j+2 (row 0 is the fixed initial condition)
-  float* pb1 = p.phibar + (size_t)(j + 1) * nx;
-  auto upd = [&](float old, float u, float* ph, float* pbar, int n) {
-    const float nw = old + scale * u;
+  const R scale = p.tau * p.inv_n;
+  R* phi1 = p.phi + (size_t)(j + 1) * nx;   // phi rows j+1, j+2 (row 0 is the fixed initial condition)
+  R* pb1 = p.phibar + (size_t)(j + 1) * nx;
+  auto upd = [&](R old, R u, R* ph, R* pbar, int n) {
+    const R nw = old + scale * u;
     ph[n] = nw;
-    pbar[n] = 2.f * nw - old;
+    pbar[n] = (R)2 * nw - old;
     const double d = (double)nw - (double)old;
     s[0] += d * d;
     s[1] += (double)old * (double)old;
@@ -239,23 +266,23 @@ __global__ void __launch_bounds__(256) k_f16a_inv_1d(KP<float> p, const float2* 
   // (the stores go through the same pointer, so the compiler cannot move later loads above them)
 #pragma unroll
   for (int h0 = 0; h0 < 16; h0 += 8) {
-    float oa[8][2], ob[8][2];
+    R oa[8][2], ob[8][2];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int n1 = h0 + q;
       const int na = kF16N2 * n1 + ca, nb = kF16N2 * (15 - n1) + cb;
 #pragma unroll
       for (int r = 0; r < 2; ++r) {
-        const float* ph = phi1 + (size_t)r * nx;
+        const R* ph = phi1 + (size_t)r * nx;
         const bool live = r == 0 || has2;
-        oa[q][r] = live ? ph[na] : 0.f;
-        ob[q][r] = live ? ph[(t == 0) ? kF16N2 * n1 + cb : nb] : 0.f;
+        oa[q][r] = live ? ph[na] : (R)0;
+        ob[q][r] = live ? ph[(t == 0) ? kF16N2 * n1 + cb : nb] : (R)0;
       }
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int n1 = h0 + q;
-      HPair ha, hb;
+      HPair<R> ha, hb;
       int na, nb;
       if (t != 0) {   // x = 4096 n1 + t pairs with 4096 (15 - n1) + 4096 - t
         ha = hunpack(fa[n1], fb[15 - n1]);
@@ -265,7 +292,7 @@ __global__ void __launch_bounds__(256) k_f16a_inv_1d(KP<float> p, const float2* 
         nb = kF16N2 * (15 - n1) + cb;
       } else {        // column 0: partner row (16 - n1) mod 16; column 2048: partner row 15 - n1
         ha = hunpack(fa[n1], fa[(16 - n1) & 15]);
-        const HPair h2 = hunpack(fb[n1], fb[15 - n1]);
+        const HPair<R> h2 = hunpack(fb[n1], fb[15 - n1]);
         hb.ha = h2.ha;
         hb.hb = h2.hb;
         na = kF16N2 * n1;

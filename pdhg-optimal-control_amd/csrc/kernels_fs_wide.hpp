@@ -68,19 +68,19 @@ __device__ __forceinline__ void fw_fft256(float2* a, const float2* twl) {
 
 // continuity residual at x from the centre values and the x +- 1 neighbours (update_fns_in_pdhg.py:72-81;
 // cont_residual_1d with the loads done by the caller)
-template <int EGNO>
-__device__ __forceinline__ float res1d(const KP<float>& p, float r0, float rm, float rp, float rnext, float b1c,
-                                       float b1m, float b2c, float b2p, float ac, float am, float ap, bool last) {
-  const float eps = 1e-4f;
+template <int EGNO, typename R>
+__device__ __forceinline__ R res1d(const KP<R>& p, R r0, R rm, R rp, R rnext, R b1c, R b1m, R b2c, R b2p, R ac, R am,
+                                   R ap, bool last) {
+  const R eps = (R)1e-4;
   // branch-free (the callers unroll 16 rows): epsl * Dxx is added as the reference does, even for epsl = 0
-  float res = (rnext - r0) * p.inv_dt;
-  res = res + p.epsl * ((rp + rm - 2.f * r0) * p.inv_dx2);
-  const float m1c = (r0 + eps) * fpos<float>(fval<float, EGNO>(b1c, ac));
-  const float m1m = (rm + eps) * fpos<float>(fval<float, EGNO>(b1m, am));
-  const float m2c = (r0 + eps) * fneg<float>(fval<float, EGNO>(b2c, ac));
-  const float m2p = (rp + eps) * fneg<float>(fval<float, EGNO>(b2p, ap));
+  R res = (rnext - r0) * p.inv_dt;
+  res = res + p.epsl * ((rp + rm - (R)2 * r0) * p.inv_dx2);
+  const R m1c = (r0 + eps) * fpos<R>(fval<R, EGNO>(b1c, ac));
+  const R m1m = (rm + eps) * fpos<R>(fval<R, EGNO>(b1m, am));
+  const R m2c = (r0 + eps) * fneg<R>(fval<R, EGNO>(b2c, ac));
+  const R m2p = (rp + eps) * fneg<R>(fval<R, EGNO>(b2p, ap));
   res = res - ((m1c - m1m) * p.inv_dx + (m2p - m2c) * p.inv_dx);
-  return res + (last ? p.c_over_dt : 0.f);
+  return res + (last ? p.c_over_dt : (R)0);
 }
 
 // Stage 1.  grid (256/64, pairs); block 1024 (16 waves: wave w handles n1 rows w, w + 16, ...); LDS 64 lines.

@@ -125,6 +125,7 @@ struct Impl : ImplBase {
   bool fast_dual = false;                 // fp32 time-marching float4 dual kernel (k_dual_fast_2d)
   int NTd = 256, gxd = 0, gyd = 0, gzd = 0, jchunk_d = 1;
   int dual_rx = 0;   // > 0: k_dual_lds_2d with dual_rx x rows per workgroup (x neighbours through LDS)
+  int dual_ypl = 4;  // y per lane of k_dual_lds_2d (fp64: 4 or 2)
   // fused residual: the dual sweep also forms the next primal's residual rows (k_dual_lds_2d FR), the
   // residual kernel only completes the tile-edge terms and transforms (k_res_fwdy_fused_2d)
   bool fuse_res = false;
@@ -364,9 +365,11 @@ struct Impl : ImplBase {
           const int v = atoi(e);
           if (v == 0 || (((sizeof(R) == 4 && (v == 4 || v == 16)) || v == 8) && nx % v == 0)) dual_rx = v;
         }
+        if (const char* e = getenv("PDHG_DUAL_YPL"))   // tuning: fp64 LDS dual with 2 y per lane
+          if (sizeof(R) == 8 && dual_rx == 8 && atoi(e) == 2) dual_ypl = 2;
         NTd = dual_rx ? dual_rx * 64 : std::min(256, ny / 4);
         gxd = dual_rx ? nx / dual_rx : nx;
-        gyd = dual_rx ? ny / 256 : (ny / 4 + NTd - 1) / NTd;
+        gyd = dual_rx ? ny / (64 * dual_ypl) : (ny / 4 + NTd - 1) / NTd;
         const int nJ0 = std::max(1, std::min(T, (2048 + gxd * gyd - 1) / (gxd * gyd)));
         jchunk_d = (T + nJ0 - 1) / nJ0;
         gzd = (T + jchunk_d - 1) / jchunk_d;
@@ -413,11 +416,18 @@ struct Impl : ImplBase {
       // periodic bc, egno 1/2, single context; each dual workgroup must march the whole window (the
       // residual row j needs rho'_{j+1}), so only grids with enough (x, y) tiles to fill the chip
       // (PDHG_FUSE_RES=1 forces it for any eligible size, =0 turns it off)
-      if (sizeof(R) == 4 && fast_dual && dual_rx == 8 && fast_rows && RWf == 8 && pb.bc_x == 0 && pb.bc_y == 0 &&
-          pb.egno != 3 && !two_sets && !xslab) {
+      // fp64: the sweep k_dual_lds_2d<.., double, YPL = 2> (128-column strips, 211 VGPRs) and the residual in
+      // half-tile tasks of 4 rows (k_res_fwdy_fused_2d<.., 4, 512, double>, the lines + twiddles fill the LDS)
+      const bool fr_rows = sizeof(R) == 4 ? (fast_rows && RWf == 8) : (res64 && (ny == 4096 || ny == 2048));
+      if (fast_dual && dual_rx == 8 && fr_rows && pb.bc_x == 0 && pb.bc_y == 0 && pb.egno != 3 && !two_sets &&
+          !xslab) {
         fuse_res = gxd * gyd >= 1024;
         if (const char* e = getenv("PDHG_FUSE_RES")) fuse_res = atoi(e) != 0;
         if (fuse_res) {
+          if (sizeof(R) == 8) {
+            dual_ypl = 2;
+            gyd = ny / 128;
+          }
           jchunk_d = T;
           gzd = 1;
         }
@@ -436,11 +446,14 @@ struct Impl : ImplBase {
         nt1d = 1024;
         // fp32 nx = 65536 (C1): four-step DHT over 16 + 9 workgroups of 1024 threads per row pair instead of
         // one workgroup per pair (T = 400 gave 200 workgroups for 256 CUs): 1.41 -> 1.12 ms per iteration
-        fourstep = sizeof(R) == 4 && nx == 65536;
+        // fp64 nx = 65536: the same 16 x 4096 split (kernels_fs16.hpp on complex doubles) instead of the
+        // generic Stockham passes over global scratch (fp64 C1: 3.9x the algorithmic bytes)
+        fourstep = nx == 65536;
         if (const char* e = getenv("PDHG_FOURSTEP")) fourstep = fourstep && atoi(e) != 0;   // tuning override
         if (const char* e = getenv("PDHG_FS_WIDE")) fs_wide = atoi(e) != 0;                 // tuning override
         fs16 = fourstep;
         if (const char* e = getenv("PDHG_FS16")) fs16 = fs16 && atoi(e) != 0;               // tuning override
+        if (sizeof(R) == 8 && !fs16) fourstep = false;   // the other four-step forms are fp32
         if (const char* e = getenv("PDHG_F16_GROUP")) f16_group = atoi(e);                   // tuning override
       }
       g4 = 1;
@@ -504,7 +517,7 @@ struct Impl : ImplBase {
     if (fuse_res) {
       if ((rc = alloc(&p.res, (size_t)T * npl))) return rc;
       if ((rc = alloc(&p.ex, (size_t)T * (nx / 8) * 2 * ny))) return rc;
-      if ((rc = alloc(&p.ey, (size_t)T * nx * (ny / 256) * 2))) return rc;
+      if ((rc = alloc(&p.ey, (size_t)T * nx * (ny / (64 * dual_ypl)) * 2))) return rc;
     }
     if (xslab && (rc = alloc(&colwork, (size_t)T * xs_nbs * nxg * p.B))) return rc;
     if (slab) {
@@ -724,6 +737,25 @@ struct Impl : ImplBase {
       ProfScope ps(this, "residual");
       p.row_base = lo;
       p.row_cnt = hi - lo;
+      if constexpr (sizeof(R) == 8) {
+        auto go = [&](auto Nc) {
+          constexpr int N_ = decltype(Nc)::value;
+          const dim3 g(std::min((pb.nx / 4) * (hi - lo), n_cu));   // persistent, one workgroup per CU (LDS)
+          int r2;
+          if (pb.egno == 1) {
+            if ((r2 = ensure_lds(k_res_fwdy_fused_2d<1, N_, 4, 512, double>, lds_upd64))) return r2;
+            hipLaunchKernelGGL((k_res_fwdy_fused_2d<1, N_, 4, 512, double>), g, dim3(512), lds_upd64, stream, p, twy);
+          } else {
+            if ((r2 = ensure_lds(k_res_fwdy_fused_2d<2, N_, 4, 512, double>, lds_upd64))) return r2;
+            hipLaunchKernelGGL((k_res_fwdy_fused_2d<2, N_, 4, 512, double>), g, dim3(512), lds_upd64, stream, p, twy);
+          }
+          return (int)PDHG_OK;
+        };
+        rc = pb.ny == 4096 ? go(std::integral_constant<int, 4096>{}) : go(std::integral_constant<int, 2048>{});
+        if (rc) return rc;
+        HIP_TRY(hipGetLastError());
+        return PDHG_OK;
+      }
       rc = with_fast_rows([&](auto Nc, auto RWc, auto NTc) {
         constexpr int N_ = decltype(Nc)::value, RW_ = decltype(RWc)::value, NT_ = decltype(NTc)::value;
         int r2;
@@ -1061,9 +1093,7 @@ struct Impl : ImplBase {
         hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, p.partials, upd_rows, 1, p.ctrl);
     } else {
       int rc;
-      if constexpr (sizeof(R) == 4) {
-        if (fourstep) return launch_fourstep_1d(p);
-      }
+      if (fourstep) return launch_fourstep_1d(p);
       {
         ProfScope ps(this, "residual");
         rc = with_line_fft(plx, [&](auto f) {
@@ -1103,8 +1133,8 @@ struct Impl : ImplBase {
 
   // 1-D primal with the four-step DHT (nx = 65536, fp32): residual + DHT, Thomas, inverse DHT + update
   int launch_fourstep_1d(const KP<R>& p) {
+    if (fs16) return launch_fs16_1d(p);
     if constexpr (sizeof(R) == 4) {
-      if (fs16) return launch_fs16_1d(p);
       if (fs_wide) return launch_fourstep_wide_1d(p);
       constexpr int kFsNT = 1024;   // 16 waves: the load / unpack loops keep more rows in flight
       const int npairs = (pb.T + 1) / 2;
@@ -1179,24 +1209,24 @@ struct Impl : ImplBase {
   // the same as 16 x 4096 with a chunk-major spectrum (kernels_fs16.hpp): 16 + 8 workgroups per row pair
   // forward, 8 + 8 inverse
   int launch_fs16_1d(const KP<R>& p) {
-    if constexpr (sizeof(R) == 4) {
+    {
       const int npairs = (pb.T + 1) / 2;
       const size_t ldsb = (size_t)(2 * kF16Line + twlds_size(kF16N2)) * sizeof(C);
-      float2* Y = reinterpret_cast<float2*>(p.gscr);
+      C* Y = reinterpret_cast<C*>(p.gscr);
       int rc;
       {
         ProfScope ps(this, "residual");
         const dim3 ga(kF16N2 / 256, npairs);
         auto fwd = [&](auto eg) {
           constexpr int E = decltype(eg)::value;
-          if (f16_group == 4) hipLaunchKernelGGL((k_f16a_fwd_1d<E, 4>), ga, dim3(256), 0, stream, p, twx, Y);
-          else if (f16_group == 8) hipLaunchKernelGGL((k_f16a_fwd_1d<E, 8>), ga, dim3(256), 0, stream, p, twx, Y);
-          else hipLaunchKernelGGL((k_f16a_fwd_1d<E, 16>), ga, dim3(256), 0, stream, p, twx, Y);
+          if (f16_group == 4) hipLaunchKernelGGL((k_f16a_fwd_1d<E, 4, R>), ga, dim3(256), 0, stream, p, twx, Y);
+          else if (f16_group == 8) hipLaunchKernelGGL((k_f16a_fwd_1d<E, 8, R>), ga, dim3(256), 0, stream, p, twx, Y);
+          else hipLaunchKernelGGL((k_f16a_fwd_1d<E, 16, R>), ga, dim3(256), 0, stream, p, twx, Y);
         };
         if (pb.egno == 1) fwd(std::integral_constant<int, 1>{});
         else fwd(std::integral_constant<int, 2>{});
-        if ((rc = ensure_lds(k_f16b_fwd_1d, ldsb))) return rc;
-        hipLaunchKernelGGL(k_f16b_fwd_1d, dim3(8, npairs), dim3(512), ldsb, stream, p, twx, Y);
+        if ((rc = ensure_lds(k_f16b_fwd_1d<R>, ldsb))) return rc;
+        hipLaunchKernelGGL(k_f16b_fwd_1d<R>, dim3(8, npairs), dim3(512), ldsb, stream, p, twx, Y);
       }
       {
         ProfScope ps(this, "precond");
@@ -1204,9 +1234,9 @@ struct Impl : ImplBase {
       }
       {
         ProfScope ps(this, "update");
-        if ((rc = ensure_lds(k_f16b_inv_1d, ldsb))) return rc;
-        hipLaunchKernelGGL(k_f16b_inv_1d, dim3(8, npairs), dim3(512), ldsb, stream, p, twx, Y);
-        hipLaunchKernelGGL(k_f16a_inv_1d, dim3(kF16N2 / 2 / 256, npairs), dim3(256), 0, stream, p, twx, Y);
+        if ((rc = ensure_lds(k_f16b_inv_1d<R>, ldsb))) return rc;
+        hipLaunchKernelGGL(k_f16b_inv_1d<R>, dim3(8, npairs), dim3(512), ldsb, stream, p, twx, Y);
+        hipLaunchKernelGGL(k_f16a_inv_1d<R>, dim3(kF16N2 / 2 / 256, npairs), dim3(256), 0, stream, p, twx, Y);
       }
       hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, p.partials, 8 * npairs, 1, p.ctrl);
       HIP_TRY(hipGetLastError());
@@ -1235,8 +1265,18 @@ struct Impl : ImplBase {
       }
     } else {
       const dim3 g(gxd, gyd, gz);
+      if constexpr (EGNO != 3) {
+        if (fuse_res && p.inplace && gz == 1 && lo == 0 && hi == pb.T) {
+          hipLaunchKernelGGL((k_dual_lds_2d<EGNO, 8, true, double, 2>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi,
+                             zbase);
+          res_valid = true;
+          return;
+        }
+      }
       res_valid = false;
-      if (dual_rx == 8)
+      if (dual_rx == 8 && dual_ypl == 2)
+        hipLaunchKernelGGL((k_dual_lds_2d<EGNO, 8, false, double, 2>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase);
+      else if (dual_rx == 8)
         hipLaunchKernelGGL((k_dual_lds_2d<EGNO, 8, false, double>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase);
       else
         hipLaunchKernelGGL((k_dual_fast_2d<EGNO, double>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase);
@@ -1917,7 +1957,7 @@ struct Impl : ImplBase {
     }
     // fused residual: the dual also writes the residual rows (+1), the tile-edge row terms (2 rows per 8)
     // and the strip-edge column terms (2 per 256); the residual kernel reads them and writes the spectrum
-    const double edge = fuse_res ? 2.0 / 8.0 + 2.0 / 256.0 : 0.0;
+    const double edge = fuse_res ? 2.0 / 8.0 + 2.0 / (64.0 * dual_ypl) : 0.0;
     if (cls == "dual") return S * N * (1.0 + 2.0 * nr + (fuse_res ? 1.0 + edge : 0.0));
     if (cls == "residual") return S * N * (fuse_res ? 2.0 + edge : nr + 1.0);
     if (cls == "precond") return S * N * (d2 ? 4.0 : 2.0);   // 2-D: x-DHT+Thomas fwd (2N) + bwd+x-DHT (2N)
@@ -2147,6 +2187,7 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
     else if (k == "res64") *value = im.res64 ? 1 : 0;
     else if (k == "dual64") *value = (sizeof(typename std::remove_reference<decltype(im)>::type::Real) == 8 && im.fast_dual) ? 1 : 0;
     else if (k == "fast_dual") *value = im.fast_dual ? im.dual_rx : -1;
+    else if (k == "dual_ypl") *value = im.fast_dual && im.dual_rx ? im.dual_ypl : 0;
     else if (k == "fast_xt")
       *value = im.fast_xt ? (im.batch_xt && !im.half_real ? (im.xt_dma && im.pb.nx == 4096 ? 4 : 3) : im.ws_xt ? 2 : 1) : 0;
     else if (k == "half_real") *value = im.half_real ? 1 : 0;

@@ -1,70 +1,57 @@
-"""Diagnostic (GPU): single context vs t-slabs, iteration by iteration, from the reference initial state.
-
-usage: python scripts/diag_slab.py egno nx ny T P epsl iters [env=val ...]
-Prints per iteration the relative L2 distance of phi, rho and the four alp arrays between the single context
-and the slabs (LocalComm, the bench's schedule), and the err1 / err2 of both.
-"""
+"""Slab runner vs single context, one outer iteration at a time (GPU diagnostics for a failing slab case).
+usage: python scripts/diag_slab.py egno nx ny T P k [n] [exchange] [overlap]"""
 import os
 import sys
 
-ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
-sys.path[:0] = [os.path.join(ROOT, "pdhg-optimal-control_amd")]
+import numpy as np
 
-import numpy as np  # noqa: E402
-
-
-def rel(a, b):
-    nb = np.linalg.norm(b)
-    return float(np.linalg.norm(a - b) / (nb if nb > 0 else 1.0))
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "tests"))
+sys.path.insert(0, os.path.join(HERE, "..", "oracle"))   # tests/_problems.py builds the inputs with it
+sys.path.insert(0, os.path.join(HERE, "..", "pdhg-optimal-control_amd"))
+from _problems import make_problem, rel  # noqa: E402
 
 
 def main():
-    egno, nx, ny, T, P = (int(v) for v in sys.argv[1:6])
-    epsl, iters = float(sys.argv[6]), int(sys.argv[7])
-    for kv in sys.argv[8:]:
-        k, v = kv.split("=")
-        os.environ[k] = v
     import torch
     from pdhg_amd.context import PDHGContext
-    from pdhg_amd.slab import LocalComm, SlabContext, SlabRunner, join_state
-    xs = np.linspace(0.0, 2.0, nx, endpoint=False)
-    ys = np.linspace(0.0, 2.0, ny, endpoint=False)
-    G = {"dx": 2.0 / nx, "dy": 2.0 / ny, "dt": 1.0 / max(T, 40), "xs": xs, "ys": ys}
-    g = np.sin(np.pi * xs)[:, None] + np.sin(np.pi * ys)[None, :]     # set_fns.py:20 (egno 1/2)
+    from pdhg_amd.slab import LocalComm, SlabContext, SlabRunner, join_state, slab_bounds, split_state
+    a = sys.argv[1:]
+    egno, nx, ny, T, nr, k = (int(v) for v in a[:6])
+    n = int(a[6]) if len(a) > 6 else 6
+    exchange = a[7] if len(a) > 7 else "neighbour"
+    overlap = (a[8] != "0") if len(a) > 8 else True
+    P = make_problem(egno, 2, nx, ny, T, 0.0)
     tau, sigma = 0.1 / 1.5, 0.1 * 1.5
-    ref = PDHGContext(egno, 2, nx, ny, T, G["dx"], G["dy"], G["dt"], xs, ys, epsl=epsl, precision="fp32")
-    ref.init_state(g)
-    slabs = [SlabContext(r, P, T, egno, nx, ny, G["dx"], G["dy"], G["dt"], G["xs"], G["ys"], epsl=epsl)
-             for r in range(P)]
-    for s in slabs:
-        s.init_state(g)
-    print("single: fused", ref.path_info("fused_residual"), "fast_xt", ref.path_info("fast_xt"), "half_real",
-          ref.path_info("half_real"), "| slab0: fused", slabs[0].path_info("fused_residual"), "fast_xt",
-          slabs[0].path_info("fast_xt"), flush=True)
-    runner = SlabRunner(slabs, LocalComm(P))
-    for it in range(1, iters + 1):
-        a = ref.iterate(1, tau, sigma, -1.0, 1)
-        b = runner.iterate(1, tau, sigma, -1.0, 1)
+    ref = PDHGContext(egno, 2, nx, ny, T, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"], epsl=0.0,
+                      precision="fp32", rho_alp_iters=k)
+    ref.set_state(P["phi"], P["rho"], P["alp"])
+    slabs = [SlabContext(r, nr, T, egno, nx, ny, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"], epsl=0.0,
+                         rho_alp_iters=k) for r in range(nr)]
+    print("slab T", [s.T for s in slabs], "fast_xt", [s.path_info("fast_xt") for s in slabs], flush=True)
+    for s, part in zip(slabs, split_state(P["phi"], P["rho"], P["alp"], slab_bounds(T, nr))):
+        s.set_state(*part)
+    runner = SlabRunner(slabs, LocalComm(nr), overlap=overlap, exchange=exchange)
+    print("n_long", runner.n_long, flush=True)
+    for it in range(1, n + 1):
+        st_r = ref.iterate(1, tau, sigma, -1.0, k)
+        st = runner.iterate(1, tau, sigma, -1.0, k)
         torch.cuda.synchronize()
-        sr = ref.get_state()
-        ss = join_state([s.get_state() for s in slabs])
-        d = [rel(ss[0], sr[0]), rel(ss[1], sr[1])] + [rel(x, y) for x, y in zip(ss[2], sr[2])]
-        print("it {} phi {:.2e} rho {:.2e} alp {} | err1 {:.6e} {:.6e} err2 {:.6e} {:.6e}".format(
-            it, d[0], d[1], " ".join("{:.1e}".format(v) for v in d[2:]), a["err1"], b["err1"], a["err2"], b["err2"]),
-            flush=True)
-        if it in (1, 2):   # where in (t, x, y) the phi difference sits
-            diff = np.abs(ss[0] - sr[0])
-            per_t = diff.reshape(T + 1, -1).max(axis=1)
-            print("   phi |diff| max per t row:", " ".join("{:.1e}".format(v) for v in per_t[:: max(1, T // 16)]))
-            rdiff = np.abs(ss[1] - sr[1])
-            print("   rho |diff| max per t row:", " ".join("{:.1e}".format(v) for v in rdiff.reshape(T, -1).max(axis=1)))
-            print("   phi |diff| max per t row (all):", " ".join("{:.1e}".format(v) for v in per_t))
-            per_x = diff.max(axis=(0, 2))
-            print("   phi |diff| max per x (every nx/16):", " ".join("{:.1e}".format(v) for v in per_x[:: nx // 16]))
-            print("   argmax", np.unravel_index(np.argmax(diff), diff.shape), "max", float(diff.max()))
-    for s in slabs:
-        s.close()
-    ref.close()
+        phi_r, rho_r, alp_r = ref.get_state()
+        parts = [s.get_state() for s in slabs]
+        phi_s, rho_s, alp_s = join_state(parts)
+        fin = [bool(np.isfinite(x[0]).all() and np.isfinite(x[1]).all()) for x in parts]
+        print("it", it, "ref", {q: st_r[q] for q in ("iters_run", "status", "err1", "err2") if q in st_r},
+              "slab", {q: st[q] for q in ("iters", "status", "err1", "err2") if q in st}, "finite", fin,
+              "phi", "%.3e" % rel(phi_s, phi_r), "rho", "%.3e" % rel(rho_s, rho_r), flush=True)
+        if not all(fin):
+            for r, x in enumerate(parts):
+                bad = np.argwhere(~np.isfinite(x[0]))
+                print("  slab", r, "phi nonfinite", len(bad), bad[:5].tolist(), flush=True)
+            break
+        # rows of phi with the largest deviation
+        d = np.abs(phi_s - phi_r).reshape(phi_s.shape[0], -1).max(axis=1)
+        print("  phi max |d| per row", np.array2string(d, precision=2), flush=True)
 
 
 if __name__ == "__main__":

@@ -318,16 +318,50 @@ FP64_CASES = {
     "c3_rows_ny4096": {"res64": 1, "dual64": 1},
     "c2_x2048": {"dual64": 1},
     "c2_rows_ny2048": {"res64": 1, "dual64": 1},
-    "c1_exact": {"glb_line": 1},
+    "c1_exact": {"glb_line": 1, "fs16": 1},   # the 16 x 4096 split on complex doubles (kernels_fs16.hpp)
     "c4_halfreal_x8192": {"f64_xt": 1, "half_real": 1, "dual64": 1},   # k_precond_xt_f64_2d<4096, 512, HR>
     "c4_rows_ny8192": {"ip_rows": 1, "dual64": 1},   # row pairs transformed in one padded in-place line (FFTIp)
+    # the fp64 fused residual (k_dual_lds_2d<.., double, 2> FR + k_res_fwdy_fused_2d<.., 4, 512, double>), the
+    # default at C3's size, forced on the fixture's smaller grid
+    "c3_rows_ny4096+fr": {"res64": 1, "dual64": 1, "fused_residual": 1, "dual_ypl": 2},
+    "c2_rows_ny2048+fr": {"res64": 1, "dual64": 1, "fused_residual": 1, "dual_ypl": 2},
 }
+FP64_ENV = {"fr": {"PDHG_FUSE_RES": "1", "PDHG_SHORT_T": "0"}}
 FP64_BAR = 1e-9
 
 
+def test_fp64_fs16_matches_generic(native, monkeypatch):
+    """fp64 C1 (nx = 65536, T = 400): the 16 x 4096 split against the generic Stockham passes over global scratch
+    (PDHG_FS16=0), both the same float64 arithmetic up to the transform's association: 2 iterations from the
+    seeded state, every state array within 1e-12."""
+    F = _fixture("c1_exact")
+    egno, ndim, nx, ny, T = (int(v) for v in F["meta"])
+    P = make_problem(egno, ndim, nx, ny, T, 0.0, seeded=True)
+    out = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("PDHG_FS16", flag)
+        ctx = device_ctx(P, "fp64")
+        try:
+            assert ctx.path_info("fs16") == int(flag)
+            ctx.set_state(P["phi"], P["rho"], P["alp"])
+            st = ctx.iterate(2, TAU, SIGMA, -1.0, 1)
+            assert st["iters_run"] == 2 and st["status"] == 0
+            out.append(ctx.get_state() + (st,))
+        finally:
+            ctx.close()
+    (p1, r1, a1, s1), (p0, r0, a0, s0) = out
+    assert rel(p1, p0) < 1e-12 and rel(r1, r0) < 1e-12
+    for x, y in zip(a1, a0):
+        assert rel(x, y) < 1e-12
+    assert abs(s1["err1"] - s0["err1"]) <= 1e-10 * s0["err1"]
+
+
 @pytest.mark.parametrize("name", list(FP64_CASES))
-def test_config_fp64_fixed_bounds(native, name, parity_log):
-    F = _fixture(name)
+def test_config_fp64_fixed_bounds(native, name, parity_log, monkeypatch):
+    fixture, _, variant = name.partition("+")
+    for k, v in FP64_ENV.get(variant, {}).items():
+        monkeypatch.setenv(k, v)
+    F = _fixture(fixture)
     egno, ndim, nx, ny, T = (int(v) for v in F["meta"])
     failures = []
     for tag in [str(t) for t in F["runs"]]:

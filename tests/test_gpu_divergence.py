@@ -37,8 +37,10 @@ FP32_TOL = 1e-5      # relative, per finite iteration, against the float32 oracl
 # relative L2 over the sample points, per iteration (fp64 device vs float64 oracle): the north-star 1e-5 through
 # iteration PTS_TIGHT; after it 1e-4.  The reference's explicit sigma*epsl*Lap(phi_bar) term amplifies any
 # difference of one rounding by ~2e3-5e3 per iteration until the unstable modes dominate both runs (measured: 9e-17,
-# 2e-13, 1e-9, 8e-7 at iterations 2-5), and the float64 oracle started from phi_0 perturbed by one ulp drifts from
-# itself pointwise by the same amount (tests/golden/divergence_c3_plane_T4_points_ulp.npz)
+# 2e-13, 1e-9, 8e-7 at iterations 2-5).  The float64 oracle started from phi_0 perturbed by +-1 ulp per entry drifts
+# from itself further still (phi 4e-13, 2e-9, 1e-5, 8e-3 and rho 5e-9, 2e-5, 7e-3, 4e-2 at iterations 2-5; 0.16 / 0.42
+# at 10: tests/golden/divergence_c3_plane_T4_points_ulp.npz), so no float64 implementation can
+# be held to 1e-5 pointwise late in the growth; PTS_TOL_LATE guards the device's measured spread (2.6e-5, round 4)
 PTS_TOL, PTS_TIGHT, PTS_TOL_LATE = 1e-5, 6, 1e-4
 # err2 (utils_pdhg_solver.py:60-68) of the fp32 run: a sum of ratios ||d alp|| / ||alp|| whose numerators are
 # differences of float32 states in the growth phase (measured 2.5e-4, round 3); the norms themselves keep FP32_TOL

@@ -6,6 +6,10 @@ With rho_alp_iters = 1 the fp32 dual sweep also forms the next primal's continui
 the terms at its 8-row x 256-column tile edges.  PDHG_FUSE_RES=1 forces the path on grids smaller than the
 default threshold, =0 turns it off.  Bounds: the fp32 bounds of test_gpu_parity (phi 1e-5, rho 2e-4 after
 10 iterations from the seeded state); fused vs unfused device runs agree to fp32 reassociation (1e-5).
+
+fp64 (ny = 2048 / 4096: the sweep k_dual_lds_2d<.., double, 2> on 128-column strips, the residual in 4-row
+half-tile tasks of k_res_fwdy_fused_2d<.., 4, 512, double>): against the float64 oracle at 1e-9 (phi, rho; the
+fp64 bar of test_gpu_configs) and against the unfused fp64 kernels at 1e-12.
 """
 import numpy as np
 import pytest
@@ -31,16 +35,26 @@ UNSTABLE = [(2, 2, 256, 512, 3, 0.1), (1, 2, 256, 256, 2, 0.1)]
 UNSTABLE_IDS = ["e{}d{}_{}x{}_T{}_eps{}".format(*c) for c in UNSTABLE]
 
 
-def _ctx(P, fuse, monkeypatch):
+FUSED64 = [
+    (2, 2, 32, 2048, 4, 1e-5),
+    (1, 2, 16, 2048, 3, 0.0),
+    (2, 2, 24, 4096, 2, 1e-4),   # 3 tiles of 8 rows = 6 half-tile tasks per time row; 32 strips
+]
+IDS64 = ["e{}d{}_{}x{}_T{}_eps{}".format(*c) for c in FUSED64]
+
+
+def _ctx(P, fuse, monkeypatch, precision="fp32"):
     monkeypatch.setenv("PDHG_FUSE_RES", "1" if fuse else "0")
     monkeypatch.setenv("PDHG_SHORT_T", "0")   # these windows are short: keep the 8-row (fusable) dual
-    ctx = device_ctx(P, "fp32")
+    ctx = device_ctx(P, precision)
     assert ctx.path_info("fused_residual") == (1 if fuse else 0)
+    if precision == "fp64" and fuse:
+        assert ctx.path_info("dual_ypl") == 2 and ctx.path_info("res64") == 1
     return ctx
 
 
-def _run(P, fuse, n, monkeypatch):
-    ctx = _ctx(P, fuse, monkeypatch)
+def _run(P, fuse, n, monkeypatch, precision="fp32"):
+    ctx = _ctx(P, fuse, monkeypatch, precision)
     ctx.set_state(P["phi"], P["rho"], P["alp"])
     st = ctx.iterate(n, TAU, SIGMA, -1.0, 1)
     assert st["iters_run"] == n and st["status"] == 0
@@ -116,3 +130,20 @@ def test_fused_dropin_calls_and_state_reset(native, monkeypatch):
     assert rel(ctx.get_state()[0], ref.get_state()[0]) < 1e-6
     ref.close()
     ctx.close()
+
+
+@pytest.mark.parametrize("case", FUSED64, ids=IDS64)
+def test_fused_fp64_vs_oracle_and_unfused(native, case, monkeypatch):
+    """fp64 fused residual: 6 iterations from the seeded state against the float64 oracle and the unfused fp64
+    kernels (update_fns_in_pdhg.py:72-96 formed by the sweep, tile / strip edges completed by the residual)."""
+    P = make_problem(*case)
+    n = 6
+    phi_o, rho_o, alp_o, e1_o, _ = _oracle_iterate(P, n)
+    (s0, st0), (s1, st1) = [_run(P, fuse, n, monkeypatch, "fp64") for fuse in (False, True)]
+    assert rel(s1[0], phi_o) < 1e-9 and rel(s1[1], rho_o) < 1e-9
+    for a_d, a_o in zip(s1[2], alp_o):
+        assert rel(a_d, a_o) < 1e-7
+    assert abs(st1["err1"] - e1_o) <= 1e-7 * e1_o
+    for a, b in zip((s1[0], s1[1]) + tuple(s1[2]), (s0[0], s0[1]) + tuple(s0[2])):
+        assert rel(a, b) < 1e-12
+    assert abs(st1["err2"] - st0["err2"]) <= 1e-10 * st0["err2"]

@@ -48,7 +48,9 @@ def test_slabs_match_single_context(native, egno, nx, ny, T, nr, k, overlap, exc
     from pdhg_amd.context import PDHGContext
     from pdhg_amd.slab import LocalComm, SlabRunner, join_state, slab_bounds, split_state
     P = make_problem(egno, 2, nx, ny, T, 0.0)
-    tau, sigma, n = 0.1 / 1.5, 0.1 * 1.5, 6
+    # egno 3 at dx = 2/4096 from the seeded state diverges in the single context as well (NaN at iteration 5,
+    # scripts/diag_slab.py; err2 is inf from iteration 4): 3 iterations there
+    tau, sigma, n = 0.1 / 1.5, 0.1 * 1.5, (3 if (egno == 3 and nx >= 4096) else 6)
     ref = PDHGContext(egno, 2, nx, ny, T, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"], epsl=0.0,
                       precision="fp32", rho_alp_iters=k)
     ref.set_state(P["phi"], P["rho"], P["alp"])
