@@ -105,8 +105,9 @@ def pmc_traffic(args):
     """HBM bytes per launch of every kernel class from rocprofv3 PMC counters, collected in two
     separate child runs (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950) that are started
     BEFORE this process touches the GPU (a process that initialised HIP must not fork+exec).
-    FETCH_SIZE is doubled per MI355X_MICROARCH.md §HBM (gfx950 reports half of a wide coalesced
-    stream; uncalibrated for 4-B loads); WRITE_SIZE is exact for 16-B streaming stores.
+    FETCH_SIZE is doubled per MI355X_MICROARCH.md §HBM (gfx950 reports half of a coalesced stream);
+    calibrated on this pool for 4-, 8- and 16-B loads per lane alike, and WRITE_SIZE exact for 4-, 8- and
+    16-B stores (scripts/fetch_calib.hip, profiles/r04_fetch_calib.txt).
     Returns ({class: {"bytes", "fetch_bytes_x2", "write_bytes"}}, None) or (None, reason)."""
     import csv
     import shutil
@@ -316,8 +317,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--rho-alp-iters", type=int, default=1)
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp64"],
-                    help="fp32 (default) or fp64 (the reference's arithmetic)")
+    ap.add_argument("--precision", default=None, choices=["fp32", "fp64"],
+                    help="fp32 (default) or fp64 (the reference's arithmetic; the default of --marching, whose "
+                         "per-window stop counts are only the reference's in its arithmetic)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-T", type=int, default=1)
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
@@ -333,6 +335,8 @@ def main():
     ap.add_argument("--selftest", action="store_true",
                     help="launcher / process-group check only: no GPU work, prints the world size")
     args = ap.parse_args()
+    if args.precision is None:
+        args.precision = "fp64" if args.marching else "fp32"
 
     if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))

@@ -579,8 +579,10 @@ def PDHG_solver_oneiter(fn_update_primal, fn_update_dual, fns_dict, phi0, rho0, 
 
 def PDHG_multi_step(fn_update_primal, fn_update_dual, fns_dict, g, x_arr, ndim, nt, nspatial, dt, dspatial, c_on_rho,
                     time_step_per_PDHG=2, epsl=0.0, stepsz_param=0.9, n_ctrl=None, fv=None, N_maxiter=1000000,
-                    print_freq=1000, eps=1e-6, verbose=False):
-    """Time-window marching with NaN step back-off, utils_pdhg_solver.py:97-225 (no checkpoint resume)."""
+                    print_freq=1000, eps=1e-6, verbose=False, stats=None):
+    """Time-window marching with NaN step back-off, utils_pdhg_solver.py:97-225 (no checkpoint resume).
+    stats (test bookkeeping, not in the reference): a list that receives {"window", "window_iters", "stepsz"}
+    per solved window, as the device driver's."""
     if n_ctrl is None:
         n_ctrl = ndim
     assert (nt - 1) % (time_step_per_PDHG - 1) == 0
@@ -617,6 +619,8 @@ def PDHG_multi_step(fn_update_primal, fn_update_dual, fns_dict, g, x_arr, ndim, 
             else:
                 iters, phi_c, rho_c, alp_c = results_all[-1]
                 max_iters = max(max_iters, iters)
+                if stats is not None:
+                    stats.append({"window": i, "window_iters": iters, "stepsz": stepsz_param})
                 phi_all.append(phi_c[:-1] if i < nt_PDHG - 1 else phi_c)
                 rho_all.append(rho_c)
                 alp_all.append(np.stack(alp_c, axis=0))

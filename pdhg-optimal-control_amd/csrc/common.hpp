@@ -5,6 +5,10 @@
 
 namespace pdhg {
 
+// raw bit vectors for the buffer load / store builtins
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+
 constexpr int kWave = 64;          // CDNA wavefront width
 constexpr int kMaxPass = 24;       // max FFT passes in a plan
 constexpr int kNumSums = 16;       // doubles of partial sums per workgroup

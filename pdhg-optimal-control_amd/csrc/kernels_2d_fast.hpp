@@ -651,6 +651,12 @@ __device__ __forceinline__ float h_entry(float dd, int j0) {
   const float th = fmaxf(log1pf(dl + sqrtf(dl * (dl + 2.f))), 1e-20f);
   return expm1f(-th) * (1.f + expf(-th * (float)(2 * j0 + 1))) / expm1f(-2.f * th * (float)(j0 + 1));
 }
+__device__ __forceinline__ double h_entry(double dd, int j0) {
+  if (j0 == 0) return 1.0;
+  const double dl = 0.5 * dd;
+  const double th = fmax(log1p(dl + sqrt(dl * (dl + 2.0))), 1e-300);
+  return expm1(-th) * (1.0 + exp(-th * (double)(2 * j0 + 1))) / expm1(-2.0 * th * (double)(j0 + 1));
+}
 
 // Column-block x-transform + Thomas in t (fp32, nx = N a power of two).
 // A thread owns IT items (kx, l) of the block's NL complex lines; item (kx, l) carries the two

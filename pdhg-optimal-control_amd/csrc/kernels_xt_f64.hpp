@@ -7,8 +7,6 @@ namespace pdhg {
 // Rows of a column block through buffer loads / stores: one descriptor per row (wave-uniform base) and the
 // per-item offset i * NTT * 16 B as the scalar offset, so the 3 x IT row accesses per step need one VGPR of
 // address instead of a 64-bit address per item (64-bit per-item addresses cost the registers that made the round-3 form of this kernel spill).
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const double* base, int bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), 0, bytes, 0x00020000);
 }

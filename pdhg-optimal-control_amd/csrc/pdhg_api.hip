@@ -149,7 +149,7 @@ struct Impl : ImplBase {
   bool xt_pair = false;           // batched x transform as 2 rows x 512 threads, two workgroups per CU
   bool xt_dma = false;            // x transform with the rows staged HBM -> LDS by DMA (k_precond_xt_dma_2d)
   bool f64_xt = false;            // fp64 nx = 4096: in-place line + register carries (k_precond_xt_f64_2d)
-  bool thomas_chunk = false;      // 1-D fp32: t-solve in chunks of 32 rows (k_thomas_chunk_1d)
+  bool thomas_chunk = false;      // 1-D: t-solve in chunks of 32 rows (k_thomas_chunk_1d)
   bool fs_wide = true;            // four-step DHT with 64-column / 32-row tiles (k_fs1w_1d / k_fs2w_1d)
   int f16_group = 16;             // rows n1 per load group of k_f16a_fwd_1d (PDHG_F16_GROUP: 4, 8, 16; 16 measured best)
   bool fs16 = false;              // 16 x 4096 split with a chunk-major spectrum (kernels_fs16.hpp)
@@ -460,7 +460,7 @@ struct Impl : ImplBase {
       gx5 = (nx + 255) / 256;
       g5 = std::max(1, std::min(T, 8192 / std::max(1, gx5)));
       // chunked t-solve: one wave per 32-row chunk of 64 modes (T <= 512, Ct != 0)
-      thomas_chunk = sizeof(R) == 4 && pb.Ct != 0.0 && T <= 16 * 32;
+      thomas_chunk = pb.Ct != 0.0 && T <= 16 * 32;
       if (const char* e = getenv("PDHG_THOMAS_CHUNK")) thomas_chunk = thomas_chunk && atoi(e) != 0;   // override
     }
     g_outer = 2048;
@@ -876,12 +876,16 @@ struct Impl : ImplBase {
 
   // ---------------- launches ----------------
   void launch_thomas_1d(const KP<R>& p) {
-    if constexpr (sizeof(R) == 4) {
-      if (thomas_chunk) {
+    if (thomas_chunk) {
+      if constexpr (sizeof(R) == 4) {   // one 32-row chunk per wave
         const int P = (pb.T + 31) / 32;
-        hipLaunchKernelGGL((k_thomas_chunk_1d<32>), dim3((pb.nx + 63) / 64), dim3(64 * P), 0, stream, p);
-        return;
+        hipLaunchKernelGGL((k_thomas_chunk_1d<32, 1, R>), dim3((pb.nx + 63) / 64), dim3(64 * P), 0, stream, p);
+      } else {                           // one 16-row chunk per half-wave (32 modes per workgroup)
+        const int P = (pb.T + 15) / 16;
+        hipLaunchKernelGGL((k_thomas_chunk_1d<16, 2, R>), dim3((pb.nx + 31) / 32), dim3(64 * ((P + 1) / 2)), 0, stream,
+                           p);
       }
+      return;
     }
     hipLaunchKernelGGL((k_thomas_1d<R>), dim3((pb.nx + 255) / 256), dim3(256), 0, stream, p);
   }

@@ -283,26 +283,29 @@ def test_one_step_eps(native, name, monkeypatch, parity_log):
     assert all(v <= b for v, b in m.values()), m
 
 
-@pytest.mark.parametrize("nx,T,egno", [(65536, 100, 1), (4096, 33, 2), (1024, 400, 1), (256, 1, 2)])
-def test_chunked_thomas_matches_one_thread_per_mode(native, monkeypatch, nx, T, egno):
+@pytest.mark.parametrize("prec", ["fp32", "fp64"])
+@pytest.mark.parametrize("nx,T,egno", [(65536, 100, 1), (4096, 33, 2), (1024, 400, 1), (256, 1, 2), (512, 17, 1)])
+def test_chunked_thomas_matches_one_thread_per_mode(native, monkeypatch, nx, T, egno, prec):
     """1-D t-solve in 32-row chunks (k_thomas_chunk_1d: chunk carries folded through LDS) against the
     one-thread-per-mode recurrence (k_thomas_1d) on the same state: 3 iterations from the reference state,
     fp32, <= 1e-6 (same algebra, another association of the products).  From the seeded rough state the two
     fp32 results differ by up to 2e-5 at nx = 65536 (both within the float32 oracle's own 6.5e-5 of the
-    float64 one there: test_config_instantiation c1_exact / c1_exact@thomas1)."""
+    float64 one there: test_config_instantiation c1_exact / c1_exact@thomas1).  fp64: 16-row chunks, one per
+    half-wave (T = 17: an odd chunk count, the last half-wave's chunk empty), <= 1e-12."""
     P = make_problem(egno, 1, nx, 1, T, 0.0, seeded=False)
     out = []
     for chunk in ("0", "1"):
         monkeypatch.setenv("PDHG_THOMAS_CHUNK", chunk)
-        ctx = device_ctx(P, "fp32")
+        ctx = device_ctx(P, prec)
         try:
             assert ctx.path_info("thomas_chunk") == int(chunk)
-            ctx.set_state(*_f32_state(P))
+            ctx.set_state(*(_f32_state(P) if prec == "fp32" else (P["phi"], P["rho"], P["alp"])))
             ctx.iterate(3, TAU, SIGMA, -1.0, 1)
             out.append(ctx.get_state())
         finally:
             ctx.close()
-    assert rel(out[1][0], out[0][0]) < 1e-6 and rel(out[1][1], out[0][1]) < 1e-6
+    bar = 1e-6 if prec == "fp32" else 1e-12
+    assert rel(out[1][0], out[0][0]) < bar and rel(out[1][1], out[0][1]) < bar
 
 
 # The parity path: the same fixtures in the reference's arithmetic (fp64; jaxsrc/update_fns_in_pdhg.py:10).  Every

@@ -11,11 +11,15 @@ Tolerances (stated per SURVEY.md Appendix B.8):
     the residual is dominated by eps*Lap(noise) ~ 1e4, so fp32 input rounding alone gives
     ~kappa*6e-8 ~ 1e-5 relative error in U; bounds there are 1e-4 (U, alp) and 2e-4 (rho).
 """
+import os
+
 import numpy as np
 import pytest
 
 import pdhg_oracle as O
 from _problems import device_ctx, make_problem, oracle_fns, rel
+
+HERE = os.path.dirname(os.path.abspath(__file__))
 
 pytestmark = pytest.mark.gpu
 
@@ -515,3 +519,41 @@ def test_fp64_nx4096_x_transform(native, case):
         ctx.close()
     assert rel(phi_d, phi_o) < 1e-11 and rel(rho_d, rho_o) < 1e-10, (rel(phi_d, phi_o), rel(rho_d, rho_o))
     assert abs(st["err1"] - e1_o) <= 1e-8 * e1_o and abs(st["err2"] - e2_o) <= 1e-8 * e2_o
+
+
+def test_marching_window_counts_fp64(native):
+    """The marching default's per-window stop iterations (PDHG_multi_step, utils_pdhg_solver.py:97-225; T = 1
+    windows, rho_alp_iters = 10, eps 1e-6, NaN back-off) in the reference's arithmetic: the fp64 device driver
+    against the float64 oracle's counts at C2's dt on 64^2 (tests/golden/marching_c2dt_64.json, window 1 backs
+    off to stepsz 0.09).  Counts within one iteration, the same step size per window, the final state to 1e-8.
+    (fp32 stops elsewhere: err1 < 1e-6 is within a few float32 ulps of relative change)"""
+    import json
+    from pdhg_amd import set_fns, utils_pdhg_solver as S
+    F = json.load(open(os.path.join(HERE, "golden", "marching_c2dt_64.json")))
+    nx, ny, ndim, egno = F["nx"], F["ny"], F["ndim"], F["egno"]
+    fns = set_fns.set_up_example_fns(egno, ndim, 0)
+    x_arr = O.make_grid(ndim, nx, ny, egno)
+    g = set_fns.set_up_J(egno, ndim, (2.0, 2.0))(x_arr)
+    dsp = (2.0 / nx, 2.0 / ny)
+    fv = O.compute_Dxx_fft_fv(ndim, (nx, ny), dsp, (0, 0))
+    fp, fd = S.make_update_fns(ndim, (0, 0), rho_alp_iters=F["rho_alp_iters"], precision="fp64")
+    stats = []
+    res, _ = S.PDHG_multi_step(fp, fd, fns, g, x_arr, ndim, F["windows"] + 1, (nx, ny), F["dt"], dsp, 70.0,
+                               time_step_per_PDHG=2, epsl=F["epsl"], stepsz_param=F["stepsz"], fv=fv, n_ctrl=ndim,
+                               N_maxiter=1000000, print_freq=1000000, eps=F["eps"], verbose=False, stats=stats)
+    iters, stepsz, s, nan_attempts = [], [], F["stepsz"], 0
+    for st in stats:
+        if st["status"] == 2:
+            nan_attempts += 1
+            continue
+        iters.append(int(st["window_iters"]))
+        stepsz.append(s - 0.01 * nan_attempts)
+    assert len(iters) == F["windows"], stats
+    assert all(abs(a - b) <= 1 for a, b in zip(iters, F["window_iters"])), (iters, F["window_iters"])
+    assert np.allclose(stepsz, F["window_stepsz"], rtol=0, atol=1e-12), (stepsz, F["window_stepsz"])
+    _, phi, rho, _ = res[0]
+    assert abs(np.linalg.norm(phi) - F["phi_norm"]) <= 1e-8 * F["phi_norm"]
+    assert rel(phi.reshape(-1)[::997], np.array(F["phi_sample"])) < 1e-8
+    assert rel(rho.reshape(-1)[::997], np.array(F["rho_sample"])) < 1e-6
+    from pdhg_amd import update_fns_in_pdhg as U
+    U.clear_cache()
