@@ -42,6 +42,10 @@ CONFIGS = {
     "c3w1": (2, 2, 0.1, 4096, 4096, 2),   # one T = 1 window of C3's grid (time_step_per_PDHG = 2 default)
     "c3w4": (2, 2, 0.1, 4096, 4096, 5),   # short windows of C3's grid (kernel-policy crossover)
     "c3w8": (2, 2, 0.1, 4096, 4096, 9),
+    # one GPU's share of the 8-GPU t-slab runs as a window of its own (C3: 200 / 8 rows, C4: 400 / 8 rows; the
+    # per-GPU compute term of the multi-GPU cost model)
+    "c3w25": (2, 2, 0.1, 4096, 4096, 26),
+    "c4w50": (2, 2, 0.1, 8192, 8192, 51),
 }
 
 
