@@ -340,7 +340,7 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<R> p, const cplx<R>*
 // floats) go through a small LDS double buffer, so only the edge lanes read them.
 // fp64 (R = double): the sweep's strips are 128 columns wide (k_dual_lds_2d<.., double, YPL = 2>) and 4 rows of
 // complex double fill the LDS, so a task is half a sweep tile (RW = 4, NH = 2): the first half adds row x0's
-// p.ex term, the second row x0+RW-1's.
+// p.ex term, the second row x0+RW-1's.  fp32 at ny = 8192 (C4) likewise: 4 rows of 8192 floats fill the LDS.
 // grid: G <= T * nx/RW; block NT (N/4 % NT == 0); LDS RW/2 * (N + N/16) * sizeof(C) (+ 2 * RW * N/YW reals).
 template <int EGNO, int N, int RW, int NT, typename R = float>
 __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<R> p, const cplx<R>* __restrict__ twy) {
@@ -353,8 +353,8 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<R> p, const cplx<R>
   constexpr int GPT = (N / 4) / NT;
   constexpr int YW = sizeof(R) == 4 ? 256 : 128, NSTRIP = N / YW;
   constexpr int NEY = RW * NSTRIP * 2;   // strip-edge terms of one task
-  static_assert((sizeof(R) == 4 ? RW == 8 : RW == 4) && N % YW == 0 && (N / 4) % NT == 0,
-                "fused residual tasks: 8 (fp32) / 4 (fp64) rows of the sweep's 8-row x YW-column tiles");
+  static_assert((RW == 8 || RW == 4) && (sizeof(R) == 4 || RW == 4) && N % YW == 0 && (N / 4) % NT == 0,
+                "fused residual tasks: 8 or 4 (fp64, fp32 ny = 8192) rows of the sweep's 8-row x YW-column tiles");
   static_assert(NEY <= NT, "one strip-edge term per thread");
   if (p.ctrl->done) return;
   extern __shared__ __align__(16) unsigned char smem_raw[];
@@ -391,7 +391,8 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<R> p, const cplx<R>
         if (r >= r0 && r < r1) rows[gi][r] = ld4(R0 + (size_t)r * N + y);
     }
   };
-  constexpr int RSPLIT = (NT >= 1024) ? RW / 2 : RW;
+  // (N = 8192: none -- the 8192-point transform's registers leave no room for rows held across it)
+  constexpr int RSPLIT = (N > 4096) ? 0 : (NT >= 1024) ? RW / 2 : RW;
   auto load_edges = [&](int task) {
     const int jt = task / ngx, j = p.row_base + jt, tk = task - jt * ngx, tile = tk / NH;
     const R* E = p.ex + ((size_t)j * (ngx / NH) + tile) * 2 * N;

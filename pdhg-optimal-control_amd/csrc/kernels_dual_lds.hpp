@@ -38,6 +38,11 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<R> p, int jchunk,
   __shared__ __align__(16) V strip[2][RX + 2][64];
   // FR: [buffer][row][rho', m1x, m2x][lane]
   __shared__ __align__(16) V flux[FR ? 2 : 1][FR ? RX : 1][3][64];
+  // p.nbsync: steps staged per row wave.  A wave reads only its neighbours' strip rows and flux rows, so instead of a
+  // block barrier per step it publishes its own count after staging and waits for the two neighbours' counts: waves
+  // drift by up to a step against each other and the CU's loads are no longer issued in lock-step.  (The double
+  // buffers stay safe: a neighbour that has staged step t has finished reading the buffer staged at step t-1.)
+  __shared__ int nstaged[RX];
   const int cur = p.ctrl->cur;
   const int src_set = (p.inplace || p.sub == 0) ? cur : 1 - cur;
   const int dst_set = p.inplace ? cur : 1 - cur;
@@ -131,6 +136,24 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<R> p, int jchunk,
     }
     sty<YPL>(p.res + (size_t)jr * plane + rxc + y, out);
   };
+  const bool nbs = p.nbsync != 0;
+  // neighbour sync after staging step t's rows (see nstaged): publish, then wait for waves r-1 and r+1
+  auto step_sync = [&](int t) {
+    if (!nbs) {
+      __syncthreads();
+      return;
+    }
+    // LDS only: the count is written once this wave's strip / flux writes have landed (lgkmcnt), and no wait
+    // touches vmcnt, so the next rows' global loads stay in flight across the sync
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    typedef __attribute__((address_space(3))) volatile int lds_int;   // ds_read / ds_write (a generic pointer
+    lds_int* cnt = (lds_int*)nstaged;                                  // would be flat: vmcnt-counted)
+    if (lane == 0) cnt[r] = t;
+    const int rl = r > 0 ? r - 1 : r, rr = r < RX - 1 ? r + 1 : r;
+    while (min(cnt[rl], cnt[rr]) < t) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");   // the neighbours' rows are read after their counts
+  };
+  if (threadIdx.x < RX) nstaged[threadIdx.x] = 0;
   if (j0 < j1) {
     V f0 = ldy<YPL>(p.phibar + (size_t)j0 * plane + rxc + y);   // phi_bar row j
     // Two register sets, A and B, alternate between the rows (no copies: a register copy of a row still in
@@ -253,7 +276,7 @@ __global__ void __launch_bounds__(RX * 64, 2) k_dual_lds_2d(KP<R> p, int jchunk,
       }
       if (j + 1 < j1) {     // uniform over the workgroup
         stage(oth, buf ^ 1);
-        __syncthreads();
+        step_sync(j + 1 - j0);
       }
     };
     In A = load(j0), B = load(min(j0 + 1, j1 - 1));

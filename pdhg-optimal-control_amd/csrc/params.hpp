@@ -15,6 +15,7 @@ struct KP {
   int inplace;             // dual updates rho/alp in place (rho_alp_iters == 1)
   int sub;                 // dual sub-iteration index of this launch
   int dbg;                 // timing experiments only (env PDHG_DBG); 0 in production
+  int nbsync;              // k_dual_lds_2d: neighbour-flag sync between the row waves instead of a block barrier
   int tile_j;              // residual task tiling: TJ time rows x 4 row groups per tile (1 = off)
   int row_base, row_cnt;   // fast residual launch: time rows [row_base, row_base + row_cnt)
   R inv_dx, inv_dy, inv_dt, inv_dx2, inv_dy2;

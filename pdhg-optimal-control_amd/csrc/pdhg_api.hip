@@ -312,6 +312,10 @@ struct Impl : ImplBase {
       gx5 = (ny + 255) / 256;
       g5 = std::max(1, std::min(T * nx, 8192 / std::max(1, gx5)));
       if (const char* e = getenv("PDHG_DBG")) p.dbg = atoi(e);   // timing experiments only
+      // tuning: k_dual_lds_2d step sync through neighbour counts instead of the block barrier.  Bitwise the same
+      // results; measured (round 4, interleaved A/B at C3): fp32 dual 31.16 -> 31.85 ms, fp64 60.39 -> 60.39 ms,
+      // so the barrier is not what bounds the sweep and the default stays the barrier
+      if (const char* e = getenv("PDHG_DUAL_NBSYNC")) p.nbsync = atoi(e) != 0;
       if (const char* e = getenv("PDHG_T1_XT")) t1_xt = atoi(e) != 0;   // tuning override
       // short windows (the reference's T = 1 marching default): few time rows per workgroup leave little to
       // pipeline over t, so occupancy decides.  Measured on C3's grid (bench --config c3w1/c3w4/c3w8): the
@@ -418,10 +422,14 @@ struct Impl : ImplBase {
       // (PDHG_FUSE_RES=1 forces it for any eligible size, =0 turns it off)
       // fp64: the sweep k_dual_lds_2d<.., double, YPL = 2> (128-column strips, 211 VGPRs) and the residual in
       // half-tile tasks of 4 rows (k_res_fwdy_fused_2d<.., 4, 512, double>, the lines + twiddles fill the LDS)
-      const bool fr_rows = sizeof(R) == 4 ? (fast_rows && RWf == 8) : (res64 && (ny == 4096 || ny == 2048));
+      // fp32 ny = 8192 (C4's y extent): the 4-row fast kernels, so the residual runs half-tile tasks as in fp64
+      const bool fr_rows = sizeof(R) == 4 ? (fast_rows && (RWf == 8 || (RWf == 4 && ny == 8192)))
+                                          : (res64 && (ny == 4096 || ny == 2048));
       if (fast_dual && dual_rx == 8 && fr_rows && pb.bc_x == 0 && pb.bc_y == 0 && pb.egno != 3 && !two_sets &&
           !xslab) {
-        fuse_res = gxd * gyd >= 1024;
+        // fp32 ny = 8192: off unless asked for (c4w50 A/B, round 4: residual 31.2 -> 25.9 ms, dual 26.7 -> 31.3 ms,
+        // step 105.2 vs 104.7 -- the 4-row tasks' 16-B runs of the B = 1 spectrum, not the reads, bound the residual)
+        fuse_res = gxd * gyd >= 1024 && !(sizeof(R) == 4 && RWf == 4);
         if (const char* e = getenv("PDHG_FUSE_RES")) fuse_res = atoi(e) != 0;
         if (fuse_res) {
           if (sizeof(R) == 8) {
@@ -759,7 +767,8 @@ struct Impl : ImplBase {
       rc = with_fast_rows([&](auto Nc, auto RWc, auto NTc) {
         constexpr int N_ = decltype(Nc)::value, RW_ = decltype(RWc)::value, NT_ = decltype(NTc)::value;
         int r2;
-        if constexpr (sizeof(R) == 4 && RW_ == 8 && N_ % 256 == 0 && (N_ / 4) % NT_ == 0) {
+        if constexpr (sizeof(R) == 4 && (RW_ == 8 || (RW_ == 4 && N_ == 8192)) && N_ % 256 == 0 &&
+                      (N_ / 4) % NT_ == 0) {
           const dim3 g(std::min((pb.nx / RW_) * (hi - lo), n_cu));   // persistent, one workgroup per CU (LDS)
           auto go = [&](auto ntc) {
             constexpr int NTF = decltype(ntc)::value;
@@ -2204,8 +2213,8 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
     else if (k == "rows_rw") *value = im.fast_rows ? im.RWf : 0;   // rows per fast row-kernel workgroup
     // threads of the fast row kernels as launched (ny = 4096: 512 instead of 1024 per half_nt)
     else if (k == "row_threads") *value = im.nt_row;
-    else if (k == "res_threads") *value = im.fast_rows ? ((im.NTf == 1024 && im.RWf == 8 && (im.half_nt & 1) &&
-                                                           im.fuse_res) ? 512 : im.NTf) : 0;
+    else if (k == "res_threads") *value = im.fast_rows ? ((im.NTf == 1024 && (im.half_nt & 1) && im.fuse_res) ? 512
+                                                                                                      : im.NTf) : 0;
     else if (k == "upd_threads") *value = im.fast_rows ? ((im.NTf == 1024 && im.RWf == 8 && (im.half_nt & 2))
                                                               ? 512 : im.NTf) : 0;
     else if (k == "f64_xt") *value = im.f64_xt ? 1 : 0;   // fp64 nx = 4096 x transform (kernels_xt_f64.hpp)

@@ -147,3 +147,21 @@ def test_fused_fp64_vs_oracle_and_unfused(native, case, monkeypatch):
     for a, b in zip((s1[0], s1[1]) + tuple(s1[2]), (s0[0], s0[1]) + tuple(s0[2])):
         assert rel(a, b) < 1e-12
     assert abs(st1["err2"] - st0["err2"]) <= 1e-10 * st0["err2"]
+
+
+@pytest.mark.parametrize("prec,case", [("fp32", (2, 2, 256, 512, 5, 1e-5)), ("fp32", (1, 2, 512, 1024, 4, 1e-5)),
+                                       ("fp64", (2, 2, 32, 2048, 4, 1e-5))], ids=["fp32_e2", "fp32_e1", "fp64_e2"])
+@pytest.mark.parametrize("fuse", [True, False], ids=["fr", "nofr"])
+def test_dual_neighbour_sync_bitwise(native, monkeypatch, prec, case, fuse):
+    """k_dual_lds_2d with the per-step block barrier replaced by neighbour counts in LDS (PDHG_DUAL_NBSYNC=1):
+    the same arithmetic in the same order, so the states after 4 iterations are bitwise those of the barrier
+    form, with and without the fused residual."""
+    P = make_problem(*case)
+    out = []
+    for nb in ("0", "1"):
+        monkeypatch.setenv("PDHG_DUAL_NBSYNC", nb)
+        out.append(_run(P, fuse, 4, monkeypatch, prec))
+    (s0, st0), (s1, st1) = out
+    for a, b in zip((s1[0], s1[1]) + tuple(s1[2]), (s0[0], s0[1]) + tuple(s0[2])):
+        assert np.array_equal(a, b)
+    assert st1["err1"] == st0["err1"] and st1["err2"] == st0["err2"]
