@@ -143,18 +143,20 @@ int pdhg_synchronize(pdhg_ctx* ctx);
 int pdhg_device_bytes(pdhg_ctx* ctx, unsigned long long* bytes);
 
 /* Which kernel variant a context selected (no reference counterpart; tests and benches assert the fast
- * paths engaged): "fused_residual" 1/0 (the dual sweep forms the next residual, k_dual_lds_2d FR),
+ * paths engaged): "fused_residual" 1/0 (the dual sweep forms the next residual, k_dual_lds_2d FR; fp32 and
+ * fp64 -- fp64 on 128-column strips with 4-row residual tasks; fp32 ny = 8192 only with PDHG_FUSE_RES=1),
  * "fast_rows" 1/0 (fp32 8/4-row y-transform kernels), "fast_dual" (-1 generic, 0 row-per-thread,
  * RX rows through LDS), "dual_ypl" (y per lane of the LDS dual: 4, or 2 for fp64 with PDHG_DUAL_YPL=2;
  * 0 without it), "fast_xt" (0 generic, 1 single-role, 2 warp-specialised, 3 row-batched,
- * 4 row-batched with LDS-DMA staging x-transform), "half_real", "fourstep", "fs16", "fs_wide",
- * "glb_line", "thomas_chunk", "rows_rw", "res_threads", "upd_threads",
+ * 4 row-batched with LDS-DMA staging x-transform), "half_real", "fourstep", "fs16" (1-D nx = 65536 as
+ * 16 x 4096, fp32 and fp64), "fs_wide", "glb_line", "thomas_chunk" (1-D t-solve in chunks: 32 rows per wave
+ * fp32, 16 rows per half-wave fp64), "rows_rw", "res_threads", "upd_threads",
  * "row_threads" (threads of the generic row kernels), "res64" 1/0 (fp64 residual and update through the
  * 4-row fast kernels, ny = 2048 / 4096), "contig_fail" (large arrays of an fp32 2-D context that fell back
  * from a physically contiguous allocation to hipMalloc; environment PDHG_ALLOC=contig|none overrides the
  * contiguous-for-fp32-2-D default), "dual64" 1/0 (fp64 contexts: the row-per-thread time-marching dual
- * k_dual_fast_2d<EGNO, double>; default on where ny % 256 == 0, environment PDHG_DUAL64=0 selects the generic
- * per-point kernel), "f64_xt" 1/0 (fp64 nx = 4096: k_precond_xt_f64_2d), "graph" 1/0 (pdhg_iterate replays
+ * k_dual_fast_2d<EGNO, double>, or with nx % 8 == 0 and T >= 3 the LDS-row sweep k_dual_lds_2d<EGNO, 8, .., double>;
+ * default on where ny % 256 == 0, environment PDHG_DUAL64=0 selects the generic per-point kernel), "f64_xt" 1/0 (fp64 nx = 4096: k_precond_xt_f64_2d), "graph" 1/0 (pdhg_iterate replays
  * windows of iterations from a captured HIP graph; default on, environment PDHG_GRAPH=0 launches every
  * iteration eagerly), "graph_window" (iterations per replayed graph). */
 int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value);
