@@ -496,10 +496,17 @@ def main():
         barrier()
         el = time.perf_counter() - t0
         kern = {}
+        # rho_alp_iters > 1 with the multi-pass dual (path_info dual_multi): one "dual" launch per outer iteration
+        # covers the whole loop, so its algorithmic bytes are the sub-iterations' (mean inner count x one)
+        multi = k > 1 and ctx.path_info("dual_multi") == 1
+        inner_mean = (st.get("inner_total", 0) / max(st["iters_run"], 1)) if multi else 1.0
         for cls in ("residual", "precond", "update", "dual"):
             ms, nl = ctx.profile_query(cls)
             if nl:
-                kern[cls] = {"avg_ms": ms / nl, "launches": nl, "bytes_per_launch": ctx.algorithmic_bytes(k, cls)}
+                b = ctx.algorithmic_bytes(k, cls) * (inner_mean if cls == "dual" else 1.0)
+                kern[cls] = {"avg_ms": ms / nl, "launches": nl, "bytes_per_launch": b}
+                if cls == "dual" and multi:
+                    kern[cls]["passes"] = "probe + final (kernels_dual_multi.hpp), inner mean {:.2f}".format(inner_mean)
         ctx.profile_enable(False)
         return st, el, kern
 

@@ -51,6 +51,9 @@ struct Ctrl {
   int primal_valid;  // primal sums of the current outer iteration are valid
   int nan_seen;      // a NaN appeared in phi' or rho' (recorded even when the NaN stop is off)
   int first_nan;     // iteration (1-based, since the last reset) at which nan_seen was first set; 0: none
+  int kstar;         // chunked dual loop (k_dual_multi_2d): the exit sub-iteration count k*
+  int kstar_found;   // ... fixed by a chunk's finalize (reset by k_finalize_outer)
+  int kstored;       // ... sub-iterations of the state the second buffer set holds after the last chunk
   double err1, err2, err_inner;
   double s_dphi, s_phi_old, s_phi_new;   // finalized primal sums
   double row0_sq;                        // sum phi_0^2 of the fixed row 0 (written by set_state / init_state)

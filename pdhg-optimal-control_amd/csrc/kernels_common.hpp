@@ -97,6 +97,48 @@ __global__ void __launch_bounds__(1024) k_finalize_dual(const double* partials, 
   }
 }
 
+// Chunked dual loop (kernels_dual_multi.hpp): after the chunk of sub-iterations slo .. slo + nsub - 1, the first
+// one whose err (as k_finalize_dual, from the table of its sums) is below eps -- or the loop's last,
+// sub-iteration kmax - 1 -- fixes k* = s + 1; the bookkeeping of k_finalize_dual for that sub-iteration follows
+// (inner_count, err_inner, dual_sums [0, 1, 3+3a, 4+3a]).  kstored = slo + nsub: the state the chunk stored.
+__global__ void __launch_bounds__(1024) k_finalize_dual_multi(const double* partials, int table_rows, int nsub,
+                                                             int slo, int kmax, int na, int n_dead, double eps,
+                                                             Ctrl* ctrl) {
+  if (ctrl->done || ctrl->kstar_found) return;
+  __shared__ double out[kNumSums];
+  __shared__ int stop;
+  const int sp = 2 + 2 * na;
+  if (threadIdx.x == 0) ctrl->kstored = slo + nsub;
+  for (int i = 0; i < nsub; ++i) {
+    reduce_partials(partials + (size_t)i * table_rows * kNumSums, table_rows, sp, out);
+    if (threadIdx.x == 0) {
+      double err = out[0] / out[1];
+      for (int a = 0; a < na; ++a) err += out[2 + 2 * a] / out[3 + 2 * a];
+      for (int a = 0; a < n_dead; ++a) {
+        volatile double z = 0.0;
+        err += z / z;
+      }
+      const int s = slo + i;
+      stop = (err < eps || s + 1 >= kmax) ? 1 : 0;
+      if (stop) {
+        ctrl->kstar = s + 1;
+        ctrl->kstar_found = 1;
+        ctrl->inner_count = s + 1;
+        ctrl->err_inner = err;
+        ctrl->dual_sums[0] = out[0];
+        ctrl->dual_sums[1] = out[1];
+        for (int a = 0; a < na; ++a) {
+          ctrl->dual_sums[3 + 3 * a] = out[2 + 2 * a];
+          ctrl->dual_sums[4 + 3 * a] = out[3 + 2 * a];
+        }
+        if (err < eps) ctrl->inner_done = 1;
+      }
+    }
+    __syncthreads();
+    if (stop) break;
+  }
+}
+
 // k > 1: sums between the outer iteration's initial (cur) and final (1-cur) dual state.
 // partial rows: [0] sum (rho_f - rho_i)^2 [1] unused [2] sum rho_i^2, [3+3a] sum (da)^2, [5+3a] sum a_i^2
 template <typename R>
@@ -154,6 +196,7 @@ __global__ void __launch_bounds__(1024) k_finalize_outer(const double* partials,
     }
     if (flip) ctrl->cur = 1 - ctrl->cur;
     ctrl->inner_done = 0;
+    ctrl->kstar_found = 0;
     ctrl->primal_valid = 0;
   }
 }

@@ -17,6 +17,7 @@
 #include "kernels_2d.hpp"
 #include "kernels_2d_fast.hpp"
 #include "kernels_dual_lds.hpp"
+#include "kernels_dual_multi.hpp"
 #include "kernels_common.hpp"
 #include "kernels_xslab.hpp"
 #include "kernels_xt_batch.hpp"
@@ -123,6 +124,8 @@ struct Impl : ImplBase {
   int half_nt = 3;                        // ny = 4096 row kernels with 512 threads (bit 0 residual, bit 1 update)
   int upd_pf = 4;                         // update kernel (512 threads): old-phi row pairs in flight (1..4)
   bool fast_dual = false;                 // fp32 time-marching float4 dual kernel (k_dual_fast_2d)
+  bool dual_multi = false;   // rho_alp_iters > 1: the dual loop in chunks of sub-iterations (kernels_dual_multi.hpp)
+  static constexpr int kMultiSub = 5;     // sub-iterations one chunk pass runs
   int NTd = 256, gxd = 0, gyd = 0, gzd = 0, jchunk_d = 1;
   int dual_rx = 0;   // > 0: k_dual_lds_2d with dual_rx x rows per workgroup (x neighbours through LDS)
   int dual_ypl = 4;  // y per lane of k_dual_lds_2d (fp64: 4 or 2)
@@ -472,8 +475,19 @@ struct Impl : ImplBase {
       if (const char* e = getenv("PDHG_THOMAS_CHUNK")) thomas_chunk = thomas_chunk && atoi(e) != 0;   // override
     }
     g_outer = 2048;
+    // rho_alp_iters > 1 on the row-per-thread dual grid, single contexts: the dual loop in chunk passes of
+    // kMultiSub sub-iterations in registers (+ a final pass when the exit falls inside a chunk)
+    // Only where a pass is bandwidth-bound: C2's T = 1 marching windows (4 M points, the loop exiting after a few
+    // sub-iterations) ran 30.5 s with the chunks against 22.9 s per sub-iteration (launch-bound: the chunk computes
+    // 5 sub-iterations and the final pass re-runs k*), C2's T = 100 window 22.1 vs 10.5 it/s and C3 5.80 vs
+    // 3.00 it/s (round 4, fp64 / fp32, rho_alp_iters = 10)
+    const bool multi_ok = is2d && two_sets && fast_dual && dual_rx == 0 && !slab && !xslab &&
+                          pb.rho_alp_iters <= kDualMultiMax;
+    dual_multi = multi_ok && (double)T * nx * ny >= (double)(1 << 25);
+    if (const char* e = getenv("PDHG_DUAL_MULTI")) dual_multi = multi_ok && atoi(e) != 0;   // A/B, tests
     partial_rows = std::max<size_t>({(size_t)gx4 * g4, (size_t)gx5 * g5, (size_t)g_outer, (size_t)g_fast_upd,
-                                     (size_t)gxd * gyd * (gzd + 1), fourstep ? (size_t)9 * ((T + 1) / 2) : 1, 1});
+                                     (size_t)gxd * gyd * (gzd + 1), fourstep ? (size_t)9 * ((T + 1) / 2) : 1, 1,
+                                     dual_multi ? (size_t)kMultiSub * gxd * gyd * gzd : (size_t)1});
     p.slab = slab ? 1 : 0;
     p.j0 = slab ? slab_j0 : 0;
     p.Tg = slab ? slab_Tg : T;
@@ -1305,12 +1319,37 @@ struct Impl : ImplBase {
     return gz;
   }
 
+  // the dual loop in chunks of kMultiSub sub-iterations + a final pass when the exit falls inside a chunk
+  // (kernels_dual_multi.hpp); k in [2, kDualMultiMax]
+  template <int EGNO>
+  void launch_dual_multi_e(const KP<R>& p, int k, double eps) {
+    const dim3 g(gxd, gyd, gzd);
+    const int rows = gxd * gyd * gzd;
+    constexpr int NS = kMultiSub;
+    for (int slo = 0; slo < k; slo += NS) {
+      hipLaunchKernelGGL((k_dual_multi_2d<EGNO, R, NS, false>), g, dim3(NTd), 0, stream, p, slo, k, rows, jchunk_d, 0,
+                         pb.T, 0);
+      hipLaunchKernelGGL(k_finalize_dual_multi, dim3(1), dim3(1024), 0, stream, p.partials, rows,
+                         std::min(NS, k - slo), slo, k, na, n_dead, eps, p.ctrl);
+    }
+    hipLaunchKernelGGL((k_dual_multi_2d<EGNO, R, NS, true>), g, dim3(NTd), 0, stream, p, 0, k, rows, jchunk_d, 0, pb.T,
+                       0);
+  }
+
   int launch_dual(R sigma, double eps, int k) {
     KP<R> p = kp;
     p.sigma = sigma;
     p.inplace = (k <= 1) ? 1 : 0;
     if (!p.inplace && !two_sets)
       return fail(PDHG_ERR_STATE, "rho_alp_iters=%d needs a context created with rho_alp_iters > 1", k);
+    if (dual_multi && k > 1 && k <= kDualMultiMax) {
+      ProfScope ps(this, "dual");
+      if (pb.egno == 1) launch_dual_multi_e<1>(p, k, eps);
+      else if (pb.egno == 2) launch_dual_multi_e<2>(p, k, eps);
+      else launch_dual_multi_e<3>(p, k, eps);
+      HIP_TRY(hipGetLastError());
+      return PDHG_OK;
+    }
     for (int s = 0; s < k; ++s) {
       p.sub = s;
       {
@@ -1935,6 +1974,7 @@ struct Impl : ImplBase {
     h.done = 0;
     h.inner_done = 0;
     h.inner_count = 0;
+    h.kstar_found = 0;
     HIP_TRY(hipMemcpy(kp.ctrl, &h, sizeof(Ctrl), hipMemcpyHostToDevice));
     if ((rc = launch_dual((R)sigma, eps, k))) return rc;
     if (primal_done) {
@@ -2198,6 +2238,7 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
     else if (k == "fast_rows") *value = im.fast_rows ? 1 : 0;
     else if (k == "contig_fail") *value = im.n_contig_fail;
     else if (k == "res64") *value = im.res64 ? 1 : 0;
+    else if (k == "dual_multi") *value = im.dual_multi ? 1 : 0;   // rho_alp_iters > 1: chunked dual passes
     else if (k == "dual64") *value = (sizeof(typename std::remove_reference<decltype(im)>::type::Real) == 8 && im.fast_dual) ? 1 : 0;
     else if (k == "fast_dual") *value = im.fast_dual ? im.dual_rx : -1;
     else if (k == "dual_ypl") *value = im.fast_dual && im.dual_rx ? im.dual_ypl : 0;
