@@ -21,6 +21,8 @@
 // sub-iteration loop: states agree to an ulp per sub-iteration, not bitwise (tests/test_gpu_dual_multi.py).
 // Layout and grid as k_dual_fast_2d (a thread owns 4 consecutive y of one x row and marches over t; x
 // neighbours of phi_bar from L2, y neighbours from the adjacent lanes); block 256.
+// The err sums of a sub-iteration are formed over a thread's 4 points in R (as the fused dual's) and accumulated
+// in fp64 over its rows.
 // Partials: table i (sub-iteration SLO + i) at partials + i * table_rows rows of kNumSums doubles; per row
 // [0] sum (rho_s - rho_{s-1})^2 [1] sum rho_s^2, per live alpha a: [2+2a] sum (dalp)^2 [3+2a] sum alp_s^2.
 #pragma once
@@ -101,42 +103,57 @@ __global__ void __launch_bounds__(256) k_dual_multi_2d(KP<R> p, int slo, int kma
       const V pm = zxm ? z4r<R>() : in.pm, pp = zxp ? z4r<R>() : in.pp, pc = in.pc;
       const R pyl = lane_from_prev(pc.w, zym ? (R)0 : in.el);
       const R pyr = lane_from_next(pc.x, zyp ? (R)0 : in.er);
-      V rn4, an4[NA];
+      // the 4 points' phi_bar parts and states, then the sub-iterations over the 4 points together (4 independent
+      // chains per sub-iteration); each sub-iteration's sums over the 4 points in R, then one fp64 add per sum
+      DualPre<R> d[4];
+      R rho[4], al[4][4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const R c = f4(pc, e);
         const R lft = e == 0 ? pyl : f4(pc, e - 1);
         const R rgt = e == 3 ? pyr : f4(pc, e + 1);
-        const DualPre<R> d = dual_pre<R>(p, c, f4(pm, e), f4(pp, e), lft, rgt, f4(f0, e));
-        const R ayc = f4(ay4, e);
-        R rho = f4(in.rho, e), al[4];
+        d[e] = dual_pre<R>(p, c, f4(pm, e), f4(pp, e), lft, rgt, f4(f0, e));
+        rho[e] = f4(in.rho, e);
 #pragma unroll
-        for (int a = 0; a < NA; ++a) al[a] = f4(in.al[a], e);
+        for (int a = 0; a < NA; ++a) al[e][a] = f4(in.al[a], e);
+      }
 #pragma unroll
-        for (int it = 0; it < NIT; ++it) {
-          if (it < nrun) {   // uniform
+      for (int it = 0; it < NIT; ++it) {
+        if (it < nrun) {   // uniform
+          R tf[SP];
+#pragma unroll
+          for (int k = 0; k < SP; ++k) tf[k] = (R)0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
             R an[4];
-            const R rn = dual_core<R, EGNO>(p, d, rho, al, axc, ayc, an);
+            const R rn = dual_core<R, EGNO>(p, d[e], rho[e], al[e], axc, f4(ay4, e), an);
             if constexpr (!FINAL) {
-              double* t = sm[FINAL ? 0 : it];
-              const double dr = (double)rn - (double)rho;
-              t[0] += dr * dr;
-              t[1] += (double)rn * (double)rn;
+              const R dr = rn - rho[e];
+              tf[0] = fmar(dr, dr, tf[0]);
+              tf[1] = fmar(rn, rn, tf[1]);
 #pragma unroll
               for (int a = 0; a < NA; ++a) {
-                const double da = (double)an[a] - (double)al[a];
-                t[2 + 2 * a] += da * da;
-                t[3 + 2 * a] += (double)an[a] * (double)an[a];
+                const R da = an[a] - al[e][a];
+                tf[2 + 2 * a] = fmar(da, da, tf[2 + 2 * a]);
+                tf[3 + 2 * a] = fmar(an[a], an[a], tf[3 + 2 * a]);
               }
             }
-            rho = rn;
+            rho[e] = rn;
 #pragma unroll
-            for (int a = 0; a < NA; ++a) al[a] = an[a];
+            for (int a = 0; a < NA; ++a) al[e][a] = an[a];
+          }
+          if constexpr (!FINAL) {
+#pragma unroll
+            for (int k = 0; k < SP; ++k) sm[FINAL ? 0 : it][k] += (double)tf[k];
           }
         }
-        f4set(rn4, e, rho);
+      }
+      V rn4, an4[NA];
 #pragma unroll
-        for (int a = 0; a < NA; ++a) f4set(an4[a], e, al[a]);
+      for (int e = 0; e < 4; ++e) {
+        f4set(rn4, e, rho[e]);
+#pragma unroll
+        for (int a = 0; a < NA; ++a) f4set(an4[a], e, al[e][a]);
       }
       const size_t o = (size_t)j * plane + rxc + y;
       st4(rd + o, rn4);
