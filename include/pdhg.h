@@ -256,7 +256,7 @@ int pdhg_slab_update(pdhg_ctx* ctx, double tau, double* sums);            /* inv
  * halo_in takes the left neighbour's and the right neighbour's halo_out buffers (periodic ring).
  * wire: [nranks][T][nb/nranks][nloc][B] floats (pdhg_xslab_sizes), chunk q = for / from rank q; stage 0
  * packs the y-transformed rows, 1 unpacks the received rows into whole x lines, 2 packs the
- * preconditioned lines, 3 unpacks them back into rows.  fp32, ndim 2, bc (0,0), power-of-two ny in
+ * preconditioned lines, 3 unpacks them back into rows.  fp32, ndim 2, bc (0,0) or egno 3's (1,0) (the outer slabs' outer ghost rows replicate their edge row), power-of-two ny in
  * [256, 8192], (ny/B) % nranks == 0. */
 int pdhg_create_xslab(const pdhg_problem* p, int rank, int nranks, int device, pdhg_ctx** out);
 int pdhg_xslab_layout(pdhg_ctx* ctx, int* x0, int* nloc, int* nx_local, int* xl0);

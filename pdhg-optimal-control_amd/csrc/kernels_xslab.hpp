@@ -74,10 +74,11 @@ __global__ void __launch_bounds__(256) k_xs_halo_out(KP<R> p, int which, R* __re
 }
 
 // Halo rows in: the left ghost row (xl0 - 1) from the left neighbour's side 1, the right ghost row (xl1)
-// from the right neighbour's side 0 (layouts of k_xs_halo_out).
+// from the right neighbour's side 0 (layouts of k_xs_halo_out).  own_l / own_r (Neumann x edge of the global grid,
+// nb_index bc 1): that ghost replicates the slab's own edge row instead.
 template <typename R>
 __global__ void __launch_bounds__(256) k_xs_halo_in(KP<R> p, int which, const R* __restrict__ from_left,
-                                                    const R* __restrict__ from_right) {
+                                                    const R* __restrict__ from_right, int own_l, int own_r) {
   const int cur = p.ctrl->cur;
   const int nq = which == 0 ? 1 + p.na : 1, nr = p.T;
   const int roff = which == 0 ? 0 : 1;
@@ -89,7 +90,11 @@ __global__ void __launch_bounds__(256) k_xs_halo_in(KP<R> p, int which, const R*
     const int j = (int)(t % nr), q = (int)(t / nr);
     R* a = which == 1 ? p.phibar : (q == 0 ? p.rho[cur] : p.alp[cur][q - 1]);
     const int x = side == 0 ? p.xl0 - 1 : p.xl1;
-    a[(size_t)(j + roff) * plane + (size_t)x * ny + y] = side == 0 ? from_left[half + k] : from_right[k];
+    const size_t rowoff = (size_t)(j + roff) * plane + y;
+    R v;
+    if (side == 0) v = own_l ? a[rowoff + (size_t)p.xl0 * ny] : from_left[half + k];
+    else v = own_r ? a[rowoff + (size_t)(p.xl1 - 1) * ny] : from_right[k];
+    a[rowoff + (size_t)x * ny] = v;
   }
 }
 

@@ -498,9 +498,9 @@ struct Impl : ImplBase {
     p.xl0 = xslab ? 8 : 0;
     p.xl1 = xslab ? 8 + xs_nloc : nx;
     if (xslab) {
-      if (!(is2d && sizeof(R) == 4 && fast_rows && fast_dual && pb.bc_x == 0 && pb.bc_y == 0))
-        return fail(PDHG_ERR_UNSUPPORTED, "x-slab decomposition needs ndim 2, fp32, bc (0,0) and a power-of-two ny "
-                                          "in [256, 8192] (fast row and dual kernels)");
+      if (!(is2d && sizeof(R) == 4 && fast_rows && fast_dual && (pb.bc_x == 0 || pb.bc_x == 1) && pb.bc_y == 0))
+        return fail(PDHG_ERR_UNSUPPORTED, "x-slab decomposition needs ndim 2, fp32, bc (0,0) or (1,0) and a "
+                                          "power-of-two ny in [256, 8192] (fast row and dual kernels)");
       if (p.nb % xs_P) return fail(PDHG_ERR_UNSUPPORTED, "%d column blocks do not split over %d ranks", p.nb, xs_P);
       xs_nbs = p.nb / xs_P;
     }
@@ -1796,8 +1796,11 @@ struct Impl : ImplBase {
   int xs_halo_in(int which, const void* left, const void* right) {
     if (which != 0 && which != 1) return fail(PDHG_ERR_ARG, "unknown halo %d", which);
     const unsigned g = (unsigned)std::max<size_t>(1, std::min<size_t>((xs_halo_elems(which) + 255) / 256, 4096));
+    // Neumann x edges (bc_x 1): the first slab's left ghost and the last slab's right ghost replicate the slab's own
+    // edge row instead of the ring neighbour's
+    const int own_l = (pb.bc_x == 1 && xs_x0 == 0) ? 1 : 0, own_r = (pb.bc_x == 1 && xs_x0 + xs_nloc == xs_nxg) ? 1 : 0;
     hipLaunchKernelGGL((k_xs_halo_in<R>), dim3(g), dim3(256), 0, stream, kp, which, static_cast<const R*>(left),
-                       static_cast<const R*>(right));
+                       static_cast<const R*>(right), own_l, own_r);
     HIP_TRY(hipGetLastError());
     if (which == 0) res_valid = false;
     return PDHG_OK;
@@ -2418,7 +2421,10 @@ int pdhg_create_xslab(const pdhg_problem* prob, int rank, int nranks, int device
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail(PDHG_ERR_ARG, "rank %d of %d", rank, nranks);
   if (prob->precision != 4) return fail(PDHG_ERR_UNSUPPORTED, "x-slab decomposition is fp32 only");
   if (prob->ndim != 2) return fail(PDHG_ERR_UNSUPPORTED, "x-slab decomposition is 2-D only");
-  if (prob->bc_x != 0 || prob->bc_y != 0) return fail(PDHG_ERR_UNSUPPORTED, "x-slab decomposition needs bc (0,0)");
+  // bc (0,0), or egno 3's (1,0): Neumann x edges -- the first / last slab's outer ghost row replicates its own edge
+  // row (nb_index bc 1), the transposed x lines take the DCT of the generic x kernel
+  if (prob->bc_y != 0 || (prob->bc_x != 0 && prob->bc_x != 1))
+    return fail(PDHG_ERR_UNSUPPORTED, "x-slab decomposition needs bc (0,0) or (1,0)");
   if (prob->nx % nranks || (prob->nx / nranks) % 8)
     return fail(PDHG_ERR_UNSUPPORTED, "nx=%d must split into %d slabs of a multiple of 8 rows", prob->nx, nranks);
   // validate the rest exactly like pdhg_create (one row of the global grid), then build the slab
@@ -2439,8 +2445,9 @@ int pdhg_create_xslab(const pdhg_problem* prob, int rank, int nranks, int device
   im->xs_nloc = nloc;
   im->xs_x0 = x0;
   im->xs_local.resize(nxl);
-  for (int i = 0; i < nxl; ++i) {   // local row i = global row x0 - 8 + i (periodic)
-    const int g = ((x0 - 8 + i) % prob->nx + prob->nx) % prob->nx;
+  for (int i = 0; i < nxl; ++i) {   // local row i = global row x0 - 8 + i (periodic; clamped at Neumann edges)
+    const int gi = x0 - 8 + i;
+    const int g = prob->bc_x == 1 ? std::min(std::max(gi, 0), prob->nx - 1) : ((gi % prob->nx) + prob->nx) % prob->nx;
     im->xs_local[i] = prob->xs[g];
   }
   im->pb = *prob;

@@ -30,10 +30,13 @@ ROWS_OUT, COLS_IN, COLS_OUT, ROWS_IN = 0, 1, 2, 3   # pdhg_xslab_wire stages
 
 
 class XSlabContext(PhaseOps, PDHGContext):
-    """Slab `rank` of `nranks` of the global nx rows (fp32, 2-D, bc (0,0)).  nx / xs describe the global grid."""
+    """Slab `rank` of `nranks` of the global nx rows (fp32, 2-D, bc (0,0) or egno 3's (1,0)).  nx / xs describe the
+    global grid."""
 
     def __init__(self, rank, nranks, egno, nx, ny, T, dx, dy, dt, xs, ys, device=0, **kw):
         self.rank, self.nranks, self.nx_global = int(rank), int(nranks), int(nx)
+        bc = kw.get("bc")
+        self.bc_x = int((bc if bc is not None else ((1, 0) if egno == 3 else (0, 0)))[0])
         kw.setdefault("precision", "fp32")
         super().__init__(egno, 2, nx, ny, T, dx, dy, dt, xs, ys, device=device, **kw)
         x0, nloc, nxl, xl0 = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
@@ -52,8 +55,9 @@ class XSlabContext(PhaseOps, PDHGContext):
 
     # ---- local <-> global rows (x is axis 1 of every state array) ----
     def row_index(self):
-        """Global row of every local row (ghost and padding rows wrap periodically)."""
-        return (self.x0 - self.xl0 + np.arange(self.nx)) % self.nx_global
+        """Global row of every local row (ghost and padding rows wrap periodically; Neumann x edges: clamped)."""
+        g = self.x0 - self.xl0 + np.arange(self.nx)
+        return np.clip(g, 0, self.nx_global - 1) if self.bc_x == 1 else g % self.nx_global
 
     def local_rows(self, a):
         return np.take(np.asarray(a), self.row_index(), axis=1)

@@ -114,7 +114,7 @@ def test_xslab_create_validates_before_device(lib):
     for (rank, nranks, kw, code) in [(2, 2, {}, lib.PDHG_ERR_ARG), (0, 0, {}, lib.PDHG_ERR_ARG),
                                      (0, 2, {"precision": 8}, lib.PDHG_ERR_UNSUPPORTED),
                                      (0, 2, {"ndim": 1, "ny": 1}, lib.PDHG_ERR_UNSUPPORTED),
-                                     (0, 2, {"bc_x": 1}, lib.PDHG_ERR_UNSUPPORTED),
+                                     (0, 2, {"bc_x": 2}, lib.PDHG_ERR_UNSUPPORTED),   # Dirichlet x edges
                                      (0, 3, {}, lib.PDHG_ERR_UNSUPPORTED),      # 64 rows / 3
                                      (0, 16, {}, lib.PDHG_ERR_UNSUPPORTED)]:    # 4-row slabs
         p = prob(**kw)

@@ -26,6 +26,11 @@ CASES = [
     (1, 512, 256, 1, 2, 3, 0.0),     # T = 1 with two buffer sets: the row-per-thread dual's live-row mask
     (2, 512, 256, 2, 4, 1, 0.0),     # T = 2: short-window kernels (single-role x transform, row-per-thread dual)
     (2, 512, 256, 8, 2, 1, 0.0),     # T = 8: 8-row LDS dual, single-role x transform
+    # egno 3 (bc (1, 0): Neumann x edges, DCT along x in the generic x kernel on the transposed lines)
+    (3, 512, 256, 1, 2, 1, 0.0),
+    (3, 256, 256, 2, 4, 1, 0.0),     # the inner slabs exchange with both neighbours, the outer ones replicate
+    (3, 384, 256, 1, 2, 3, 0.0),     # non-power-of-two DCT plan, two buffer sets
+    (3, 512, 256, 4, 2, 1, 1e-3),    # (epsl = 0.1 diverges in the single context here: NaN within 6 iterations)
 ]
 
 
