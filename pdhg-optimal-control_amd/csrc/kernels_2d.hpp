@@ -379,10 +379,9 @@ __global__ void __launch_bounds__(NTB) k_invy_update_2d(KP<R> p, F ply, const cp
 // differences of phi_bar at row j+1, HJ residual (:58-70), rho prox (update_rho_2d, :115-119).
 // pc/pxm/pxp/pym/pyp: phi_bar row j+1 at (x, y) and its 4 neighbours (0 outside a Dirichlet edge);
 // f0c: phi_bar row j at (x, y).
-// Split in two: the phi_bar part (dual_pre: the one-sided differences and the time / eps terms of the HJ
-// residual) is the same for every sub-iteration of the dual loop, which keeps phi_bar fixed
-// (update_fns_in_pdhg.py:167-180); dual_core is the per-sub-iteration rest.  dual_point = core(pre(...)), with
-// every expression evaluated in the same order as one function, so both forms give the same bits.
+// The chunked dual loop (kernels_dual_multi.hpp) uses it split in two: the phi_bar part (dual_pre: the one-sided
+// differences and the time / eps terms of the HJ residual) is the same for every sub-iteration of the dual loop,
+// which keeps phi_bar fixed (update_fns_in_pdhg.py:167-180); dual_core is the per-sub-iteration rest.
 template <typename R>
 struct DualPre {
   R DxR, DxL, DyR, DyL, vec0;
@@ -434,10 +433,48 @@ __device__ __forceinline__ R dual_core(const KP<R>& p, const DualPre<R>& d, R rh
   vec = vec - L;
   return nmax<R>(rho + p.sigma * vec, (R)0);
 }
+// the per-sub-iteration kernels' form: one function, the phi_bar terms formed after the controls (the
+// compiler's FMA contraction follows this order; the chunked loop's split form agrees to rounding)
 template <typename R, int EGNO>
 __device__ __forceinline__ R dual_point(const KP<R>& p, R pc, R pxm, R pxp, R pym, R pyp, R f0c, R rho, const R* ao,
                                         R axc, R ayc, R* an, R* fo = nullptr) {
-  return dual_core<R, EGNO>(p, dual_pre<R>(p, pc, pxm, pxp, pym, pyp, f0c), rho, ao, axc, ayc, an, fo);
+  const R DxR = (pxp - pc) * p.inv_dx;
+  const R DxL = (pc - pxm) * p.inv_dx;
+  const R DyR = (pyp - pc) * p.inv_dy;
+  const R DyL = (pc - pym) * p.inv_dy;
+  const R pinv = (rho + (R)1e-4) / p.sigma;              // param_inv, set_fns.py:127 (unused for egno 2)
+  const R q = prox_recip<R, EGNO>(rho, p.sigma, pinv);
+  an[0] = alp_prox<R, EGNO>(ao[0], DxR, axc, pinv, q, true);
+  an[1] = alp_prox<R, EGNO>(ao[1], DxL, axc, pinv, q, false);
+  const R f1x = fpos<R>(fval<R, EGNO>(an[0], axc));
+  const R f2x = fneg<R>(fval<R, EGNO>(an[1], axc));
+  R f1y, f2y, L;
+  if constexpr (EGNO == 3) {
+    f1y = fpos<R>(axc);
+    f2y = fneg<R>(axc);
+    L = lag<R, EGNO>(an[0] * an[0]) + lag<R, EGNO>(an[1] * an[1]);
+  } else {
+    an[2] = alp_prox<R, EGNO>(ao[2], DyR, ayc, pinv, q, true);
+    an[3] = alp_prox<R, EGNO>(ao[3], DyL, ayc, pinv, q, false);
+    f1y = fpos<R>(fval<R, EGNO>(an[2], ayc));
+    f2y = fneg<R>(fval<R, EGNO>(an[3], ayc));
+    L = lag<R, EGNO>(an[0] * an[0]) + lag<R, EGNO>(an[1] * an[1]) + lag<R, EGNO>(an[2] * an[2]) +
+        lag<R, EGNO>(an[3] * an[3]);
+  }
+  R vec = (pc - f0c) * p.inv_dt;
+  if (p.epsl != (R)0) {
+    vec = vec - p.epsl * ((pxp + pxm - (R)2 * pc) * p.inv_dx2);
+    vec = vec - p.epsl * ((pyp + pym - (R)2 * pc) * p.inv_dy2);
+  }
+  if (fo) {   // f1x, f2x, f1y, f2y of the new controls (the next residual's fluxes, :13-47)
+    fo[0] = f1x;
+    fo[1] = f2x;
+    fo[2] = f1y;
+    fo[3] = f2y;
+  }
+  vec = vec - (DxR * f1x + DxL * f2x + DyR * f1y + DyL * f2y);
+  vec = vec - L;
+  return nmax<R>(rho + p.sigma * vec, (R)0);
 }
 
 // grid: (ceil(ny/256), G) where the G workgroup rows stride over the T*nx (j, x) rows; block 256
