@@ -156,7 +156,8 @@ int pdhg_device_bytes(pdhg_ctx* ctx, unsigned long long* bytes);
  * from a physically contiguous allocation to hipMalloc; environment PDHG_ALLOC=contig|none overrides the
  * contiguous-for-fp32-2-D default), "dual64" 1/0 (fp64 contexts: the row-per-thread time-marching dual
  * k_dual_fast_2d<EGNO, double>, or with nx % 8 == 0 and T >= 3 the LDS-row sweep k_dual_lds_2d<EGNO, 8, .., double>;
- * default on where ny % 256 == 0, environment PDHG_DUAL64=0 selects the generic per-point kernel), "f64_xt" 1/0 (fp64 nx = 4096: k_precond_xt_f64_2d), "graph" 1/0 (pdhg_iterate replays
+ * default on where ny % 256 == 0, environment PDHG_DUAL64=0 selects the generic per-point kernel), "f64_xt" 1/0 (fp64 nx = 4096: k_precond_xt_f64_2d), "t1_xt64" 1/0 (fp64 one-row windows at a power-of-two nx in
+ * 512..4096: the carry-free k_precond_x_t1_2d<..., double>; PDHG_T1_XT=0 off), "graph" 1/0 (pdhg_iterate replays
  * windows of iterations from a captured HIP graph; default on, environment PDHG_GRAPH=0 launches every
  * iteration eagerly), "graph_window" (iterations per replayed graph). */
 int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value);

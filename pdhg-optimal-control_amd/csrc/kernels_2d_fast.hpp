@@ -815,19 +815,21 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
   }
 }
 
-// ---- x-transform for a one-row window (T = 1, the reference's marching default; fp32, nx = N) ----
+// ---- x-transform for a one-row window (T = 1, the reference's marching default; nx = N) ----
 // With T = 1 the t-solve is one division per mode (the Neumann row: u = ae (dd + 1), utils_precond.py:164-169),
 // so no carries are kept: forward DHT_x of the block's NL packed lines in LDS, scale every item, write it
 // back as the packed lines, inverse DHT_x (same transform), store.  LDS = the padded lines + twiddle seeds
-// (41 KiB at N = 4096), two workgroups per CU: HIP's second __launch_bounds__ argument is the minimum waves
-// per SIMD, and a 512-thread workgroup puts 2 waves on each SIMD, so 4 guarantees two workgroups (<= 128 VGPRs).
-template <int N, int NL, int NT>
-__global__ void __launch_bounds__(NT, 4) k_precond_x_t1_2d(KP<float> p, const float2* __restrict__ twx) {
-  using C = float2;
+// (fp32: 41 KiB at N = 4096, N * NL = 4096; fp64: N * NL = 2048, or N = 4096 with NL = 1, the column pair of
+// k_precond_xt_f64_2d).  HIP's second __launch_bounds__ argument is the minimum waves per SIMD: 4 keeps the
+// kernel at <= 128 VGPRs, so two 512-thread (four 256-thread) workgroups fit a CU.
+template <int N, int NL, int NT, typename R = float>
+__global__ void __launch_bounds__(NT, 4) k_precond_x_t1_2d(KP<R> p, const cplx<R>* __restrict__ twx) {
+  using C = cplx<R>;
   constexpr int IT = N * NL / NT;
   constexpr int B = 2 * NL;
   constexpr int LINE = Pad<N>::LINE;
   constexpr int lnl = (NL == 1) ? 0 : (NL == 2) ? 1 : (NL == 4) ? 2 : 3;
+  static_assert(IT * NT == N * NL, "whole items per thread");
   if (p.ctrl->done) return;
   extern __shared__ __align__(16) unsigned char smem_raw[];
   C* A = reinterpret_cast<C*>(smem_raw);
@@ -847,16 +849,16 @@ __global__ void __launch_bounds__(NT, 4) k_precond_x_t1_2d(KP<float> p, const fl
   }
   lds_sync();
   lds_fft_inplace_tl<C, N, NL, NT>(A, twl);
-  const float inv_ae = 1.f / p.ae;
+  const R inv_ae = (R)1 / p.ae;
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
     const int item = tid + i * NT;
     const int kx = item >> lnl, l = item & (NL - 1);
-    float ha, hb;
-    hartley_padded<C, float>(A + l * LINE, N, kx, ha, hb);
-    const float lx = p.lamx[kx];
-    const float dd0 = (p.C - lx - p.lamy[b * B + 2 * l]) * inv_ae, dd1 = (p.C - lx - p.lamy[b * B + 2 * l + 1]) * inv_ae;
-    v[i] = make_float2(ha * inv_ae / (dd0 + 1.f), hb * inv_ae / (dd1 + 1.f));
+    R ha, hb;
+    hartley_padded<C, R>(A + l * LINE, N, kx, ha, hb);
+    const R lx = p.lamx[kx];
+    const R dd0 = (p.C - lx - p.lamy[b * B + 2 * l]) * inv_ae, dd1 = (p.C - lx - p.lamy[b * B + 2 * l + 1]) * inv_ae;
+    v[i] = cmk<C>(ha * inv_ae / (dd0 + (R)1), hb * inv_ae / (dd1 + (R)1));
   }
   lds_sync();   // every item has read its Hartley pair
 #pragma unroll
@@ -870,9 +872,9 @@ __global__ void __launch_bounds__(NT, 4) k_precond_x_t1_2d(KP<float> p, const fl
   for (int i = 0; i < IT; ++i) {
     const int item = tid + i * NT;
     const int kx = item >> lnl, l = item & (NL - 1);
-    float ha, hb;
-    hartley_padded<C, float>(A + l * LINE, N, kx, ha, hb);
-    wb[item] = make_float2(ha, hb);
+    R ha, hb;
+    hartley_padded<C, R>(A + l * LINE, N, kx, ha, hb);
+    wb[item] = cmk<C>(ha, hb);
   }
 }
 

@@ -47,8 +47,11 @@ __device__ void reduce_partials(const double* __restrict__ partials, int nrows, 
 
 // First level of a two-level fold for long partial tables: workgroup b reduces rows [b chunk, (b+1) chunk)
 // into row b of out (fixed order, as reduce_partials); the finalize kernels then read gridDim.x rows.
+// ctrl (optional): skip the fold once the dual loop has exited (the per-sub-iteration kernels still launch and
+// return at once; their tables are not read)
 __global__ void __launch_bounds__(1024) k_fold_partials(const double* __restrict__ partials, int nrows, int ns,
-                                                       int chunk, double* __restrict__ out) {
+                                                       int chunk, double* __restrict__ out, const Ctrl* ctrl) {
+  if (ctrl && (ctrl->done || ctrl->inner_done)) return;
   __shared__ double o[kNumSums];
   const int r0 = blockIdx.x * chunk;
   reduce_partials(partials + (size_t)r0 * kNumSums, max(0, min(chunk, nrows - r0)), ns, o);

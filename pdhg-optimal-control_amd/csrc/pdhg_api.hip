@@ -151,6 +151,7 @@ struct Impl : ImplBase {
   int xt_rpre = 0;
   bool xt_pair = false;           // batched x transform as 2 rows x 512 threads, two workgroups per CU
   bool xt_dma = false;            // x transform with the rows staged HBM -> LDS by DMA (k_precond_xt_dma_2d)
+  bool t1_xt64 = false;           // fp64 T = 1 windows: k_precond_x_t1_2d<..., double> (shares PDHG_T1_XT)
   bool f64_xt = false;            // fp64 nx = 4096: in-place line + register carries (k_precond_xt_f64_2d)
   bool thomas_chunk = false;      // 1-D: t-solve in chunks of 32 rows (k_thomas_chunk_1d)
   bool fs_wide = true;            // four-step DHT with 64-column / 32-row tiles (k_fs1w_1d / k_fs2w_1d)
@@ -286,6 +287,9 @@ struct Impl : ImplBase {
       // registers, so the column pair (B = 2) fits LDS although 5 M reals would not
       f64_xt = sizeof(R) == 8 && pb.bc_x == 0 && !xslab && !slab &&
                ((nxg == 4096 && B == 2) || (nxg == 8192 && half_real));
+      // fp64 one-row windows at a power-of-two nx: the carry-free transform needs only the padded lines
+      t1_xt64 = sizeof(R) == 8 && T == 1 && pb.bc_x == 0 && !half_real && !xslab && !slab && plx.pow2 &&
+                nxg >= 512 && nxg <= 4096 && nxg * (B / 2) == (nxg == 4096 ? 4096 : 2048);
       if (!half_real && !f64_xt && (size_t)nxg * B > cap)
         return fail(PDHG_ERR_UNSUPPORTED, "nx=%d too large for the x-transform slab (max %zu in this precision)", nxg,
                     cap / 2);
@@ -942,6 +946,29 @@ struct Impl : ImplBase {
       }
     }
     if constexpr (sizeof(R) == 8) {
+      // fp64 one-row window (the reference's marching default in its own precision): the carry-free x transform,
+      // four 256-thread workgroups per CU.  Measured (C2 marching, nx = 2048, B = 2): the generic kernel took
+      // 156 us per launch
+      if (t1_xt64 && p.T == 1 && !p.slab && p.xt_phase == 0 && t1_xt) {
+        ProfScope ps(this, "precond");
+        const size_t lds = (size_t)((p.B / 2) * (p.nx + p.nx / 16) + twlds_size(p.nx)) * sizeof(C);
+        auto go = [&](auto kern, int nt) -> int {
+          int r2;
+          if ((r2 = ensure_lds(kern, lds))) return r2;
+          hipLaunchKernelGGL(kern, dim3(nblk), dim3(nt), lds, stream, p, twx);
+          return (int)PDHG_OK;
+        };
+        switch (p.nx) {
+          case 4096: rc = go(k_precond_x_t1_2d<4096, 1, 512, double>, 512); break;
+          case 2048: rc = go(k_precond_x_t1_2d<2048, 1, 256, double>, 256); break;
+          case 1024: rc = go(k_precond_x_t1_2d<1024, 2, 512, double>, 512); break;
+          case 512: rc = go(k_precond_x_t1_2d<512, 4, 512, double>, 512); break;
+          default: rc = fail(PDHG_ERR_UNSUPPORTED, "no fp64 one-row x kernel for nx=%d", p.nx);
+        }
+        if (rc) return rc;
+        HIP_TRY(hipGetLastError());
+        return PDHG_OK;
+      }
       if (f64_xt) {
         ProfScope ps(this, "precond");
         if (p.xt_phase != 0 || p.b0 != 0 || nblk != p.nb)
@@ -1376,7 +1403,7 @@ struct Impl : ImplBase {
       if (nrows_d > 2 * kFoldRows * 16) {   // one workgroup reading ~1 MiB of rows took 45-65 us at C1 / C3
         const int chunk = (nrows_d + kFoldRows - 1) / kFoldRows;
         hipLaunchKernelGGL(k_fold_partials, dim3(kFoldRows), dim3(1024), 0, stream, p.partials, nrows_d, 3 + 3 * na,
-                           chunk, fold_out);
+                           chunk, fold_out, p.ctrl);
         rows = fold_out;
         nrows = kFoldRows;
       }
@@ -2262,6 +2289,7 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
     else if (k == "upd_threads") *value = im.fast_rows ? ((im.NTf == 1024 && im.RWf == 8 && (im.half_nt & 2))
                                                               ? 512 : im.NTf) : 0;
     else if (k == "f64_xt") *value = im.f64_xt ? 1 : 0;   // fp64 nx = 4096 x transform (kernels_xt_f64.hpp)
+    else if (k == "t1_xt64") *value = (im.t1_xt64 && im.t1_xt) ? 1 : 0;   // fp64 T = 1: carry-free x transform
     else if (k == "graph") *value = im.use_graph ? 1 : 0;   // iteration windows replayed from a HIP graph
     else if (k == "graph_window") *value = im.gexec ? im.g_window : 0;   // 0: no graph captured yet
     else return fail(PDHG_ERR_ARG, "unknown path key %s", key);

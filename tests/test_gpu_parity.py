@@ -384,6 +384,37 @@ def test_t1_x_transform_fp32(native, case):
     ctx.close()
 
 
+@pytest.mark.parametrize("case", T1_FAST, ids=["e{}d{}_{}x{}_T{}_eps{}".format(*c) for c in T1_FAST])
+def test_t1_x_transform_fp64(native, monkeypatch, case):
+    """The same one-row windows in the reference's precision: k_precond_x_t1_2d<..., double> vs the oracle (primal
+    U <= 1e-12, 10 iterations <= 1e-10) and vs the generic runtime-radix x kernel (PDHG_T1_XT=0) to rounding."""
+    P = make_problem(*case, seeded=False)
+    phi_o = _oracle_primal(P, P["phi"], P["rho"], P["alp"])
+    out = []
+    for t1 in ("1", "0"):
+        monkeypatch.setenv("PDHG_T1_XT", t1)
+        ctx = device_ctx(P, "fp64")
+        try:
+            assert ctx.path_info("t1_xt64") == int(t1)
+            ctx.set_state(P["phi"], P["rho"], P["alp"])
+            ctx.update_primal(TAU)
+            out.append(ctx.get_state()[0])
+        finally:
+            ctx.close()
+    assert rel(out[0], phi_o) < 1e-12 and rel(out[0], out[1]) < 1e-13
+    phi_o, rho_o, _, e1_o, _ = _oracle_iterate(P, 10)
+    monkeypatch.setenv("PDHG_T1_XT", "1")
+    ctx = device_ctx(P, "fp64")
+    try:
+        ctx.set_state(P["phi"], P["rho"], P["alp"])
+        st = ctx.iterate(10, TAU, SIGMA, -1.0, 1)
+        phi_d, rho_d, _ = ctx.get_state()
+    finally:
+        ctx.close()
+    assert rel(phi_d, phi_o) < 1e-10 and rel(rho_d, rho_o) < 1e-10
+    assert abs(st["err1"] - e1_o) <= 1e-8 * e1_o
+
+
 PRECOND_1D = [   # (C, pow, Ct): utils_precond.py:125-134, run_example.py:436-438 flags
     (2.0, 1.0, 1.0), (1.0, 2.0, 1.0), (1.0, 1.0, 0.0), (1.0, 1.0, 2.0), (0.5, 2.0, 0.0), (3.0, 2.0, 2.0)]
 
