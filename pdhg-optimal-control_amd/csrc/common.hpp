@@ -54,6 +54,7 @@ struct Ctrl {
   int kstar;         // chunked dual loop (k_dual_multi_2d): the exit sub-iteration count k*
   int kstar_found;   // ... fixed by a chunk's finalize (reset by k_finalize_outer)
   int kstored;       // ... sub-iterations of the state the second buffer set holds after the last chunk
+  int fold_ticket;   // k_fold_finalize_dual: workgroups done with their fold row (0 between launches)
   double err1, err2, err_inner;
   double s_dphi, s_phi_old, s_phi_new;   // finalized primal sums
   double row0_sq;                        // sum phi_0^2 of the fixed row 0 (written by set_state / init_state)

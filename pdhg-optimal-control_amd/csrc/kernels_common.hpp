@@ -77,12 +77,9 @@ __global__ void __launch_bounds__(1024) k_finalize_primal(const double* partials
 // After dual sub-iteration `sub`: err = sum (drho)^2/sum rho'^2 + sum_a sum (dalp)^2/sum alp'^2
 // (update_fns_in_pdhg.py:162-164); early exit flag when err < eps (:176).  n_dead reference
 // arrays that are not stored (egno 3's y controls, identically zero) contribute 0/0 = NaN.
-__global__ void __launch_bounds__(1024) k_finalize_dual(const double* partials, int nrows, int na, int n_dead,
-                                                       double eps, int sub, Ctrl* ctrl) {
-  if (ctrl->done || ctrl->inner_done) return;
-  __shared__ double out[kNumSums];
+__device__ __forceinline__ void finalize_dual_sums(const double* out, int na, int n_dead, double eps, int sub,
+                                                   Ctrl* ctrl) {
   const int ns = 3 + 3 * na;
-  reduce_partials(partials, nrows, ns, out);
   if (threadIdx.x == 0) {
     double err = out[0] / out[1];
     for (int a = 0; a < na; ++a) err += out[3 + 3 * a] / out[4 + 3 * a];
@@ -99,6 +96,38 @@ __global__ void __launch_bounds__(1024) k_finalize_dual(const double* partials, 
     if (err < eps) ctrl->inner_done = 1;
   }
 }
+__global__ void __launch_bounds__(1024) k_finalize_dual(const double* partials, int nrows, int na, int n_dead,
+                                                       double eps, int sub, Ctrl* ctrl) {
+  if (ctrl->done || ctrl->inner_done) return;
+  __shared__ double out[kNumSums];
+  reduce_partials(partials, nrows, 3 + 3 * na, out);
+  finalize_dual_sums(out, na, n_dead, eps, sub, ctrl);
+}
+
+// The fold and the finalize of a dual sub-iteration in one launch: workgroup b folds its chunk of the table into
+// row b of fold (as k_fold_partials); the last workgroup to finish (ticket in ctrl->fold_ticket, device-scope
+// fences on both sides of it) reduces the gridDim.x rows in fixed order and finalizes (as k_finalize_dual), then
+// re-arms the ticket.  Same sums, same order as the two-launch form; one launch fewer per sub-iteration.
+__global__ void __launch_bounds__(1024) k_fold_finalize_dual(const double* __restrict__ partials, int nrows,
+                                                            int chunk, double* fold, int na, int n_dead, double eps,
+                                                            int sub, Ctrl* ctrl) {
+  if (ctrl->done || ctrl->inner_done) return;
+  __shared__ double o[kNumSums];
+  __shared__ int last;
+  const int ns = 3 + 3 * na;
+  const int r0 = blockIdx.x * chunk;
+  reduce_partials(partials + (size_t)r0 * kNumSums, max(0, min(chunk, nrows - r0)), ns, o);
+  if ((int)threadIdx.x < ns) fold[(size_t)blockIdx.x * kNumSums + threadIdx.x] = o[threadIdx.x];
+  __threadfence();      // release the row before taking a ticket
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(&ctrl->fold_ticket, 1) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();      // acquire the other workgroups' rows
+  reduce_partials(fold, gridDim.x, ns, o);
+  finalize_dual_sums(o, na, n_dead, eps, sub, ctrl);
+  if (threadIdx.x == 0) ctrl->fold_ticket = 0;
+}
 
 // Chunked dual loop (kernels_dual_multi.hpp): after the chunk of sub-iterations slo .. slo + nsub - 1, the first
 // one whose err (as k_finalize_dual, from the table of its sums) is below eps -- or the loop's last,
@@ -107,7 +136,7 @@ __global__ void __launch_bounds__(1024) k_finalize_dual(const double* partials, 
 __global__ void __launch_bounds__(1024) k_finalize_dual_multi(const double* partials, int table_rows, int nsub,
                                                              int slo, int kmax, int na, int n_dead, double eps,
                                                              Ctrl* ctrl) {
-  if (ctrl->done || ctrl->kstar_found) return;
+  if (ctrl->done || ctrl->kstar_found || ctrl->inner_done) return;   // inner_done alone: the head's sub-iteration 0
   __shared__ double out[kNumSums];
   __shared__ int stop;
   const int sp = 2 + 2 * na;
@@ -145,8 +174,11 @@ __global__ void __launch_bounds__(1024) k_finalize_dual_multi(const double* part
 // k > 1: sums between the outer iteration's initial (cur) and final (1-cur) dual state.
 // partial rows: [0] sum (rho_f - rho_i)^2 [1] unused [2] sum rho_i^2, [3+3a] sum (da)^2, [5+3a] sum a_i^2
 template <typename R>
-__global__ void __launch_bounds__(256) k_outer_sums(KP<R> p, size_t n) {
-  if (p.ctrl->done) return;
+// k1_skip: a loop that exited after its first sub-iteration (inner_count == 1) left the initial-vs-final sums in
+// ctrl->outer_sums already (sub-iteration 0 reads the initial state and writes the final one), so the pass is
+// skipped and k_finalize_outer takes those (the same sums up to summation order)
+__global__ void __launch_bounds__(256) k_outer_sums(KP<R> p, size_t n, int k1_skip) {
+  if (p.ctrl->done || (k1_skip && p.ctrl->inner_count == 1)) return;
   const int cur = p.ctrl->cur;
   double s[kNumSums];
   for (int i = 0; i < kNumSums; ++i) s[i] = 0.0;
@@ -169,11 +201,14 @@ __global__ void __launch_bounds__(256) k_outer_sums(KP<R> p, size_t n) {
 }
 
 // End of an outer iteration: err1, err2 (utils_pdhg_solver.py:58-68), stop tests (:74-80).
-// outer_rows > 0: reduce k_outer_sums partials first (k > 1); else use the sub-iteration-0 sums.
+// outer_rows > 0: reduce k_outer_sums partials first (k > 1); else use the sub-iteration-0 sums (also with k1_skip
+// when the dual loop ran one sub-iteration: k_outer_sums skipped).
 __global__ void __launch_bounds__(1024) k_finalize_outer(const double* partials, int outer_rows, int na, double eps,
-                                                        int flip, int stop_conv, int stop_nan, Ctrl* ctrl) {
+                                                        int flip, int stop_conv, int stop_nan, Ctrl* ctrl,
+                                                        int k1_skip = 0) {
   if (ctrl->done) return;
   __shared__ double out[kNumSums];
+  if (k1_skip && ctrl->inner_count == 1) outer_rows = 0;   // uniform: inner_count is not written below
   if (outer_rows > 0) reduce_partials(partials, outer_rows, kNumSums, out);
   if (threadIdx.x == 0) {
     const double* os = (outer_rows > 0) ? out : ctrl->outer_sums;

@@ -19,6 +19,10 @@
 // formed once per pass; every sub-iteration is dual_core, the per-sub-iteration kernels' arithmetic -- up to
 // the compiler's FMA contraction, which differs once the phi_bar products (D * a(x)) are hoisted out of the
 // sub-iteration loop: states agree to an ulp per sub-iteration, not bitwise (tests/test_gpu_dual_multi.py).
+// Head form (the default below 2^25 points per window): sub-iteration 0 through the per-sub-iteration kernel and
+// its finalize, then the chunks from SLO = 1 (they read the state sub-iteration 0 stored) -- a loop that exits after
+// sub-iteration 0 then costs three returning launches instead of 2 (k - 1), and its state is the per-sub-iteration
+// kernels' bit for bit.
 // Layout and grid as k_dual_fast_2d (a thread owns 4 consecutive y of one x row and marches over t; x
 // neighbours of phi_bar from L2, y neighbours from the adjacent lanes); block 256.
 // The err sums of a sub-iteration are formed over a thread's 4 points in R (as the fused dual's) and accumulated
@@ -40,8 +44,9 @@ __global__ void __launch_bounds__(256) k_dual_multi_2d(KP<R> p, int slo, int kma
   constexpr int SP = 2 + 2 * NA;
   constexpr int NIT = FINAL ? kDualMultiMax : NSUB;
   if (p.ctrl->done) return;
-  if (!FINAL && slo > 0 && p.ctrl->kstar_found) return;
-  if (FINAL && p.ctrl->kstar == p.ctrl->kstored) return;   // the stored chunk state is the exit state
+  // inner_done without kstar_found: the head form's sub-iteration 0 (a per-sub-iteration kernel) exited the loop
+  if (!FINAL && slo > 0 && (p.ctrl->kstar_found || p.ctrl->inner_done)) return;
+  if (FINAL && (!p.ctrl->kstar_found || p.ctrl->kstar == p.ctrl->kstored)) return;   // stored state is the exit one
   // sub-iterations this pass runs (uniform)
   const int nrun = FINAL ? p.ctrl->kstar : min(NSUB, kmax - slo);
   const int cur = p.ctrl->cur;

@@ -124,6 +124,13 @@ struct Impl : ImplBase {
   int half_nt = 3;                        // ny = 4096 row kernels with 512 threads (bit 0 residual, bit 1 update)
   int upd_pf = 4;                         // update kernel (512 threads): old-phi row pairs in flight (1..4)
   bool fast_dual = false;                 // fp32 time-marching float4 dual kernel (k_dual_fast_2d)
+  // rho_alp_iters > 1 loops that exit after one sub-iteration (most of C2's marching iterations): no outer-sum
+  // pass, the sub-iteration-0 sums are the outer ones (env PDHG_K1_OUTER=0: always the pass)
+  bool k1_outer = true;
+  // dual sub-iterations with a folded partial table: fold + finalize in one launch (k_fold_finalize_dual; env
+  // PDHG_FOLD_FIN=0: two launches)
+  bool fold_fin = false;
+  bool dual_head = false;    // ... below 2^25 points: sub-iteration 0 alone, the rest in chunks (kernels_dual_multi.hpp)
   bool dual_multi = false;   // rho_alp_iters > 1: the dual loop in chunks of sub-iterations (kernels_dual_multi.hpp)
   static constexpr int kMultiSub = 5;     // sub-iterations one chunk pass runs
   int NTd = 256, gxd = 0, gyd = 0, gzd = 0, jchunk_d = 1;
@@ -324,6 +331,8 @@ struct Impl : ImplBase {
       // so the barrier is not what bounds the sweep and the default stays the barrier
       if (const char* e = getenv("PDHG_DUAL_NBSYNC")) p.nbsync = atoi(e) != 0;
       if (const char* e = getenv("PDHG_T1_XT")) t1_xt = atoi(e) != 0;   // tuning override
+      if (const char* e = getenv("PDHG_K1_OUTER")) k1_outer = atoi(e) != 0;   // tuning override
+      if (const char* e = getenv("PDHG_FOLD_FIN")) fold_fin = atoi(e) != 0;   // tuning override
       // short windows (the reference's T = 1 marching default): few time rows per workgroup leave little to
       // pipeline over t, so occupancy decides.  Measured on C3's grid (bench --config c3w1/c3w4/c3w8): the
       // single-role x-transform kernel beats the warp-specialised one up to T = 8 at least (T = 1: 0.18 vs
@@ -489,9 +498,13 @@ struct Impl : ImplBase {
                           pb.rho_alp_iters <= kDualMultiMax;
     dual_multi = multi_ok && (double)T * nx * ny >= (double)(1 << 25);
     if (const char* e = getenv("PDHG_DUAL_MULTI")) dual_multi = multi_ok && atoi(e) != 0;   // A/B, tests
+    // below that: the head form (sub-iteration 0 per-sub-iteration, the rest in chunks).  C2's marching windows exit
+    // after sub-iteration 0 in nearly every outer iteration, where 18 returning launches cost ~0.2 ms
+    dual_head = multi_ok && !dual_multi;
+    if (const char* e = getenv("PDHG_DUAL_HEAD")) dual_head = multi_ok && !dual_multi && atoi(e) != 0;   // A/B, tests
     partial_rows = std::max<size_t>({(size_t)gx4 * g4, (size_t)gx5 * g5, (size_t)g_outer, (size_t)g_fast_upd,
                                      (size_t)gxd * gyd * (gzd + 1), fourstep ? (size_t)9 * ((T + 1) / 2) : 1, 1,
-                                     dual_multi ? (size_t)kMultiSub * gxd * gyd * gzd : (size_t)1});
+                                     (dual_multi || dual_head) ? (size_t)kMultiSub * gxd * gyd * gzd : (size_t)1});
     p.slab = slab ? 1 : 0;
     p.j0 = slab ? slab_j0 : 0;
     p.Tg = slab ? slab_Tg : T;
@@ -1349,11 +1362,11 @@ struct Impl : ImplBase {
   // the dual loop in chunks of kMultiSub sub-iterations + a final pass when the exit falls inside a chunk
   // (kernels_dual_multi.hpp); k in [2, kDualMultiMax]
   template <int EGNO>
-  void launch_dual_multi_e(const KP<R>& p, int k, double eps) {
+  void launch_dual_multi_e(const KP<R>& p, int k, double eps, int slo0 = 0) {   // slo0 = 1: head form
     const dim3 g(gxd, gyd, gzd);
     const int rows = gxd * gyd * gzd;
     constexpr int NS = kMultiSub;
-    for (int slo = 0; slo < k; slo += NS) {
+    for (int slo = slo0; slo < k; slo += NS) {
       hipLaunchKernelGGL((k_dual_multi_2d<EGNO, R, NS, false>), g, dim3(NTd), 0, stream, p, slo, k, rows, jchunk_d, 0,
                          pb.T, 0);
       hipLaunchKernelGGL(k_finalize_dual_multi, dim3(1), dim3(1024), 0, stream, p.partials, rows,
@@ -1377,7 +1390,9 @@ struct Impl : ImplBase {
       HIP_TRY(hipGetLastError());
       return PDHG_OK;
     }
-    for (int s = 0; s < k; ++s) {
+    // head form: sub-iteration 0 below, then the chunks from sub-iteration 1
+    const bool head = dual_head && k > 1 && k <= kDualMultiMax;
+    for (int s = 0; s < (head ? 1 : k); ++s) {
       p.sub = s;
       {
         ProfScope ps(this, "dual");
@@ -1402,12 +1417,23 @@ struct Impl : ImplBase {
       int nrows = nrows_d;
       if (nrows_d > 2 * kFoldRows * 16) {   // one workgroup reading ~1 MiB of rows took 45-65 us at C1 / C3
         const int chunk = (nrows_d + kFoldRows - 1) / kFoldRows;
+        if (fold_fin) {   // fold + finalize in one launch (the last workgroup finalizes)
+          hipLaunchKernelGGL(k_fold_finalize_dual, dim3(kFoldRows), dim3(1024), 0, stream, p.partials, nrows_d, chunk,
+                             fold_out, na, n_dead, eps, s, p.ctrl);
+          continue;
+        }
         hipLaunchKernelGGL(k_fold_partials, dim3(kFoldRows), dim3(1024), 0, stream, p.partials, nrows_d, 3 + 3 * na,
                            chunk, fold_out, p.ctrl);
         rows = fold_out;
         nrows = kFoldRows;
       }
       hipLaunchKernelGGL(k_finalize_dual, dim3(1), dim3(1024), 0, stream, rows, nrows, na, n_dead, eps, s, p.ctrl);
+    }
+    if (head) {
+      ProfScope ps(this, "dual");
+      if (pb.egno == 1) launch_dual_multi_e<1>(p, k, eps, 1);
+      else if (pb.egno == 2) launch_dual_multi_e<2>(p, k, eps, 1);
+      else launch_dual_multi_e<3>(p, k, eps, 1);
     }
     HIP_TRY(hipGetLastError());
     return PDHG_OK;
@@ -1416,12 +1442,15 @@ struct Impl : ImplBase {
   int launch_outer(double eps, int k) {
     KP<R> p = kp;
     int rows = 0;
+    // the chunked dual loop keeps no sub-iteration-0 outer sums (its tables hold 2 + 2 na sums), so only the
+    // per-sub-iteration kernels skip the outer pass after a one-sub-iteration loop
+    const int k1_skip = (k1_outer && !dual_multi) ? 1 : 0;
     if (k > 1) {
-      hipLaunchKernelGGL((k_outer_sums<R>), dim3(g_outer), dim3(256), 0, stream, p, (size_t)pb.T * plane());
+      hipLaunchKernelGGL((k_outer_sums<R>), dim3(g_outer), dim3(256), 0, stream, p, (size_t)pb.T * plane(), k1_skip);
       rows = g_outer;
     }
     hipLaunchKernelGGL(k_finalize_outer, dim3(1), dim3(1024), 0, stream, p.partials, rows, na, eps, k > 1 ? 1 : 0,
-                       stop_conv, stop_nan, p.ctrl);
+                       stop_conv, stop_nan, p.ctrl, k > 1 ? k1_skip : 0);
     HIP_TRY(hipGetLastError());
     return PDHG_OK;
   }
@@ -1728,7 +1757,7 @@ struct Impl : ImplBase {
   }
   int slab_outer(int k, double* sums) {
     if (k > 1) {
-      hipLaunchKernelGGL((k_outer_sums<R>), dim3(g_outer), dim3(256), 0, stream, kp, (size_t)pb.T * plane());
+      hipLaunchKernelGGL((k_outer_sums<R>), dim3(g_outer), dim3(256), 0, stream, kp, (size_t)pb.T * plane(), 0);
       hipLaunchKernelGGL(k_reduce_vec, dim3(1), dim3(1024), 0, stream, kp.partials, g_outer, kNumSums, 0.0, sums);
     }
     HIP_TRY(hipGetLastError());
@@ -2269,6 +2298,7 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
     else if (k == "contig_fail") *value = im.n_contig_fail;
     else if (k == "res64") *value = im.res64 ? 1 : 0;
     else if (k == "dual_multi") *value = im.dual_multi ? 1 : 0;   // rho_alp_iters > 1: chunked dual passes
+    else if (k == "dual_head") *value = im.dual_head ? 1 : 0;   // ... sub-iteration 0 alone, then the chunks
     else if (k == "dual64") *value = (sizeof(typename std::remove_reference<decltype(im)>::type::Real) == 8 && im.fast_dual) ? 1 : 0;
     else if (k == "fast_dual") *value = im.fast_dual ? im.dual_rx : -1;
     else if (k == "dual_ypl") *value = im.fast_dual && im.dual_rx ? im.dual_ypl : 0;
