@@ -23,8 +23,10 @@
 // its finalize, then the chunks from SLO = 1 (they read the state sub-iteration 0 stored) -- a loop that exits after
 // sub-iteration 0 then costs three returning launches instead of 2 (k - 1), and its state is the per-sub-iteration
 // kernels' bit for bit.
-// Layout and grid as k_dual_fast_2d (a thread owns 4 consecutive y of one x row and marches over t; x
-// neighbours of phi_bar from L2, y neighbours from the adjacent lanes); block 256.
+// Layout as k_dual_fast_2d (a thread owns 4 consecutive y of one x row and marches over t; x neighbours of phi_bar
+// from L2, y neighbours from the adjacent lanes); block 256; a workgroup takes a run of xrun consecutive x rows
+// (grid x = ceil(nx / xrun)): the head form's chunk passes, which return at once after most loops, launch 4x fewer
+// workgroups (a returning 4096-workgroup launch of this kernel took 12 us).
 // The err sums of a sub-iteration are formed over a thread's 4 points in R (as the fused dual's) and accumulated
 // in fp64 over its rows.
 // Partials: table i (sub-iteration SLO + i) at partials + i * table_rows rows of kNumSums doubles; per row
@@ -38,7 +40,7 @@ constexpr int kDualMultiMax = 10;   // rho_alp_iters handled in registers (the r
 
 template <int EGNO, typename R, int NSUB, bool FINAL>
 __global__ void __launch_bounds__(256) k_dual_multi_2d(KP<R> p, int slo, int kmax, int table_rows, int jchunk,
-                                                       int jbase, int jend, int zbase) {
+                                                       int jbase, int jend, int zbase, int xrun) {
   using V = V4<R>;
   constexpr int NA = (EGNO == 3) ? 2 : 4;
   constexpr int SP = 2 + 2 * NA;
@@ -52,7 +54,7 @@ __global__ void __launch_bounds__(256) k_dual_multi_2d(KP<R> p, int slo, int kma
   const int cur = p.ctrl->cur;
   const int nx = p.nx, ny = p.ny;
   const size_t plane = (size_t)nx * ny;
-  const int x = xcd_remap(blockIdx.x, gridDim.x);
+  const int xb = xcd_remap(blockIdx.x, gridDim.x);   // x rows [xb xrun, xb xrun + xrun): a run per workgroup
   const int y = 4 * (blockIdx.y * blockDim.x + threadIdx.x);
   const int j0 = jbase + blockIdx.z * jchunk;
   const int j1 = min(jend, j0 + jchunk);
@@ -61,6 +63,8 @@ __global__ void __launch_bounds__(256) k_dual_multi_2d(KP<R> p, int slo, int kma
   for (int i = 0; i < (FINAL ? 1 : NSUB); ++i)
 #pragma unroll
     for (int k = 0; k < SP; ++k) sm[i][k] = 0.0;
+#pragma unroll 1
+  for (int x = xb * xrun; x < min(nx, xb * xrun + xrun); ++x) {
   if (y < ny) {
     const int yw0 = __builtin_amdgcn_readfirstlane(y);
     const int ywm = nb_index(yw0 - 1, ny, p.bcy), ywp = nb_index(yw0 + 4 * kWave, ny, p.bcy);
@@ -167,6 +171,7 @@ __global__ void __launch_bounds__(256) k_dual_multi_2d(KP<R> p, int slo, int kma
       f0 = pc;
     }
   }
+  }   // x run
   if constexpr (!FINAL) {
     const int row = ((zbase + (int)blockIdx.z) * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
 #pragma unroll

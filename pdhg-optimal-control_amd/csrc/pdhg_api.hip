@@ -1363,17 +1363,20 @@ struct Impl : ImplBase {
   // (kernels_dual_multi.hpp); k in [2, kDualMultiMax]
   template <int EGNO>
   void launch_dual_multi_e(const KP<R>& p, int k, double eps, int slo0 = 0) {   // slo0 = 1: head form
-    const dim3 g(gxd, gyd, gzd);
-    const int rows = gxd * gyd * gzd;
+    // head form: runs of 4 x rows per workgroup (its passes mostly return at once; fewer workgroups to retire)
+    const int xrun = (slo0 > 0 && pb.nx % 4 == 0) ? 4 : 1;
+    const int gx = (pb.nx + xrun - 1) / xrun;
+    const dim3 g(gx, gyd, gzd);
+    const int rows = gx * gyd * gzd;
     constexpr int NS = kMultiSub;
     for (int slo = slo0; slo < k; slo += NS) {
       hipLaunchKernelGGL((k_dual_multi_2d<EGNO, R, NS, false>), g, dim3(NTd), 0, stream, p, slo, k, rows, jchunk_d, 0,
-                         pb.T, 0);
+                         pb.T, 0, xrun);
       hipLaunchKernelGGL(k_finalize_dual_multi, dim3(1), dim3(1024), 0, stream, p.partials, rows,
                          std::min(NS, k - slo), slo, k, na, n_dead, eps, p.ctrl);
     }
     hipLaunchKernelGGL((k_dual_multi_2d<EGNO, R, NS, true>), g, dim3(NTd), 0, stream, p, 0, k, rows, jchunk_d, 0, pb.T,
-                       0);
+                       0, xrun);
   }
 
   int launch_dual(R sigma, double eps, int k) {
@@ -1904,18 +1907,26 @@ struct Impl : ImplBase {
     const size_t npl = plane();
     const int T = pb.T;
     const int cur = 0;
-    std::vector<R> buf((size_t)(T + 1) * npl);
+    const size_t nphi = (size_t)(T + 1) * npl;
+    std::unique_ptr<R[]> buf(new R[nphi]);   // not value-initialised: filled before every copy out of it
+    // fp64 planes straight from the caller's arrays (same layout); fp32 through a narrowing copy
+    auto src_of = [&](const double* p, size_t cnt) -> const R* {
+      if constexpr (sizeof(R) == 8) {
+        (void)cnt;
+        return p;
+      } else {
+        for (size_t i = 0; i < cnt; ++i) buf[i] = (R)p[i];
+        return buf.get();
+      }
+    };
     if (phi) {
-      for (size_t i = 0; i < buf.size(); ++i) buf[i] = (R)phi[i];
-      HIP_TRY(hipMemcpy(kp.phi, buf.data(), buf.size() * sizeof(R), hipMemcpyHostToDevice));
-      HIP_TRY(hipMemcpy(kp.phibar, buf.data(), buf.size() * sizeof(R), hipMemcpyHostToDevice));
-      compute_row0_sq(std::vector<R>(buf.begin(), buf.begin() + npl));
+      const R* src = src_of(phi, nphi);
+      HIP_TRY(hipMemcpy(kp.phi, src, nphi * sizeof(R), hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(kp.phibar, src, nphi * sizeof(R), hipMemcpyHostToDevice));
+      compute_row0_sq(std::vector<R>(src, src + npl));
     }
     const size_t n = (size_t)T * npl;
-    if (rho) {
-      for (size_t i = 0; i < n; ++i) buf[i] = (R)rho[i];
-      HIP_TRY(hipMemcpy(kp.rho[cur], buf.data(), n * sizeof(R), hipMemcpyHostToDevice));
-    }
+    if (rho) HIP_TRY(hipMemcpy(kp.rho[cur], src_of(rho, n), n * sizeof(R), hipMemcpyHostToDevice));
     if (alp) {
       const int nc = n_ctrl(), nar = n_alp_ref();
       for (int a = 0; a < nar; ++a)
@@ -1930,7 +1941,7 @@ struct Impl : ImplBase {
         for (int c = 0; c < nc; ++c) {
           if (!live(a, c, nc)) continue;
           for (size_t i = 0; i < n; ++i) buf[i] = (R)alp[((size_t)a * n + i) * nc + c];
-          HIP_TRY(hipMemcpy(kp.alp[cur][a], buf.data(), n * sizeof(R), hipMemcpyHostToDevice));
+          HIP_TRY(hipMemcpy(kp.alp[cur][a], buf.get(), n * sizeof(R), hipMemcpyHostToDevice));
         }
     }
     Ctrl h{};
@@ -1966,23 +1977,28 @@ struct Impl : ImplBase {
     const int cur = h.cur;
     const size_t npl = plane();
     const int T = pb.T;
-    std::vector<R> buf((size_t)(T + 1) * npl);
-    if (phi) {
-      HIP_TRY(hipMemcpy(buf.data(), kp.phi, buf.size() * sizeof(R), hipMemcpyDeviceToHost));
-      for (size_t i = 0; i < buf.size(); ++i) phi[i] = (double)buf[i];
-    }
+    const size_t nphi = (size_t)(T + 1) * npl;
+    std::unique_ptr<R[]> buf(new R[nphi]);   // not value-initialised: every element read is copied in first
     const size_t n = (size_t)T * npl;
-    if (rho) {
-      HIP_TRY(hipMemcpy(buf.data(), kp.rho[cur], n * sizeof(R), hipMemcpyDeviceToHost));
-      for (size_t i = 0; i < n; ++i) rho[i] = (double)buf[i];
-    }
+    // fp64 planes straight into the caller's arrays (same layout); fp32 through the buffer and a widening copy
+    auto plane_out = [&](double* dst, const R* src, size_t cnt) -> int {
+      if constexpr (sizeof(R) == 8) {
+        HIP_TRY(hipMemcpy(dst, src, cnt * sizeof(R), hipMemcpyDeviceToHost));
+      } else {
+        HIP_TRY(hipMemcpy(buf.get(), src, cnt * sizeof(R), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < cnt; ++i) dst[i] = (double)buf[i];
+      }
+      return PDHG_OK;
+    };
+    if (phi && (rc = plane_out(phi, kp.phi, nphi))) return rc;
+    if (rho && (rc = plane_out(rho, kp.rho[cur], n))) return rc;
     if (alp) {
       const int nc = n_ctrl(), nar = n_alp_ref();
       std::memset(alp, 0, sizeof(double) * n * nc * nar);
       for (int a = 0; a < nar; ++a)
         for (int c = 0; c < nc; ++c) {
           if (!live(a, c, nc)) continue;
-          HIP_TRY(hipMemcpy(buf.data(), kp.alp[cur][a], n * sizeof(R), hipMemcpyDeviceToHost));
+          HIP_TRY(hipMemcpy(buf.get(), kp.alp[cur][a], n * sizeof(R), hipMemcpyDeviceToHost));
           for (size_t i = 0; i < n; ++i) alp[((size_t)a * n + i) * nc + c] = (double)buf[i];
         }
     }

@@ -73,12 +73,13 @@ class PDHGContext:
             alp = alp.reshape((self.n_alp, self.T) + self._space + (self.n_ctrl,))
         N.check(self._lib.pdhg_set_state(self._h, N.dptr(phi), N.dptr(rho), N.dptr(alp)))
 
-    def get_state(self):
-        phi = np.empty((self.T + 1,) + self._space)
-        rho = np.empty((self.T,) + self._space)
-        alp = np.empty((self.n_alp, self.T) + self._space + (self.n_ctrl,))
+    def get_state(self, phi=True, rho=True, alp=True):
+        """(phi, rho, alp) from the device; a part passed as False is not copied and comes back as None."""
+        phi = np.empty((self.T + 1,) + self._space) if phi else None
+        rho = np.empty((self.T,) + self._space) if rho else None
+        alp = np.empty((self.n_alp, self.T) + self._space + (self.n_ctrl,)) if alp else None
         N.check(self._lib.pdhg_get_state(self._h, N.dptr(phi), N.dptr(rho), N.dptr(alp)))
-        return phi, rho, tuple(alp[i] for i in range(self.n_alp))
+        return phi, rho, (None if alp is None else tuple(alp[i] for i in range(self.n_alp)))
 
     def get_phi_bar(self):
         pb = np.empty((self.T + 1,) + self._space)

@@ -55,12 +55,16 @@ def _device_oneiter(tag, fns_dict, phi0, rho0, alp0, x_arr, ndim, dt, dspatial, 
     last = None
     while i < N_maxiter:
         if print_freq > 0 and i % print_freq == 0:
-            phi_prev, rho_prev, _ = ctx.get_state()
+            if i == 0:   # the state just set: the caller's arrays (as the reference records them), no device copy
+                phi_prev = phi0.copy()
+                rho_prev = np.array(rho0, dtype=np.float64).reshape((T,) + phi0.shape[1:])
+            else:
+                phi_prev, rho_prev, _ = ctx.get_state(alp=False)
             st = ctx.iterate(1, tau, sigma, eps, k)
             last = st
             if st["status"] != 0:
                 break
-            _, _, alp_next = ctx.get_state()
+            _, _, alp_next = ctx.get_state(phi=False, rho=False)
             error = np.array([st["err1"], st["err2"]])
             results_all.append((i, phi_prev, rho_prev, alp_next))
             error_all.append(error)
