@@ -103,6 +103,11 @@ int pdhg_destroy(pdhg_ctx* ctx);
 int pdhg_set_state(pdhg_ctx* ctx, const double* phi, const double* rho, const double* alp);
 int pdhg_get_state(pdhg_ctx* ctx, double* phi, double* rho, double* alp);
 int pdhg_get_phi_bar(pdhg_ctx* ctx, double* phi_bar);   /* [T+1][nx][ny] */
+/* Rows [row0, row0 + nrows) of the state in the reference layouts (a window of 3.4e9 points per array, C3's and
+ * C4's, does not fit a host copy): phi / phi_bar rows of [T+1] -> [nrows][nx][ny], rho rows of [T] -> [nrows][nx][ny],
+ * alp -> [n_alp][nrows][nx][ny][n_ctrl] (dead components zero).  Null pointers are skipped; rho / alp need
+ * row0 + nrows <= T.  Same values as the matching rows of pdhg_get_state / pdhg_get_phi_bar. */
+int pdhg_get_rows(pdhg_ctx* ctx, int row0, int nrows, double* phi, double* phi_bar, double* rho, double* alp);
 /* phi_bar input of the drop-in dual update (update_dual_oneiter's first argument). */
 int pdhg_set_phi_bar(pdhg_ctx* ctx, const double* phi_bar);
 
@@ -197,12 +202,16 @@ int pdhg_algorithmic_bytes(pdhg_ctx* ctx, int k, const char* kernel_class, doubl
  * row unless this is the window's last slab; dual: row 0 unless it is the first slab, then the sums).
  * The Thomas recurrences are affine in the carries entering a slab (oracle/slab_oracle.py): D = the
  * zero-carry forward sweep's last row, S1 = sum P'_k b0_k; allGS: every slab's [G, S2]
- * (pdhg_slab_carry_gain, iteration-invariant, gather once).  Planes are device pointers (float; D/S1 and
- * G/S2 are pairs of spectral planes, see pdhg_slab_plane_size); sums are device vectors of 16 doubles.
+ * (pdhg_slab_carry_gain, iteration-invariant, gather once).  Planes are device pointers in the context's
+ * precision (float for p->precision 4, double for 8; D/S1 and G/S2 are pairs of spectral planes, see
+ * pdhg_slab_plane_size); sums are device vectors of 16 doubles.
  * All calls enqueue on the context's stream (pdhg_set_stream to share the caller's).
- * fp32, ndim 2, a power-of-two ny in [256, 8192] (the residual's halo-row split runs the fast row kernels); any nx
- * the single context supports: the fast DHT x kernels, or the generic runtime-radix kernel (other nx, and egno 3's
- * bc (1,0) DCT along x, jaxsrc/utils/utils_precond.py:159-174). */
+ * ndim 2.  fp32: a power-of-two ny in [256, 8192] (the residual's halo-row split runs the fast row kernels).
+ * fp64 (the reference's arithmetic, jaxsrc/update_fns_in_pdhg.py:10): any ny; ny = 2048 / 4096 split the halo row
+ * off with the 4-row kernels, other ny run the generic row kernels over the whole slab after the halo.  Any nx
+ * the single context supports: the fast DHT x kernels (fp32), the fp64 nx = 4096 kernel and its half-real
+ * nx = 8192 form (kernels_xt_f64.hpp), or the generic runtime-radix kernel (other nx, and egno 3's bc (1,0) DCT
+ * along x, jaxsrc/utils/utils_precond.py:159-174). */
 int pdhg_create_slab(const pdhg_problem* p, int j0, int T_total, int device, pdhg_ctx** out);
 int pdhg_set_stream(pdhg_ctx* ctx, void* hip_stream);
 int pdhg_slab_plane_size(pdhg_ctx* ctx, unsigned long long* spatial, unsigned long long* spectral);
@@ -277,9 +286,10 @@ int pdhg_xslab_update(pdhg_ctx* ctx, double tau, double* sums);            /* in
  * sums folded in slab order on the first device, so a C / Go / Java caller gets the multi-GPU window without
  * re-implementing pdhg_amd/slab.py or linking RCCL.  The window's rows [0, p->T) are split near-equally
  * (the first T % ndev slabs get one more row).  State arrays are the WHOLE window in the reference layouts
- * (as pdhg_set_state / pdhg_get_state).  Same support as the t-slab (fp32, ndim 2, bc (0,0) or egno 3's (1,0)).
- * The stop-test sums are folded on every device from its peers' buffers when all device pairs have peer
- * access (environment PDHG_MULTI_PEER_FOLD=0: gathered on the first device and copied back).
+ * (as pdhg_set_state / pdhg_get_state).  Same support as the t-slab (fp32 or fp64, ndim 2, bc (0,0) or egno 3's
+ * (1,0)).  The stop-test sums are gathered on the first device, folded in slab order and copied back; with
+ * PDHG_MULTI_PEER_FOLD=1 (and peer access between every device pair) each device folds them from its peers'
+ * buffers instead (opt-in until validated on separate devices).
  * Keys of pdhg_multi_info: "ndev", "long_modes", "rows:<i>" (rows of slab i), "peer_fold". */
 typedef struct pdhg_multi pdhg_multi;
 int pdhg_create_multi(const pdhg_problem* p, const int* devices, int ndev, pdhg_multi** out);

@@ -51,7 +51,8 @@ __device__ __forceinline__ double theta_of(double dd) {
 // z[m] = x[2m] + i x[2m+1] into the N-point FFT and split with realsplit_padded (the fp32 warp-specialised kernel's
 // HR form); item k carries the modes kx = k and k + N, and the inverse stages x of both modes at their real positions
 // and splits again.  The split twiddles W_{2N}^k come from two 64-entry LDS tables (W^(k mod 64) W^(64 (k/64))).
-// Single context only (no t-slab phases: the slab decomposition is fp32).
+// t-slab phases (p.slab, xt_phase 1 / 2) as in the fp32 kernels: global-row pivots, zero-carry forward sweep
+// storing every row, backward sweep from the right carry (carry_y) -- oracle/slab_oracle.py.
 // grid: nb column blocks; block NT; LDS (N + N/16 + TwLds<N> + N (+ 128 HR)) * 16 B.
 template <int N, int NT, bool HR = false>
 __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const double2* __restrict__ twx) {
@@ -72,7 +73,7 @@ __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const do
     for (int i = threadIdx.x; i < 128; i += blockDim.x) rsw[i] = twx[i < 64 ? i : 64 * (i - 64)];
   }
   const int T = p.T, tid = threadIdx.x;
-  const int b = blockIdx.x;
+  const int b = blockIdx.x + p.b0;   // t-slab carry exchange: blocks [b0, b0 + gridDim.x)
   double* wb = p.work + (size_t)b * M;
   const size_t kstride = (size_t)p.nb * M;
   const double inv_ae = 1.0 / (double)p.ae;
@@ -125,87 +126,105 @@ __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const do
 #pragma unroll
     for (int i = 0; i < IT; ++i) pf[i] = buf_ld2(r, voff, i * NT * (int)sizeof(C));
   };
-#pragma unroll
-  for (int i = 0; i < IT; ++i) {
-    c1[i] = dd_of(i);
-    c2[i] = make_double2(1.0, 1.0);   // h_{-1} = 1: the first row's pivot is dd + 2
-    bp[kx_of(i)] = make_double2(0.0, 0.0);
-  }
-  // ---------------- forward: DHT_x + elimination ----------------
-  //   s = dd + h_{k-1},  g_k = 1/(1+s),  h_k = s g_k,  b'_k = (rhs/ae + b'_{k-1}) g_k
-  //   last (Neumann) row: x_{T-1} = (rhs/ae + b'_{T-2}) / (dd + h_{T-2})   [converged: dd + h = (1 - g)/g]
-  ldrow(0);
-  for (int k = 0; k < T; ++k) {
-#pragma unroll
-    for (int i = 0; i < IT; ++i) A[pix(kx_of(i))] = pf[i];
-    if (k + 1 < T) ldrow(k + 1);
-    lds_sync();
-    lds_fft_inplace_tl<C, N, 1, NT>(A, twl);
-#pragma unroll
-    for (int i = 0; i < IT; ++i)   // items whose pivots have converged switch to g = e^-th (dd -> e^-th)
-      if (k == kf[i] && k < T - 1) c1[i] = make_double2(eth_of(c1[i].x), eth_of(c1[i].y));
-    const auto dst = rowr(k);
+  const int j0 = p.j0;
+  const bool slab = p.slab != 0;
+  if (p.xt_phase != 2) {
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
-      const int kx = kx_of(i);
-      double ha, hb;
-      unpack2(i, ha, hb);
-      const C b0 = bp[kx];
-      const double r0 = ha * inv_ae + b0.x, r1 = hb * inv_ae + b0.y;
-      C bn;
-      const bool fast = k > kf[i] || (k == kf[i] && k < T - 1);
-      if (k < T - 1) {
-        if (fast) {
-          bn = make_double2(r0 * c1[i].x, r1 * c1[i].y);
-        } else {
-          const double s0 = c1[i].x + c2[i].x, s1 = c1[i].y + c2[i].y;
-          const double g0 = 1.0 / (1.0 + s0), g1 = 1.0 / (1.0 + s1);
-          bn = make_double2(r0 * g0, r1 * g1);
-          c2[i] = make_double2(s0 * g0, s1 * g1);
-        }
-        buf_st2(dst, voff, i * NT * (int)sizeof(C), bn);
-      } else if (fast) {
-        bn = make_double2(r0 * c1[i].x / (1.0 - c1[i].x), r1 * c1[i].y / (1.0 - c1[i].y));
-      } else {
-        bn = make_double2(r0 / (c1[i].x + c2[i].x), r1 / (c1[i].y + c2[i].y));
-      }
-      bp[kx] = bn;
+      c1[i] = dd_of(i);
+      // h_{j0-1}: 1 entering the window; a t-slab's entry pivot state in closed form (h_entry)
+      c2[i] = slab ? make_double2(h_entry(c1[i].x, j0), h_entry(c1[i].y, j0)) : make_double2(1.0, 1.0);
+      bp[kx_of(i)] = make_double2(0.0, 0.0);   // zero carry (a t-slab's carry is folded in by k_slab_fix)
     }
-    lds_sync();
+    // ---------------- forward: DHT_x + elimination ----------------
+    //   s = dd + h_{k-1},  g_k = 1/(1+s),  h_k = s g_k,  b'_k = (rhs/ae + b'_{k-1}) g_k
+    //   last (Neumann) row of the window: x_{T-1} = (rhs/ae + b'_{T-2}) / (dd + h_{T-2})   [converged: dd + h = (1 - g)/g]
+    // A t-slab indexes the pivots by the GLOBAL row j0 + k; only the window's last slab has the Neumann row, and
+    // a slab stores every row (the backward sweep is a separate launch after the carry fix-up).
+    ldrow(0);
+    for (int k = 0; k < T; ++k) {
+      const int kg = j0 + k;
+      const bool nrow = k == T - 1 && p.last_slab;   // the window's Neumann row
+#pragma unroll
+      for (int i = 0; i < IT; ++i) A[pix(kx_of(i))] = pf[i];
+      if (k + 1 < T) ldrow(k + 1);
+      lds_sync();
+      lds_fft_inplace_tl<C, N, 1, NT>(A, twl);
+#pragma unroll
+      for (int i = 0; i < IT; ++i)   // items whose pivots have converged switch to g = e^-th (dd -> e^-th) on
+        if (kg == max(kf[i], j0) && !nrow)   // the first converged row of this sweep (a slab may start past kf)
+          c1[i] = make_double2(eth_of(c1[i].x), eth_of(c1[i].y));
+      const auto dst = rowr(k);
+#pragma unroll
+      for (int i = 0; i < IT; ++i) {
+        const int kx = kx_of(i);
+        double ha, hb;
+        unpack2(i, ha, hb);
+        const C b0 = bp[kx];
+        const double r0 = ha * inv_ae + b0.x, r1 = hb * inv_ae + b0.y;
+        C bn;
+        const int kfj = max(kf[i], j0);
+        const bool fast = kg > kfj || (kg == kfj && !nrow);
+        if (!nrow) {
+          if (fast) {
+            bn = make_double2(r0 * c1[i].x, r1 * c1[i].y);
+          } else {
+            const double s0 = c1[i].x + c2[i].x, s1 = c1[i].y + c2[i].y;
+            const double g0 = 1.0 / (1.0 + s0), g1 = 1.0 / (1.0 + s1);
+            bn = make_double2(r0 * g0, r1 * g1);
+            c2[i] = make_double2(s0 * g0, s1 * g1);
+          }
+          buf_st2(dst, voff, i * NT * (int)sizeof(C), bn);
+        } else {
+          if (fast) bn = make_double2(r0 * c1[i].x / (1.0 - c1[i].x), r1 * c1[i].y / (1.0 - c1[i].y));
+          else bn = make_double2(r0 / (c1[i].x + c2[i].x), r1 / (c1[i].y + c2[i].y));
+          if (slab) buf_st2(dst, voff, i * NT * (int)sizeof(C), bn);   // re-read after the carry fix-up
+        }
+        bp[kx] = bn;
+      }
+      lds_sync();
+    }
   }
+  if (p.xt_phase == 1) return;   // forward sweep only (t-slab: the carry fix-up runs in between)
   // ---------------- backward: substitution + inverse DHT_x ----------------
   //   x_k = b'_k + g_k x_{k+1},  g_k = e^-th E_{k+1}/E_{k+2},  E_m = expm1(-2 th m),  cosh th = 1 + dd/2
   //   (th -> 0: g_k -> (k+1)/(k+2)); converged: g = e^-th
+  // single context: from x_{T-1} (the forward's Neumann row, held in bp); t-slab: from the right carry x_{j0+T}
+  // (carry_y, written by k_slab_fix), substituting every local row from the fixed-up b' rows in work
+  const int ks = slab ? T - 1 : T - 2;   // first substituted local row
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
     const C dd = dd_of(i);
     c1[i] = make_double2(theta_of(dd.x), theta_of(dd.y));
-    if (T - 2 >= kf[i]) {   // row T-2 converged
+    if (j0 + ks >= kf[i]) {   // row ks converged
       c2[i] = make_double2(exp(-c1[i].x), exp(-c1[i].y));
-    } else {                // E_{k+2} for the first substituted row, k = T-2
-      c2[i] = make_double2(expm1(-2.0 * c1[i].x * T), expm1(-2.0 * c1[i].y * T));
+    } else {                  // E_{k+2} for the first substituted row, k = ks (global j0 + ks)
+      c2[i] = make_double2(expm1(-2.0 * c1[i].x * (j0 + ks + 2)), expm1(-2.0 * c1[i].y * (j0 + ks + 2)));
     }
+    if (slab) bp[kx_of(i)] = p.carry_y ? reinterpret_cast<const C*>(p.carry_y + (size_t)b * M)[kx_of(i)]
+                                       : make_double2(0.0, 0.0);
   }
-  if (T >= 2) ldrow(T - 2);
+  if (ks >= 0) ldrow(ks);
   for (int k = T - 1; k >= 0; --k) {
+    const int kg = j0 + k;
 #pragma unroll
     for (int i = 0; i < IT; ++i)   // items leaving the converged regime: E_{k+2} from theta
-      if (k + 1 == kf[i] && k < T - 2)
-        c2[i] = make_double2(expm1(-2.0 * c1[i].x * (k + 2)), expm1(-2.0 * c1[i].y * (k + 2)));
+      if (kg + 1 == kf[i] && k < ks)
+        c2[i] = make_double2(expm1(-2.0 * c1[i].x * (kg + 2)), expm1(-2.0 * c1[i].y * (kg + 2)));
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       const int kx = kx_of(i);
       C x = bp[kx];
-      if (k < T - 1) {
+      if (k <= ks) {
         double g0, g1;
-        if (k >= kf[i]) {
+        if (kg >= kf[i]) {
           g0 = c2[i].x;
           g1 = c2[i].y;
         } else {
           const double t0 = c1[i].x, t1 = c1[i].y;
-          const double e0 = expm1(-2.0 * t0 * (k + 1)), e1 = expm1(-2.0 * t1 * (k + 1));
-          g0 = t0 > 1e-150 ? exp(-t0) * e0 / c2[i].x : (double)(k + 1) / (double)(k + 2);
-          g1 = t1 > 1e-150 ? exp(-t1) * e1 / c2[i].y : (double)(k + 1) / (double)(k + 2);
+          const double e0 = expm1(-2.0 * t0 * (kg + 1)), e1 = expm1(-2.0 * t1 * (kg + 1));
+          g0 = t0 > 1e-150 ? exp(-t0) * e0 / c2[i].x : (double)(kg + 1) / (double)(kg + 2);
+          g1 = t1 > 1e-150 ? exp(-t1) * e1 / c2[i].y : (double)(kg + 1) / (double)(kg + 2);
           c2[i] = make_double2(e0, e1);
         }
         x = make_double2(pf[i].x + g0 * x.x, pf[i].y + g1 * x.y);
@@ -213,7 +232,7 @@ __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const do
       }
       stage2(i, x);
     }
-    if (k < T - 1 && k >= 1) ldrow(k - 1);
+    if (k <= ks && k >= 1) ldrow(k - 1);
     lds_sync();
     lds_fft_inplace_tl<C, N, 1, NT>(A, twl);
     const auto wk = rowr(k);

@@ -288,11 +288,12 @@ struct Impl : ImplBase {
       if (B > nyp) B = nyp;
       // fp32 nx = 8192 (C4): one real column per block, packed into a 4096-point FFT (half_real)
       // fp64 nx = 8192 (C4's grid in the reference's precision): the same half-real split in k_precond_xt_f64_2d<HR>
-      half_real = nxg == 8192 && pb.bc_x == 0 && (sizeof(R) == 4 || (!xslab && !slab));
+      half_real = nxg == 8192 && pb.bc_x == 0 && (sizeof(R) == 4 || !xslab);
       if (half_real) B = 1;
       // fp64 nx = 4096 (C3's grid in the reference's precision): k_precond_xt_f64_2d keeps the carries in
       // registers, so the column pair (B = 2) fits LDS although 5 M reals would not
-      f64_xt = sizeof(R) == 8 && pb.bc_x == 0 && !xslab && !slab &&
+      // (t-slab phases too: kernels_xt_f64.hpp)
+      f64_xt = sizeof(R) == 8 && pb.bc_x == 0 && !xslab &&
                ((nxg == 4096 && B == 2) || (nxg == 8192 && half_real));
       // fp64 one-row windows at a power-of-two nx: the carry-free transform needs only the padded lines
       t1_xt64 = sizeof(R) == 8 && T == 1 && pb.bc_x == 0 && !half_real && !xslab && !slab && plx.pow2 &&
@@ -311,7 +312,7 @@ struct Impl : ImplBase {
       lds_xt = (size_t)5 * nmodes * sizeof(R);
       // fp64 ny = 8192 (C4's y extent in the reference's precision): the generic row kernels transform the row pair
       // in place in one padded line (FFTIp, 136 KiB) instead of a Stockham ping-pong of two (256 KiB)
-      ip_rows = sizeof(R) == 8 && ny == 8192 && lds_res > kLdsBytes && !xslab && !slab;
+      ip_rows = sizeof(R) == 8 && ny == 8192 && lds_res > kLdsBytes && !xslab;
       if (ip_rows) lds_res = (size_t)Pad<8192>::LINE * csz;
       if (lds_res > kLdsBytes) return fail(PDHG_ERR_UNSUPPORTED, "ny=%d exceeds the LDS row transform", ny);
       {   // generic row kernels: when the LDS admits few workgroups per CU (fp64 ny = 4096: one), wider
@@ -521,11 +522,13 @@ struct Impl : ImplBase {
       if (p.nb % xs_P) return fail(PDHG_ERR_UNSUPPORTED, "%d column blocks do not split over %d ranks", p.nb, xs_P);
       xs_nbs = p.nb / xs_P;
     }
-    // t-slab phases: the fast DHT x kernels (power-of-two nx 512 - 8192) or the generic runtime-radix kernel (any
-    // nx, the DCT of egno 3's bc (1, 0)); the halo row split of the residual needs the fast row kernels
-    if (slab && !(is2d && sizeof(R) == 4 && fast_rows))
-      return fail(PDHG_ERR_UNSUPPORTED, "t-slab decomposition needs ndim 2, fp32 and a power-of-two ny in [256, 8192] "
-                                        "(fast row kernels)");
+    // t-slab phases: the fast DHT x kernels (power-of-two nx 512 - 8192), the fp64 x kernel (nx = 4096, and 8192
+    // half-real) or the generic runtime-radix kernel (any nx, the DCT of egno 3's bc (1, 0)).  fp32 needs the
+    // fast row kernels; fp64 splits the residual's halo row off with the 4-row kernels (ny 2048 / 4096) and runs
+    // the generic row kernels over the whole slab after the halo otherwise
+    if (slab && !(is2d && (fast_rows || sizeof(R) == 8)))
+      return fail(PDHG_ERR_UNSUPPORTED, "t-slab decomposition needs ndim 2 and, in fp32, a power-of-two ny in "
+                                        "[256, 8192] (fast row kernels)");
 
     // ---- device buffers ----
     const size_t npl = plane();
@@ -984,8 +987,6 @@ struct Impl : ImplBase {
       }
       if (f64_xt) {
         ProfScope ps(this, "precond");
-        if (p.xt_phase != 0 || p.b0 != 0 || nblk != p.nb)
-          return fail(PDHG_ERR_UNSUPPORTED, "the fp64 nx = 4096 x transform runs whole windows only");
         if (half_real) {   // nx = 8192: one real column per block + the split-twiddle tables
           const size_t lds = (size_t)(Pad<4096>::LINE + TwLds<4096>::SIZE + 4096 + 128) * sizeof(C);
           if ((rc = ensure_lds(k_precond_xt_f64_2d<4096, 512, true>, lds))) return rc;
@@ -1333,7 +1334,7 @@ struct Impl : ImplBase {
     } else {
       const dim3 g(gxd, gyd, gz);
       if constexpr (EGNO != 3) {
-        if (fuse_res && p.inplace && gz == 1 && lo == 0 && hi == pb.T) {
+        if (fuse_res && p.inplace && gz == 1 && (slab || (lo == 0 && hi == pb.T))) {
           hipLaunchKernelGGL((k_dual_lds_2d<EGNO, 8, true, double, 2>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi,
                              zbase);
           res_valid = true;
@@ -1602,7 +1603,8 @@ struct Impl : ImplBase {
   // residual rows: parts bit 0 = the rows that do not read the rho halo, bit 1 = the row that does
   // (the last row, unless this is the window's last slab)
   int slab_residual(int parts) {
-    const int T = pb.T, split = (fast_rows && !kp.last_slab) ? T - 1 : (fast_rows ? T : 0);
+    const bool rows = fast_rows || res64;   // row-range residual kernels (else the whole slab after the halo)
+    const int T = pb.T, split = (rows && !kp.last_slab) ? T - 1 : (rows ? T : 0);
     int rc;
     if ((parts & 1) && (rc = launch_residual(kp, 0, split))) return rc;
     if ((parts & 2) && (rc = launch_residual(kp, split, T))) return rc;
@@ -2005,6 +2007,42 @@ struct Impl : ImplBase {
     return PDHG_OK;
   }
 
+  // rows [row0, row0 + nrows) of phi / phi_bar ([T+1]) and rho / alp ([T]) in the reference layouts
+  int get_rows(int row0, int nrows, double* phi, double* pbar, double* rho, double* alp) {
+    const int T = pb.T;
+    if (row0 < 0 || nrows < 1 || row0 + nrows > T + 1 || ((rho || alp) && row0 + nrows > T))
+      return fail(PDHG_ERR_ARG, "rows [%d, %d) outside phi [0, %d) / rho, alp [0, %d)", row0, row0 + nrows, T + 1, T);
+    HIP_TRY(hipStreamSynchronize(stream));
+    Ctrl h;
+    int rc;
+    if ((rc = read_ctrl(h))) return rc;
+    const size_t npl = plane(), n = (size_t)nrows * npl, off = (size_t)row0 * npl;
+    std::unique_ptr<R[]> buf(sizeof(R) == 8 && !alp ? nullptr : new R[n]);
+    auto rows_out = [&](double* dst, const R* src) -> int {
+      if constexpr (sizeof(R) == 8) {
+        HIP_TRY(hipMemcpy(dst, src + off, n * sizeof(R), hipMemcpyDeviceToHost));
+      } else {
+        HIP_TRY(hipMemcpy(buf.get(), src + off, n * sizeof(R), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < n; ++i) dst[i] = (double)buf[i];
+      }
+      return PDHG_OK;
+    };
+    if (phi && (rc = rows_out(phi, kp.phi))) return rc;
+    if (pbar && (rc = rows_out(pbar, kp.phibar))) return rc;
+    if (rho && (rc = rows_out(rho, kp.rho[h.cur]))) return rc;
+    if (alp) {
+      const int nc = n_ctrl(), nar = n_alp_ref();
+      std::memset(alp, 0, sizeof(double) * n * nc * nar);
+      for (int a = 0; a < nar; ++a)
+        for (int c = 0; c < nc; ++c) {
+          if (!live(a, c, nc)) continue;
+          HIP_TRY(hipMemcpy(buf.get(), kp.alp[h.cur][a] + off, n * sizeof(R), hipMemcpyDeviceToHost));
+          for (size_t i = 0; i < n; ++i) alp[((size_t)a * n + i) * nc + c] = (double)buf[i];
+        }
+    }
+    return PDHG_OK;
+  }
+
   int init_state(const double* g) {
     res_valid = false;
     const size_t npl = plane();
@@ -2121,33 +2159,31 @@ int dispatch(pdhg_ctx* ctx, F&& f) {
 // phases shared by the t-slab and x-slab contexts (begin, finalizers, dual, outer, status)
 template <typename F>
 int phase_dispatch(pdhg_ctx* ctx, F&& f) {
-  CtxBox* b = ctx_box(ctx);
-  if (!b) return fail(PDHG_ERR_ARG, "null or foreign context handle");
-  if (b->precision != 4) return fail(PDHG_ERR_STATE, "not a t-slab / x-slab context");
-  auto& im = *static_cast<Impl<float>*>(b->impl.get());
-  if (!im.slab && !im.xslab) return fail(PDHG_ERR_STATE, "not a t-slab / x-slab context");
-  return f(im);
+  return dispatch(ctx, [&](auto& im) {
+    if (!im.slab && !im.xslab) return fail(PDHG_ERR_STATE, "not a t-slab / x-slab context");
+    return f(im);
+  });
 }
 
 template <typename F>
 int xslab_dispatch(pdhg_ctx* ctx, F&& f) {
-  CtxBox* b = ctx_box(ctx);
-  if (!b) return fail(PDHG_ERR_ARG, "null or foreign context handle");
-  if (b->precision != 4) return fail(PDHG_ERR_STATE, "not an x-slab context");
-  auto& im = *static_cast<Impl<float>*>(b->impl.get());
-  int rc = im.need_xslab();
-  return rc ? rc : f(im);
+  return dispatch(ctx, [&](auto& im) {
+    int rc = im.need_xslab();
+    return rc ? rc : f(im);
+  });
 }
 
+// t-slab contexts are fp32 or fp64 (the reference's arithmetic); planes crossing this ABI are in the context's
+// precision (RealOf)
 template <typename F>
 int slab_dispatch(pdhg_ctx* ctx, F&& f) {
-  CtxBox* b = ctx_box(ctx);
-  if (!b) return fail(PDHG_ERR_ARG, "null or foreign context handle");
-  if (b->precision != 4) return fail(PDHG_ERR_STATE, "not a t-slab context");
-  auto& im = *static_cast<Impl<float>*>(b->impl.get());
-  int rc = im.need_slab();
-  return rc ? rc : f(im);
+  return dispatch(ctx, [&](auto& im) {
+    int rc = im.need_slab();
+    return rc ? rc : f(im);
+  });
 }
+template <typename I>
+using RealOf = typename std::remove_reference<I>::type::Real;
 
 // the multi-device context (pdhg_multi.hpp): the done flag of a slab's control block, read by a synchronous
 // copy that does not wait for the slab's stream (the caller synchronised on an event recorded after the
@@ -2255,6 +2291,9 @@ int pdhg_get_phi_bar(pdhg_ctx* ctx, double* phi_bar) {
 int pdhg_set_phi_bar(pdhg_ctx* ctx, const double* phi_bar) {
   if (!phi_bar) return fail(PDHG_ERR_ARG, "null phi_bar");
   return dispatch(ctx, [&](auto& im) { return im.set_phi_bar(phi_bar); });
+}
+int pdhg_get_rows(pdhg_ctx* ctx, int row0, int nrows, double* phi, double* phi_bar, double* rho, double* alp) {
+  return dispatch(ctx, [&](auto& im) { return im.get_rows(row0, nrows, phi, phi_bar, rho, alp); });
 }
 int pdhg_init_state(pdhg_ctx* ctx, const double* g) {
   if (!g) return fail(PDHG_ERR_ARG, "null g");
@@ -2381,9 +2420,9 @@ int pdhg_create_slab(const pdhg_problem* prob, int j0, int T_total, int device, 
   *out = nullptr;
   if (j0 < 0 || prob->T < 1 || j0 + prob->T > T_total)
     return fail(PDHG_ERR_ARG, "slab rows [%d, %d) outside the window of %d rows", j0, j0 + prob->T, T_total);
-  if (prob->precision != 4) return fail(PDHG_ERR_UNSUPPORTED, "t-slab decomposition is fp32 only");
   if (prob->ndim != 2) return fail(PDHG_ERR_UNSUPPORTED, "t-slab decomposition is 2-D only");
-  // validate the rest exactly like pdhg_create, then rebuild as a slab
+  // validate the rest exactly like pdhg_create, then rebuild as a slab (fp32, or fp64 = the reference's arithmetic,
+  // jaxsrc/update_fns_in_pdhg.py:10)
   pdhg_ctx* probe = nullptr;
   pdhg_problem q = *prob;
   q.T = 1;
@@ -2391,15 +2430,20 @@ int pdhg_create_slab(const pdhg_problem* prob, int j0, int T_total, int device, 
   if (rc) return rc;
   pdhg_destroy(probe);
   auto box = std::make_unique<CtxBox>();
-  box->precision = 4;
-  auto im = std::make_unique<Impl<float>>();
-  im->pb = *prob;
-  im->device = device;
-  im->slab = true;
-  im->slab_j0 = j0;
-  im->slab_Tg = T_total;
-  rc = im->setup();
-  box->impl = std::move(im);
+  box->precision = prob->precision;
+  auto build = [&](auto tag) {
+    using Rt = decltype(tag);
+    auto im = std::make_unique<Impl<Rt>>();
+    im->pb = *prob;
+    im->device = device;
+    im->slab = true;
+    im->slab_j0 = j0;
+    im->slab_Tg = T_total;
+    const int r = im->setup();
+    box->impl = std::move(im);
+    return r;
+  };
+  rc = prob->precision == 8 ? build(0.0) : build(0.f);
   if (rc) return rc;
   *out = reinterpret_cast<pdhg_ctx*>(box.release());
   return PDHG_OK;
@@ -2413,25 +2457,25 @@ int pdhg_slab_begin(pdhg_ctx* ctx) {
 }
 int pdhg_slab_carry_gain(pdhg_ctx* ctx, void* GS_out) {
   if (!GS_out) return fail(PDHG_ERR_ARG, "null plane");
-  return slab_dispatch(ctx, [&](auto& im) { return im.slab_G(static_cast<float*>(GS_out)); });
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_G(static_cast<RealOf<decltype(im)>*>(GS_out)); });
 }
 int pdhg_slab_residual(pdhg_ctx* ctx, int parts) {
   return slab_dispatch(ctx, [&](auto& im) { return im.slab_residual(parts); });
 }
 int pdhg_slab_forward(pdhg_ctx* ctx, double tau) {
-  return slab_dispatch(ctx, [&](auto& im) { return im.slab_forward((float)tau); });
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_forward((RealOf<decltype(im)>)tau); });
 }
 int pdhg_slab_fixup(pdhg_ctx* ctx, const void* all_DS, const void* all_GS, int rank, int nranks) {
   if (!all_DS || !all_GS) return fail(PDHG_ERR_ARG, "null carry planes");
   if (rank < 0 || rank >= nranks) return fail(PDHG_ERR_ARG, "rank %d of %d", rank, nranks);
   return slab_dispatch(ctx, [&](auto& im) {
-    return im.slab_fixup(static_cast<const float*>(all_DS), static_cast<const float*>(all_GS), rank, nranks);
+    return im.slab_fixup(static_cast<const RealOf<decltype(im)>*>(all_DS), static_cast<const RealOf<decltype(im)>*>(all_GS), rank, nranks);
   });
 }
 int pdhg_slab_long_modes(pdhg_ctx* ctx, const void* all_GS, int nranks, double delta, int* K) {
   if (!all_GS || !K || nranks < 1) return fail(PDHG_ERR_ARG, "null plane / count or nranks < 1");
   return slab_dispatch(ctx, [&](auto& im) {
-    return im.slab_long_modes(static_cast<const float*>(all_GS), nranks, delta, K);
+    return im.slab_long_modes(static_cast<const RealOf<decltype(im)>*>(all_GS), nranks, delta, K);
   });
 }
 int pdhg_slab_fixup_nb(pdhg_ctx* ctx, const void* D_left, const void* S1_right, const void* all_long,
@@ -2439,13 +2483,13 @@ int pdhg_slab_fixup_nb(pdhg_ctx* ctx, const void* D_left, const void* S1_right, 
   if (!D_left || !S1_right || !all_GS || rank < 0 || rank >= nranks)
     return fail(PDHG_ERR_ARG, "null plane or rank %d outside [0, %d)", rank, nranks);
   return slab_dispatch(ctx, [&](auto& im) {
-    return im.slab_fixup_nb(static_cast<const float*>(D_left), static_cast<const float*>(S1_right),
-                            static_cast<const float*>(all_long), static_cast<const float*>(all_GS), rank, nranks);
+    return im.slab_fixup_nb(static_cast<const RealOf<decltype(im)>*>(D_left), static_cast<const RealOf<decltype(im)>*>(S1_right),
+                            static_cast<const RealOf<decltype(im)>*>(all_long), static_cast<const RealOf<decltype(im)>*>(all_GS), rank, nranks);
   });
 }
 int pdhg_slab_backward(pdhg_ctx* ctx, double tau, double* sums) {
   if (!sums) return fail(PDHG_ERR_ARG, "null sums");
-  return slab_dispatch(ctx, [&](auto& im) { return im.slab_backward((float)tau, sums); });
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_backward((RealOf<decltype(im)>)tau, sums); });
 }
 int pdhg_slab_primal_finalize(pdhg_ctx* ctx, const double* sums) {
   if (!sums) return fail(PDHG_ERR_ARG, "null sums");
@@ -2453,7 +2497,7 @@ int pdhg_slab_primal_finalize(pdhg_ctx* ctx, const double* sums) {
 }
 int pdhg_slab_dual(pdhg_ctx* ctx, double sigma, int rho_alp_iters, int sub, double* sums, int parts) {
   if (!sums) return fail(PDHG_ERR_ARG, "null sums");
-  return phase_dispatch(ctx, [&](auto& im) { return im.slab_dual((float)sigma, rho_alp_iters, sub, sums, parts); });
+  return phase_dispatch(ctx, [&](auto& im) { return im.slab_dual((RealOf<decltype(im)>)sigma, rho_alp_iters, sub, sums, parts); });
 }
 int pdhg_slab_dual_finalize(pdhg_ctx* ctx, double eps, int sub, const double* sums) {
   if (!sums) return fail(PDHG_ERR_ARG, "null sums");
@@ -2574,7 +2618,7 @@ int pdhg_xslab_precond(pdhg_ctx* ctx) {
 }
 int pdhg_xslab_update(pdhg_ctx* ctx, double tau, double* sums) {
   if (!sums) return fail(PDHG_ERR_ARG, "null sums");
-  return xslab_dispatch(ctx, [&](auto& im) { return im.xs_update((float)tau, sums); });
+  return xslab_dispatch(ctx, [&](auto& im) { return im.xs_update((RealOf<decltype(im)>)tau, sums); });
 }
 
 int pdhg_slab_part_modes(pdhg_ctx* ctx, int part, int nparts, unsigned long long* m0, unsigned long long* m1) {
@@ -2590,7 +2634,7 @@ int pdhg_slab_part_modes(pdhg_ctx* ctx, int part, int nparts, unsigned long long
 }
 int pdhg_slab_forward_part(pdhg_ctx* ctx, double tau, int part, int nparts) {
   if (nparts < 1 || part < 0 || part >= nparts) return fail(PDHG_ERR_ARG, "part %d of %d", part, nparts);
-  return slab_dispatch(ctx, [&](auto& im) { return im.slab_forward_part((float)tau, part, nparts); });
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_forward_part((RealOf<decltype(im)>)tau, part, nparts); });
 }
 int pdhg_slab_carry_out_part(pdhg_ctx* ctx, void* dst, int part, int nparts) {
   if (!dst || nparts < 1 || part < 0 || part >= nparts) return fail(PDHG_ERR_ARG, "null plane or part %d of %d", part, nparts);
@@ -2601,18 +2645,18 @@ int pdhg_slab_fixup_nb_part(pdhg_ctx* ctx, const void* D_left, const void* S1_ri
   if (!D_left || !S1_right || !all_GS || rank < 0 || rank >= nranks || nparts < 1 || part < 0 || part >= nparts)
     return fail(PDHG_ERR_ARG, "null plane, rank %d of %d or part %d of %d", rank, nranks, part, nparts);
   return slab_dispatch(ctx, [&](auto& im) {
-    return im.slab_fixup_nb(static_cast<const float*>(D_left), static_cast<const float*>(S1_right),
-                            static_cast<const float*>(all_long), static_cast<const float*>(all_GS), rank, nranks,
+    return im.slab_fixup_nb(static_cast<const RealOf<decltype(im)>*>(D_left), static_cast<const RealOf<decltype(im)>*>(S1_right),
+                            static_cast<const RealOf<decltype(im)>*>(all_long), static_cast<const RealOf<decltype(im)>*>(all_GS), rank, nranks,
                             part, nparts);
   });
 }
 int pdhg_slab_backward_part(pdhg_ctx* ctx, double tau, int part, int nparts) {
   if (nparts < 1 || part < 0 || part >= nparts) return fail(PDHG_ERR_ARG, "part %d of %d", part, nparts);
-  return slab_dispatch(ctx, [&](auto& im) { return im.slab_backward_part((float)tau, part, nparts); });
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_backward_part((RealOf<decltype(im)>)tau, part, nparts); });
 }
 int pdhg_slab_update(pdhg_ctx* ctx, double tau, double* sums) {
   if (!sums) return fail(PDHG_ERR_ARG, "null sums");
-  return slab_dispatch(ctx, [&](auto& im) { return im.slab_update((float)tau, sums); });
+  return slab_dispatch(ctx, [&](auto& im) { return im.slab_update((RealOf<decltype(im)>)tau, sums); });
 }
 
 }  // extern "C"

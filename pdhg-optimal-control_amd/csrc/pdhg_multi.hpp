@@ -12,7 +12,8 @@
 //     part q+1 sweeps forward (SlabRunner's schedule, pdhg_amd/slab.py);
 //   * waits are per neighbour (rho halo: r+1 -> r, phi_bar halo: r-1 -> r, D: r-1 -> r, S1: r+1 -> r), never
 //     all-to-all; only the long-range carry modes (few, pdhg_slab_long_modes) and the sums need every slab;
-//   * the 16-double sum vectors: with peer access between every pair of devices (xGMI), every slab's main
+//   * the 16-double sum vectors (opt-in, PDHG_MULTI_PEER_FOLD=1; default: the gather fold below): with peer
+//     access between every pair of devices (xGMI), every slab's main
 //     stream waits for every slab's contribution event and one 64-thread kernel on its own device folds the P
 //     vectors in slab order straight from their owners' memory (peer pointers) -- the same order on every
 //     device, so every slab takes bitwise the same stop decisions in its own control block, with no copies
@@ -63,10 +64,12 @@ struct pdhg_multi {
   size_t sp = 0, spec = 0;
   int K = 0;               // long-range modes
   int nar = 4, nc = 2;     // reference alp layout [nar][T][nx][ny][nc]
+  size_t es = 4;           // bytes per plane element: 4 (fp32 slabs) or 8 (fp64, the reference's arithmetic)
   struct Buf {
-    float *rho_send = nullptr, *rho_recv = nullptr, *pb_send = nullptr, *pb_recv = nullptr;
-    float *DS = nullptr, *GS = nullptr, *Dl = nullptr, *S1r = nullptr, *LONG = nullptr, *allLong = nullptr,
-          *allGS = nullptr;
+    // planes in the slabs' precision (es bytes per element): byte pointers, element offsets scaled by es
+    char *rho_send = nullptr, *rho_recv = nullptr, *pb_send = nullptr, *pb_recv = nullptr;
+    char *DS = nullptr, *GS = nullptr, *Dl = nullptr, *S1r = nullptr, *LONG = nullptr, *allLong = nullptr,
+         *allGS = nullptr;
     double* sums = nullptr;      // the folded vector this slab's finalize kernels read
     double* contrib = nullptr;   // peer fold: [2][16] contributions, alternating per allreduce
     // events: producer side (main stream) and receiver side (side stream)
@@ -194,6 +197,7 @@ struct pdhg_multi {
     pb.xs = xs.data();
     pb.ys = ys.data();
     nc = prob.egno == 3 ? 1 : 2;
+    es = prob.precision == 8 ? 8 : 4;
     const int T = prob.T;
     if (P < 1 || P > T) return fail(PDHG_ERR_ARG, "need 1 <= ndev <= T (ndev %d, T %d)", P, T);
     if (const char* e = getenv("PDHG_MULTI_PARTS")) parts = std::max(1, atoi(e));   // tuning override
@@ -204,10 +208,12 @@ struct pdhg_multi {
       j1.push_back(j + n);
       j += n;
     }
-    // peer access where the runtime offers it (copies work either way; the sums fold reads peer memory only when
-    // every pair has it)
-    peer_fold = P <= pdhg::kMultiMaxPeerFold;
-    if (const char* e = getenv("PDHG_MULTI_PEER_FOLD")) peer_fold = peer_fold && atoi(e) != 0;   // tuning override
+    // peer access where the runtime offers it (copies work either way).  The per-device peer fold of the sums
+    // (plain loads of another device's buffers, cross-device event order for the alternating contribution
+    // buffers) is opt-in, PDHG_MULTI_PEER_FOLD=1, until a run on two real devices has shown it bitwise equal to
+    // the gather fold; the default is the gather -> fold -> scatter chain on slab 0's device
+    peer_fold = false;
+    if (const char* e = getenv("PDHG_MULTI_PEER_FOLD")) peer_fold = P <= pdhg::kMultiMaxPeerFold && atoi(e) != 0;
     for (int r = 0; r < P; ++r)
       for (int q = 0; q < P; ++q) {
         if (dev[r] == dev[q]) continue;
@@ -249,9 +255,11 @@ struct pdhg_multi {
     spec = c;
     for (int r = 0; r < P; ++r) {
       Buf& x = b[r];
-      if ((rc = alloc(r, &x.rho_send, sp)) || (rc = alloc(r, &x.rho_recv, sp)) || (rc = alloc(r, &x.pb_send, sp)) ||
-          (rc = alloc(r, &x.pb_recv, sp)) || (rc = alloc(r, &x.DS, 2 * spec)) || (rc = alloc(r, &x.GS, 2 * spec)) ||
-          (rc = alloc(r, &x.Dl, spec)) || (rc = alloc(r, &x.S1r, spec)) || (rc = alloc(r, &x.allGS, 2 * spec * P)) ||
+      if ((rc = alloc(r, &x.rho_send, sp * es)) || (rc = alloc(r, &x.rho_recv, sp * es)) ||
+          (rc = alloc(r, &x.pb_send, sp * es)) || (rc = alloc(r, &x.pb_recv, sp * es)) ||
+          (rc = alloc(r, &x.DS, 2 * spec * es)) || (rc = alloc(r, &x.GS, 2 * spec * es)) ||
+          (rc = alloc(r, &x.Dl, spec * es)) || (rc = alloc(r, &x.S1r, spec * es)) ||
+          (rc = alloc(r, &x.allGS, 2 * spec * P * es)) ||
           (rc = alloc(r, &x.sums, (size_t)kNumSums)) || (rc = alloc(r, &x.contrib, (size_t)2 * kNumSums)))
         return rc;
       if ((rc = pdhg_slab_carry_gain(s[r], x.GS))) return rc;
@@ -261,7 +269,7 @@ struct pdhg_multi {
     if ((rc = full_barrier())) return rc;
     for (int r = 0; r < P; ++r)
       for (int q = 0; q < P; ++q)
-        if ((rc = copy(r, st[r], b[r].allGS + (size_t)q * 2 * spec, q, b[q].GS, 2 * spec * sizeof(float)))) return rc;
+        if ((rc = copy(r, st[r], b[r].allGS + (size_t)q * 2 * spec * es, q, b[q].GS, 2 * spec * es))) return rc;
     if ((rc = full_barrier())) return rc;
     for (int r = 0; r < P; ++r) {
       int k = 0;
@@ -270,8 +278,8 @@ struct pdhg_multi {
       else if (k != K) return fail(PDHG_ERR_STATE, "slabs disagree on the long-range modes (%d vs %d)", k, K);
     }
     for (int r = 0; r < P; ++r)
-      if ((rc = alloc(r, &b[r].LONG, (size_t)std::max(1, 2 * K))) ||
-          (rc = alloc(r, &b[r].allLong, (size_t)std::max(1, 2 * K) * P)))
+      if ((rc = alloc(r, &b[r].LONG, (size_t)std::max(1, 2 * K) * es)) ||
+          (rc = alloc(r, &b[r].allLong, (size_t)std::max(1, 2 * K) * P * es)))
         return rc;
     return full_barrier();
   }
@@ -300,7 +308,7 @@ struct pdhg_multi {
   // one outer iteration (include/pdhg.h t-slab choreography, neighbour exchange in `parts` column-block parts)
   int step(double tau, double sigma, double eps, int k) {
     int rc;
-    const size_t pbytes = sp * sizeof(float);
+    const size_t pbytes = sp * es;
     if ((rc = mark(0))) return rc;
     // rho halo (row 0 of slab r+1 -> slab r) on the receiver's side stream || the residual rows without it
     for (int r = 0; r < P; ++r)
@@ -321,7 +329,7 @@ struct pdhg_multi {
     for (int q = 0; q < parts; ++q) {
       unsigned long long m0 = 0, m1 = 0;
       if ((rc = pdhg_slab_part_modes(s[0], q, parts, &m0, &m1))) return rc;
-      const size_t off = m0, n = (m1 - m0) * sizeof(float);
+      const size_t off = m0 * es, n = (m1 - m0) * es;   // bytes
       for (int r = 0; r < P; ++r)
         if ((rc = pdhg_slab_forward_part(s[r], tau, q, parts)) || (rc = pdhg_slab_carry_out_part(s[r], b[r].DS, q, parts)) ||
             (rc = rec(b[r].ds[q], r, st[r])))
@@ -331,7 +339,7 @@ struct pdhg_multi {
                       (rc = copy(r, ss[r], b[r].Dl + off, r - 1, b[r - 1].DS + off, n))))
           return rc;
         if (r + 1 < P && ((rc = wait(r, ss[r], b[r + 1].ds[q])) ||
-                          (rc = copy(r, ss[r], b[r].S1r + off, r + 1, b[r + 1].DS + spec + off, n))))
+                          (rc = copy(r, ss[r], b[r].S1r + off, r + 1, b[r + 1].DS + spec * es + off, n))))
           return rc;
         if ((rc = rec(b[r].carry_in[q], r, ss[r]))) return rc;
       }
@@ -343,7 +351,7 @@ struct pdhg_multi {
       for (int r = 0; r < P; ++r) {
         for (int q = 0; q < P; ++q)
           if ((rc = wait(r, ss[r], b[q].longp)) ||
-              (rc = copy(r, ss[r], b[r].allLong + (size_t)q * 2 * K, q, b[q].LONG, 2 * (size_t)K * sizeof(float))))
+              (rc = copy(r, ss[r], b[r].allLong + (size_t)q * 2 * K * es, q, b[q].LONG, 2 * (size_t)K * es)))
             return rc;
         if ((rc = rec(b[r].long_in, r, ss[r]))) return rc;
       }

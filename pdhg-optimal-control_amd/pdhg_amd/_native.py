@@ -22,7 +22,7 @@ PDHG_ERR_NOMEM = -5
 # every symbol declared in include/pdhg.h
 EXPORTS = (
     "pdhg_last_error", "pdhg_abi_version", "pdhg_device_count", "pdhg_create", "pdhg_destroy",
-    "pdhg_set_state", "pdhg_get_state", "pdhg_get_phi_bar", "pdhg_set_phi_bar", "pdhg_init_state",
+    "pdhg_set_state", "pdhg_get_state", "pdhg_get_phi_bar", "pdhg_set_phi_bar", "pdhg_get_rows", "pdhg_init_state",
     "pdhg_update_primal", "pdhg_update_dual", "pdhg_errors", "pdhg_inner_error", "pdhg_iterate", "pdhg_set_stop_rules", "pdhg_synchronize",
     "pdhg_device_bytes", "pdhg_path_info", "pdhg_profile_enable", "pdhg_profile_query", "pdhg_algorithmic_bytes",
     # t-slab decomposition (multi-GPU)
@@ -102,6 +102,7 @@ def load():
         "pdhg_get_state": ([P, dp, dp, dp], ctypes.c_int),
         "pdhg_get_phi_bar": ([P, dp], ctypes.c_int),
         "pdhg_set_phi_bar": ([P, dp], ctypes.c_int),
+        "pdhg_get_rows": ([P, ctypes.c_int, ctypes.c_int, dp, dp, dp, dp], ctypes.c_int),
         "pdhg_init_state": ([P, dp], ctypes.c_int),
         "pdhg_update_primal": ([P, ctypes.c_double], ctypes.c_int),
         "pdhg_update_dual": ([P, ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.POINTER(ctypes.c_int)],

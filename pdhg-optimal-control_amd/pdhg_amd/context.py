@@ -81,6 +81,17 @@ class PDHGContext:
         N.check(self._lib.pdhg_get_state(self._h, N.dptr(phi), N.dptr(rho), N.dptr(alp)))
         return phi, rho, (None if alp is None else tuple(alp[i] for i in range(self.n_alp)))
 
+    def get_rows(self, row0, nrows, phi=True, phi_bar=False, rho=True, alp=True):
+        """Rows [row0, row0 + nrows) of (phi, phi_bar, rho, alp) in the reference layouts (pdhg_get_rows): for
+        windows too large for a host copy of the whole state.  A part passed as False comes back as None."""
+        sp = self._space
+        f = lambda on: np.empty((nrows,) + sp) if on else None  # noqa: E731
+        a = np.empty((self.n_alp, nrows) + sp + (self.n_ctrl,)) if alp else None
+        ph, pb, rh = f(phi), f(phi_bar), f(rho)
+        N.check(self._lib.pdhg_get_rows(self._h, int(row0), int(nrows), N.dptr(ph), N.dptr(pb), N.dptr(rh),
+                                        N.dptr(a)))
+        return ph, pb, rh, (None if a is None else tuple(a[i] for i in range(self.n_alp)))
+
     def get_phi_bar(self):
         pb = np.empty((self.T + 1,) + self._space)
         N.check(self._lib.pdhg_get_phi_bar(self._h, N.dptr(pb)))

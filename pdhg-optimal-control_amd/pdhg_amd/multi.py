@@ -21,8 +21,8 @@ from . import _native as N
 class MultiContext:
     def __init__(self, egno, nx, ny, T, dx, dy, dt, xs, ys, devices=(0, 0), epsl=0.0, c_on_rho=70.0,
                  precision="fp32", rho_alp_iters=1):
-        if precision not in ("fp32", 4):
-            raise N.PDHGUnsupported(N.PDHG_ERR_UNSUPPORTED, "the multi-device context is fp32 only (t-slab kernels)")
+        if precision not in ("fp32", "fp64", 4, 8):
+            raise ValueError("precision must be fp32 or fp64")
         self._lib = N.load()
         self.egno, self.ndim, self.nx, self.ny, self.T = int(egno), 2, int(nx), int(ny), int(T)
         self.n_ctrl = 1 if egno == 3 else 2
@@ -34,7 +34,8 @@ class MultiContext:
         prob = N.pdhg_problem()
         prob.egno, prob.ndim, prob.bc_x, prob.bc_y = self.egno, 2, bcx, 0
         prob.nx, prob.ny, prob.T = self.nx, self.ny, self.T
-        prob.precision = 4
+        prob.precision = {"fp32": 4, "fp64": 8, 4: 4, 8: 8}[precision]   # fp64: the reference's arithmetic
+        self.precision = precision
         prob.rho_alp_iters = self.rho_alp_iters
         prob.dx, prob.dy, prob.dt = float(dx), float(dy), float(dt)
         prob.epsl, prob.c_on_rho = float(epsl), float(c_on_rho)

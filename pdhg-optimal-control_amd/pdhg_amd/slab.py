@@ -82,8 +82,10 @@ class PhaseOps:
 
 
 class SlabContext(PhaseOps, PDHGContext):
-    """The slab [j0, j1) of a window of T_total rows (fp32, 2-D).  Arrays at this boundary are the
-    slab's rows: phi [T+1, nx, ny] (row 0 = global phi row j0), rho / alp [T, nx, ny(, n_ctrl)]."""
+    """The slab [j0, j1) of a window of T_total rows (2-D; precision "fp32", or "fp64" = the reference's
+    arithmetic, jaxsrc/update_fns_in_pdhg.py:10).  Arrays at this boundary are the slab's rows: phi [T+1, nx, ny]
+    (row 0 = global phi row j0), rho / alp [T, nx, ny(, n_ctrl)].  Device planes exchanged between slabs are in
+    the slab's precision (plane_dtype)."""
 
     def __init__(self, rank, nranks, T_total, egno, nx, ny, dx, dy, dt, xs, ys, device=0, **kw):
         self.rank, self.nranks, self.T_total = int(rank), int(nranks), int(T_total)
@@ -97,6 +99,11 @@ class SlabContext(PhaseOps, PDHGContext):
         return h
 
     @property
+    def plane_dtype(self):
+        import torch
+        return torch.float64 if self.precision in ("fp64", 8) else torch.float32
+
+    @property
     def last(self):
         return self.rank == self.nranks - 1
 
@@ -106,7 +113,7 @@ class SlabContext(PhaseOps, PDHGContext):
         return sp.value, spec.value
 
 
-    # thin wrappers; tensor arguments are device tensors (float32 planes)
+    # thin wrappers; tensor arguments are device tensors (planes of plane_dtype)
     def carry_gain(self, GS):
         N.check(self._lib.pdhg_slab_carry_gain(self._h, _ptr(GS)))
 
@@ -310,7 +317,9 @@ class SlabRunner:
         self.parts = int(parts) if (exchange == "neighbour" and overlap) else 1
         dev = torch.device("cuda", torch.cuda.current_device())
         sp, spec = self.slabs[0].plane_sizes()
-        f32, f64 = torch.float32, torch.float64
+        f32, f64 = self.slabs[0].plane_dtype, torch.float64   # planes in the slabs' precision; sums fp64
+        if any(s.plane_dtype != f32 for s in self.slabs):
+            raise ValueError("slabs of one runner must share a precision")
         self.b = []
         handle = torch.cuda.current_stream().cuda_stream
         for s in self.slabs:

@@ -36,3 +36,16 @@ def test_gpus_mismatch_with_launcher_env_fails():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--selftest"], env=env,
                        capture_output=True, text=True, timeout=120)
     assert p.returncode != 0 and "WORLD_SIZE=1" in (p.stderr + p.stdout)
+
+
+def test_dual_passes_of_the_chunked_loop():
+    """The chunked dual (kernels_dual_multi.hpp) moves one sub-iteration's bytes per pass: ceil(inner / 5) chunk
+    passes + the final re-run when the exit falls inside a chunk -- what bench.py prices the dual class with, so no
+    record reports more bytes than crossed HBM (frac 2.01 from bytes x inner count)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.dual_passes(10.0) == 2.0        # no early exit at k = 10: two chunks of 5
+    assert bench.dual_passes(5.0) == 1.0
+    assert bench.dual_passes(3.0) == 2.0         # exit inside the first chunk: chunk + final
+    assert bench.dual_passes(7.0) == 3.0
+    assert bench.dual_passes(1.0) == 2.0

@@ -39,6 +39,14 @@ DECOMP = {
 # distributed t-solve) for epsl = 0; with epsl = 0.1 from the rough state the explicit sigma*epsl*Lap(phi_bar)
 # term amplifies that phi_bar rounding ~5e5-fold into rho (test_gpu_configs.py docstring)
 BOUNDS = {0.0: {"phi": 2e-5, "rho": 2e-4, "alp": 2e-4}, 0.1: {"phi": 2e-5, "rho": 2e-3, "alp": 2e-2}}
+# fp64 (the reference's arithmetic, jaxsrc/update_fns_in_pdhg.py:10): the same decomposition in double, against
+# the single fp64 context -- the distributed t-solve's other association of the carry sums rounds in the last
+# bits only
+BOUNDS64 = {0.0: {"phi": 1e-12, "rho": 1e-12, "alp": 1e-12}, 0.1: {"phi": 1e-12, "rho": 1e-12, "alp": 1e-12}}
+# fp64 slab kernels: the fp64 x transform with its slab phases (kernels_xt_f64.hpp; half-real at nx = 8192)
+PATH64 = {4096: {"f64_xt": 1}, 8192: {"f64_xt": 1, "half_real": 1}}
+CASES = [(n, "fp32") for n in DECOMP] + [(n, "fp64") for n in DECOMP]
+IDS = ["{}@{}".format(n, p) for n, p in CASES]
 
 
 def _grid(egno, nx, ny, T, epsl):
@@ -49,8 +57,8 @@ def _grid(egno, nx, ny, T, epsl):
     return G
 
 
-def _single(P, n):
-    ref = device_ctx(P, "fp32")
+def _single(P, n, prec="fp32"):
+    ref = device_ctx(P, prec)
     try:
         ref.init_state(P["g"])
         st = ref.iterate(n, TAU, SIGMA, -1.0, 1)
@@ -59,25 +67,27 @@ def _single(P, n):
         ref.close()
 
 
-def _check(name, got, want, st, st_ref, epsl, parity_log, driver):
-    b = BOUNDS[epsl]
+def _check(name, got, want, st, st_ref, epsl, parity_log, driver, prec="fp32"):
+    b = (BOUNDS64 if prec == "fp64" else BOUNDS)[epsl]
     m = {"phi": rel(got[0], want[0]), "rho": rel(got[1], want[1]),
          "alp": rel(np.stack(got[2]), np.stack(want[2])),
          "err1": abs(st["err1"] - st_ref["err1"]) / st_ref["err1"]}
-    bounds = dict(b, err1=1e-3 if epsl == 0.0 else 1e-2)
-    parity_log("test_gpu_decomp", "{}/{}".format(name, driver), m, bounds)
+    bounds = dict(b, err1=(1e-3 if epsl == 0.0 else 1e-2) if prec == "fp32" else 1e-12)
+    parity_log("test_gpu_decomp", "{}/{}@{}".format(name, driver, prec), m, bounds)
     assert all(m[k] <= bounds[k] for k in m), (name, driver, m, bounds)
 
 
-@pytest.mark.parametrize("name", list(DECOMP))
-def test_slab_runner_at_config_decomposition(native, name, parity_log):
+@pytest.mark.parametrize("name,prec", CASES, ids=IDS)
+def test_slab_runner_at_config_decomposition(native, name, prec, parity_log):
     import torch
     from pdhg_amd.slab import LocalComm, SlabContext, SlabRunner, join_state
     egno, nx, ny, T, nr, epsl, n, path = DECOMP[name]
+    if prec == "fp64":
+        path = PATH64[nx]
     P = _grid(egno, nx, ny, T, epsl)
-    st_ref, want = _single(P, n)
-    slabs = [SlabContext(r, nr, T, egno, nx, ny, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"], epsl=epsl)
-             for r in range(nr)]
+    st_ref, want = _single(P, n, prec)
+    slabs = [SlabContext(r, nr, T, egno, nx, ny, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"], epsl=epsl,
+                         precision=prec) for r in range(nr)]
     try:
         for s in slabs:
             for k, v in path.items():
@@ -93,16 +103,17 @@ def test_slab_runner_at_config_decomposition(native, name, parity_log):
         for s in slabs:
             s.close()
     assert st["iters"] == st_ref["iters_run"] == n
-    _check(name, got, want, st, st_ref, epsl, parity_log, "slabrunner")
+    _check(name, got, want, st, st_ref, epsl, parity_log, "slabrunner", prec)
 
 
-@pytest.mark.parametrize("name", list(DECOMP))
-def test_multi_context_at_config_decomposition(native, name, parity_log):
+@pytest.mark.parametrize("name,prec", CASES, ids=IDS)
+def test_multi_context_at_config_decomposition(native, name, prec, parity_log):
     from pdhg_amd.multi import MultiContext
     egno, nx, ny, T, nr, epsl, n, _ = DECOMP[name]
     P = _grid(egno, nx, ny, T, epsl)
-    st_ref, want = _single(P, n)
-    m = MultiContext(egno, nx, ny, T, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"], devices=[0] * nr, epsl=epsl)
+    st_ref, want = _single(P, n, prec)
+    m = MultiContext(egno, nx, ny, T, P["dx"], P["dy"], P["dt"], P["xs"], P["ys"], devices=[0] * nr, epsl=epsl,
+                     precision=prec)
     try:
         assert m.info("ndev") == nr and m.info("parts") == 2
         assert all(m.info("device:%d" % r) == 0 for r in range(nr))   # each slab computes on its listed device
@@ -115,7 +126,7 @@ def test_multi_context_at_config_decomposition(native, name, parity_log):
         m.close()
     assert st["iters_run"] == st_ref["iters_run"] == n
     assert ph.get("step", 0.0) > 0.0 and all(v >= 0.0 for v in ph.values()), ph
-    _check(name, got, want, st, st_ref, epsl, parity_log, "multi")
+    _check(name, got, want, st, st_ref, epsl, parity_log, "multi", prec)
 
 
 def test_multi_handle_is_not_a_context(native):
