@@ -51,6 +51,11 @@ CONFIGS = {
 }
 
 
+def progress(msg):
+    """One progress line per phase on stderr (long runs: the PMC passes and the nested run are child processes)."""
+    print("[bench {}] {}".format(time.strftime("%H:%M:%S"), msg), file=sys.stderr, flush=True)
+
+
 def grid(ndim, nx, ny):
     x1 = np.linspace(0.0, 2.0, num=nx, endpoint=False)
     if ndim == 1:
@@ -107,6 +112,9 @@ def cpu_baseline(cfg, T_sample, threads, reps_min=3):
             "reps": len(times)}
 
 
+PMC_ITERS = 3   # outer iterations of each PMC child run (1 warm-up + 2 steps, no probe)
+
+
 def pmc_traffic(args):
     """HBM bytes per launch of every kernel class from rocprofv3 PMC counters, collected in two
     separate child runs (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950) that are started
@@ -124,9 +132,11 @@ def pmc_traffic(args):
         return None, "rocprofv3 not found"
     vals = {}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        progress("rocprofv3 {} pass".format(ctr))
         d = tempfile.mkdtemp(prefix="pdhg_pmc_", dir="/tmp")
         cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "run", "--",
-               sys.executable, os.path.abspath(__file__), "--config", args.config, "--steps", "2", "--warmup", "1",
+               sys.executable, os.path.abspath(__file__), "--config", args.config, "--steps", str(PMC_ITERS - 1),
+               "--warmup", "1",
                "--rho-alp-iters", str(args.rho_alp_iters), "--precision", args.precision, "--no-cpu-baseline",
                "--no-pmc", "--no-probe", "--no-reference-precision"]
         try:
@@ -160,7 +170,11 @@ def pmc_traffic(args):
             split[("residual_first", ctr)] = {n: v for n, v in by_name.items() if "fused" not in n}
             vals[(cls, ctr)] = {n: v for n, v in by_name.items() if "fused" in n}
     vals.update(split)
-    vals = {key: sum(sum(v) / len(v) for v in by_name.values()) for key, by_name in vals.items() if by_name}
+    # per class launch: each kernel name's average per launch, summed over the class's names -- except the dual:
+    # with rho_alp_iters > 1 one dual "launch" (outer iteration) runs several kernel launches (the chunked loop's
+    # passes, kernels_dual_multi.hpp), so its bytes are all its kernels' bytes over the child's PMC_ITERS iterations
+    vals = {key: (sum(sum(v) for v in by_name.values()) / PMC_ITERS if key[0] == "dual" else
+                  sum(sum(v) / len(v) for v in by_name.values())) for key, by_name in vals.items() if by_name}
     out = {}
     for cls in list(KERNEL_SYMBOL) + ["residual_first"]:
         f, w = vals.get((cls, "FETCH_SIZE")), vals.get((cls, "WRITE_SIZE"))
@@ -275,6 +289,7 @@ def other_precision_run(args, prec):
     before it touches the GPU).  Returns the child's JSON line (nested as "reference_precision" / "fp32_precision")
     or an error note."""
     import subprocess
+    progress("nested {} run (child process)".format(prec))
     cmd = [sys.executable, os.path.abspath(__file__), "--config", args.config, "--steps", str(args.steps),
            "--warmup", str(args.warmup), "--rho-alp-iters", str(args.rho_alp_iters), "--precision", prec,
            "--no-cpu-baseline", "--no-reference-precision"]
@@ -417,6 +432,7 @@ def main():
 
     from pdhg_amd.context import PDHGContext
 
+    progress("context ({}, {})".format(args.config, args.precision))
     egno, ndim, epsl, nx, ny, nt = CONFIGS[args.config]
     T = nt - 1
     k = args.rho_alp_iters
@@ -497,6 +513,7 @@ def main():
     # reference initial state, the first iteration whose phi' or rho' holds a NaN (NaN stop on).
     first_nonfinite = None
     probe_n = 0
+    progress("context ready")
     if not args.no_probe:
         init()
         ctx.set_stop_rules(converge=True, nan=True)
@@ -558,6 +575,7 @@ def main():
 
     # the contract's run: W untimed warm-up iterations from the reference state, then exactly K timed
     # iterations continuing from there (so the first iteration's unfused residual is in the warm-up)
+    progress("warm-up + timed run")
     init()
     if args.warmup > 0:
         run(args.warmup)
@@ -656,6 +674,7 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
         sample_cfg = CONFIGS[args.config]
+        progress("cpu baseline (float64 oracle, bounded sample)")
         out["cpu_baseline"] = cpu_baseline(sample_cfg, args.cpu_sample_T if ndim == 2 else 8, threads)
     print(json.dumps(out), flush=True)
     if dist is not None:

@@ -54,7 +54,9 @@ __device__ __forceinline__ double theta_of(double dd) {
 // t-slab phases (p.slab, xt_phase 1 / 2) as in the fp32 kernels: global-row pivots, zero-carry forward sweep
 // storing every row, backward sweep from the right carry (carry_y) -- oracle/slab_oracle.py.
 // grid: nb column blocks; block NT; LDS (N + N/16 + TwLds<N> + N (+ 128 HR)) * 16 B.
-template <int N, int NT, bool HR = false>
+// BPR: b' / x of the thread's items in registers instead of the LDS array (nx <= 2048: IT <= 4 items leave the
+// registers for it, and the smaller LDS footprint admits a second workgroup per CU).
+template <int N, int NT, bool HR = false, bool BPR = false>
 __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const double2* __restrict__ twx) {
   using C = double2;
   constexpr int IT = N / NT;
@@ -65,8 +67,9 @@ __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const do
   extern __shared__ __align__(16) unsigned char smem_raw[];
   C* A = reinterpret_cast<C*>(smem_raw);
   C* twl = A + LINE;
-  C* bp = twl + TwLds<N>::SIZE;   // b' / x per item
-  C* rsw = bp + N;                // HR: W_{2N}^j and W_{2N}^{64 j}, j < 64
+  C* bp = twl + TwLds<N>::SIZE;   // b' / x per item (BPR: unused, none allocated)
+  C* rsw = bp + (BPR ? 0 : N);    // HR: W_{2N}^j and W_{2N}^{64 j}, j < 64
+  static_assert(!(BPR && HR), "half-real blocks keep b' in LDS");
   fill_twlds<C, N>(twl, twx, HR ? 2 : 1);   // HR: twx holds W_{2N}
   if constexpr (HR) {
     static_assert(N == 4096, "split-twiddle tables sized for 2N = 8192");
@@ -109,6 +112,15 @@ __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const do
   // c1: forward dd, then e^-th once converged; backward theta.  c2: forward h = 1 - g; backward E_{k+2}, or
   // e^-th once converged.
   C c1[IT], c2[IT], pf[IT];
+  C bpr[BPR ? IT : 1];
+  auto bp_ld = [&](int i) -> C {
+    if constexpr (BPR) return bpr[i];
+    else return bp[kx_of(i)];
+  };
+  auto bp_st = [&](int i, C v) {
+    if constexpr (BPR) bpr[i] = v;
+    else bp[kx_of(i)] = v;
+  };
   // kf[i]: the first row from which item i uses the converged pivot: th (k+1) > 20 in every lane of the wave
   // (kf = floor(20 / min th) over the wave's two modes per lane); wave-uniform, held in SGPRs
   int kf[IT];
@@ -134,7 +146,7 @@ __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const do
       c1[i] = dd_of(i);
       // h_{j0-1}: 1 entering the window; a t-slab's entry pivot state in closed form (h_entry)
       c2[i] = slab ? make_double2(h_entry(c1[i].x, j0), h_entry(c1[i].y, j0)) : make_double2(1.0, 1.0);
-      bp[kx_of(i)] = make_double2(0.0, 0.0);   // zero carry (a t-slab's carry is folded in by k_slab_fix)
+      bp_st(i, make_double2(0.0, 0.0));   // zero carry (a t-slab's carry is folded in by k_slab_fix)
     }
     // ---------------- forward: DHT_x + elimination ----------------
     //   s = dd + h_{k-1},  g_k = 1/(1+s),  h_k = s g_k,  b'_k = (rhs/ae + b'_{k-1}) g_k
@@ -157,10 +169,9 @@ __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const do
       const auto dst = rowr(k);
 #pragma unroll
       for (int i = 0; i < IT; ++i) {
-        const int kx = kx_of(i);
         double ha, hb;
         unpack2(i, ha, hb);
-        const C b0 = bp[kx];
+        const C b0 = bp_ld(i);
         const double r0 = ha * inv_ae + b0.x, r1 = hb * inv_ae + b0.y;
         C bn;
         const int kfj = max(kf[i], j0);
@@ -180,7 +191,7 @@ __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const do
           else bn = make_double2(r0 / (c1[i].x + c2[i].x), r1 / (c1[i].y + c2[i].y));
           if (slab) buf_st2(dst, voff, i * NT * (int)sizeof(C), bn);   // re-read after the carry fix-up
         }
-        bp[kx] = bn;
+        bp_st(i, bn);
       }
       lds_sync();
     }
@@ -201,8 +212,8 @@ __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const do
     } else {                  // E_{k+2} for the first substituted row, k = ks (global j0 + ks)
       c2[i] = make_double2(expm1(-2.0 * c1[i].x * (j0 + ks + 2)), expm1(-2.0 * c1[i].y * (j0 + ks + 2)));
     }
-    if (slab) bp[kx_of(i)] = p.carry_y ? reinterpret_cast<const C*>(p.carry_y + (size_t)b * M)[kx_of(i)]
-                                       : make_double2(0.0, 0.0);
+    if (slab) bp_st(i, p.carry_y ? reinterpret_cast<const C*>(p.carry_y + (size_t)b * M)[kx_of(i)]
+                                 : make_double2(0.0, 0.0));
   }
   if (ks >= 0) ldrow(ks);
   for (int k = T - 1; k >= 0; --k) {
@@ -213,8 +224,7 @@ __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const do
         c2[i] = make_double2(expm1(-2.0 * c1[i].x * (kg + 2)), expm1(-2.0 * c1[i].y * (kg + 2)));
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
-      const int kx = kx_of(i);
-      C x = bp[kx];
+      C x = bp_ld(i);
       if (k <= ks) {
         double g0, g1;
         if (kg >= kf[i]) {
@@ -228,7 +238,7 @@ __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const do
           c2[i] = make_double2(e0, e1);
         }
         x = make_double2(pf[i].x + g0 * x.x, pf[i].y + g1 * x.y);
-        bp[kx] = x;
+        bp_st(i, x);
       }
       stage2(i, x);
     }

@@ -160,6 +160,7 @@ struct Impl : ImplBase {
   bool xt_dma = false;            // x transform with the rows staged HBM -> LDS by DMA (k_precond_xt_dma_2d)
   bool t1_xt64 = false;           // fp64 T = 1 windows: k_precond_x_t1_2d<..., double> (shares PDHG_T1_XT)
   bool f64_xt = false;            // fp64 nx = 4096: in-place line + register carries (k_precond_xt_f64_2d)
+  int xt64_var = 0;               // nx = 2048 shape of it (threads, b' in registers or LDS)
   bool thomas_chunk = false;      // 1-D: t-solve in chunks of 32 rows (k_thomas_chunk_1d)
   bool fs_wide = true;            // four-step DHT with 64-column / 32-row tiles (k_fs1w_1d / k_fs2w_1d)
   int f16_group = 16;             // rows n1 per load group of k_f16a_fwd_1d (PDHG_F16_GROUP: 4, 8, 16; 16 measured best)
@@ -293,8 +294,12 @@ struct Impl : ImplBase {
       // fp64 nx = 4096 (C3's grid in the reference's precision): k_precond_xt_f64_2d keeps the carries in
       // registers, so the column pair (B = 2) fits LDS although 5 M reals would not
       // (t-slab phases too: kernels_xt_f64.hpp)
+      // fp64 nx = 2048 (C2's grid): the same kernel with b' in registers (BPR) instead of the generic runtime-radix
+      // kernel's global carries (10.97 ms at C2, 0.15 of the HBM roofline, round 4)
       f64_xt = sizeof(R) == 8 && pb.bc_x == 0 && !xslab &&
-               ((nxg == 4096 && B == 2) || (nxg == 8192 && half_real));
+               (((nxg == 4096 || nxg == 2048) && B == 2) || (nxg == 8192 && half_real));
+      if (const char* e = getenv("PDHG_XT64")) f64_xt = f64_xt && atoi(e) != 0;   // A/B: 0 = generic kernel
+      if (const char* e = getenv("PDHG_XT64_VAR")) xt64_var = atoi(e);              // A/B: nx = 2048 shapes
       // fp64 one-row windows at a power-of-two nx: the carry-free transform needs only the padded lines
       t1_xt64 = sizeof(R) == 8 && T == 1 && pb.bc_x == 0 && !half_real && !xslab && !slab && plx.pow2 &&
                 nxg >= 512 && nxg <= 4096 && nxg * (B / 2) == (nxg == 4096 ? 4096 : 2048);
@@ -991,6 +996,23 @@ struct Impl : ImplBase {
           const size_t lds = (size_t)(Pad<4096>::LINE + TwLds<4096>::SIZE + 4096 + 128) * sizeof(C);
           if ((rc = ensure_lds(k_precond_xt_f64_2d<4096, 512, true>, lds))) return rc;
           hipLaunchKernelGGL((k_precond_xt_f64_2d<4096, 512, true>), dim3(nblk), dim3(512), lds, stream, p, twx);
+          HIP_TRY(hipGetLastError());
+          return PDHG_OK;
+        }
+        if (p.nx == 2048) {   // b' in registers (IT = 4 at 512 threads; PDHG_XT64_VAR: A/B of the shapes)
+          const int var = xt64_var;
+          auto go = [&](auto kern, int nt, bool bpr) -> int {
+            const size_t lds = (size_t)(Pad<2048>::LINE + TwLds<2048>::SIZE + (bpr ? 0 : 2048)) * sizeof(C);
+            int r2;
+            if ((r2 = ensure_lds(kern, lds))) return r2;
+            hipLaunchKernelGGL(kern, dim3(nblk), dim3(nt), lds, stream, p, twx);
+            return (int)PDHG_OK;
+          };
+          if (var == 1) rc = go(k_precond_xt_f64_2d<2048, 256, false, false>, 256, false);
+          else if (var == 2) rc = go(k_precond_xt_f64_2d<2048, 256, false, true>, 256, true);
+          else if (var == 3) rc = go(k_precond_xt_f64_2d<2048, 1024, false, true>, 1024, true);
+          else rc = go(k_precond_xt_f64_2d<2048, 512, false, true>, 512, true);
+          if (rc) return rc;
           HIP_TRY(hipGetLastError());
           return PDHG_OK;
         }

@@ -16,6 +16,10 @@ From the reference initial state (utils_pdhg_solver.py:123-137: phi rows = g, rh
       M u1 = 1:    u1_k = (1 - cosh(th (T + 1/2 - k)) / cosh(th (T + 1/2))) / dd
       M u2 = e_T:  u2_k = sinh(th k) / (2 cosh(th (T + 1/2)) sinh(th / 2))
   and phi''_k = g + tau U_k, phi_bar''_k = g + 2 tau U_k -- one inverse FFT per sampled row, no window-sized array.
+
+The dual steps are local in x (one-sided differences and the Laplacian reach x +- 1), so they are evaluated on
+BANDS of x rows (the oracle on the band with one margin row either side, periodic wrap only reaching the margins):
+at C4's 67 M-point plane a full-plane oracle dual step takes minutes on the host.
 """
 import os
 
@@ -38,16 +42,33 @@ def grid_problem(egno, nx, ny, T, epsl, period=2.0):
                 fv=O.compute_Dxx_fft_fv(2, (nx, ny), dsp, bc), xs=x_arr[0, :, 0, 0], ys=x_arr[0, 0, :, 1])
 
 
-def iteration1_plane(P, sigma, c_on_rho=70.0):
-    """(r, a): the dual step of iteration 1 (one plane; every row of rho', alp' equals it)."""
-    g = P["g"]
+def band(nx, x0, w):
+    """x rows of a band [x0, x0 + w) with one margin row either side (periodic indices); interior = [1:-1]."""
+    return np.arange(x0 - 1, x0 + w + 1) % nx
+
+
+def _xa(P, idx):
+    return P["x_arr"] if idx is None else P["x_arr"][:, idx]
+
+
+def _cut(a, idx):
+    return a if idx is None else a[idx]
+
+
+def _inner(a, idx):
+    return a if idx is None else a[1:-1]
+
+
+def iteration1_plane(P, sigma, c_on_rho=70.0, idx=None):
+    """(r, a): the dual step of iteration 1 (one plane; every row of rho', alp' equals it); idx: on a band only."""
+    g = _cut(P["g"], idx)
     n_ctrl = 1 if P["egno"] == 3 else 2
     phibar = np.stack([g, g])
     rho = np.full((1,) + g.shape, c_on_rho)
     alp = tuple(np.zeros((1,) + g.shape + (n_ctrl,)) for _ in range(4))
-    r, a, _ = O.update_dual_oneiter(phibar, rho, c_on_rho, alp, sigma, P["dt"], P["dsp"], P["epsl"], P["x_arr"], None,
+    r, a, _ = O.update_dual_oneiter(phibar, rho, c_on_rho, alp, sigma, P["dt"], P["dsp"], P["epsl"], _xa(P, idx), None,
                                     P["bc"], P["fns"], 2)
-    return r[0], tuple(x[0] for x in a)
+    return _inner(r[0], idx), tuple(_inner(x[0], idx) for x in a)
 
 
 def _theta(dd):
@@ -74,12 +95,12 @@ class Iteration2:
         if P["bc"] != (0, 0):
             raise NotImplementedError("periodic bc only (FFT2 modes)")
         dt = P["dt"]
-        rho2 = np.stack([r, r])
-        alp2 = tuple(np.stack([x, x]) for x in a)
-        R2 = O.compute_cont_residual_2d(rho2, alp2, dt, P["dsp"], P["fns"], c_on_rho, P["epsl"], P["x_arr"], None,
-                                        P["bc"])
-        Q = R2[-2]                        # an interior row (rho_{j+1} = rho_j)
+        # the oracle's residual of a one-row window is the last row's, Q + (c - r)/dt (update_fns_in_pdhg.py:95)
+        R1 = O.compute_cont_residual_2d(r[None], tuple(x[None] for x in a), dt, P["dsp"], P["fns"], c_on_rho,
+                                        P["epsl"], P["x_arr"], None, P["bc"])
         W = (c_on_rho - r) / dt           # the last row's extra term
+        Q = R1[-1] - W                    # an interior row (rho_{j+1} = rho_j)
+        del R1
         self.Qh = sfft.fft2(Q, workers=_W)
         self.Wh = sfft.fft2(W, workers=_W)
         self.dd = (C - np.asarray(P["fv"]).real) * dt * dt
@@ -98,8 +119,11 @@ class Iteration2:
         return self.g + 2.0 * tau * self.U(k)
 
 
-def dual_row(P, pb_j, pb_j1, r, a, sigma, c_on_rho=70.0):
-    """rho'' / alp'' of row j from phi_bar rows j, j+1 and the row's (r, a) (the oracle's dual on a one-row window)."""
-    rn, an, _ = O.update_dual_oneiter(np.stack([pb_j, pb_j1]), r[None], c_on_rho, tuple(x[None] for x in a), sigma,
-                                      P["dt"], P["dsp"], P["epsl"], P["x_arr"], None, P["bc"], P["fns"], 2)
-    return rn[0], tuple(x[0] for x in an)
+def dual_row(P, pb_j, pb_j1, r, a, sigma, c_on_rho=70.0, idx=None):
+    """rho'' / alp'' of row j from phi_bar rows j, j+1 and the row's (r, a) (the oracle's dual on a one-row window);
+    idx: on a band of x rows (inputs are full planes, the result the band's interior)."""
+    c = lambda v: _cut(v, idx)  # noqa: E731
+    rn, an, _ = O.update_dual_oneiter(np.stack([c(pb_j), c(pb_j1)]), c(r)[None], c_on_rho,
+                                      tuple(c(x)[None] for x in a), sigma, P["dt"], P["dsp"], P["epsl"], _xa(P, idx),
+                                      None, P["bc"], P["fns"], 2)
+    return _inner(rn[0], idx), tuple(_inner(x[0], idx) for x in an)

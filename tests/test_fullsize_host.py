@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 
 import pdhg_oracle as O
-from _fullsize import Iteration2, dual_row, grid_problem, iteration1_plane, mode_weights
+from _fullsize import Iteration2, band, dual_row, grid_problem, iteration1_plane, mode_weights
 
 TAU, SIGMA = 0.1 / 1.5, 0.1 * 1.5
 
@@ -52,6 +52,16 @@ def test_predictor_matches_oracle(egno, nx, ny, T, epsl):
         for k in range(4):
             if np.linalg.norm(alp2[k][j]) > 0:
                 assert _rel(an[k], alp2[k][j]) < 1e-12, (j, k)
+    # the band forms (x rows [x0, x0 + w), margins wrapping periodically) equal the full-plane values there
+    for x0, w in ((0, 5), (nx - 4, 4), (nx // 2, 3)):
+        idx = band(nx, x0, w)
+        rows_ = np.arange(x0, x0 + w) % nx
+        rb, ab = iteration1_plane(P, SIGMA, idx=idx)
+        assert np.array_equal(rb, r[rows_]) and all(np.array_equal(x, y[rows_]) for x, y in zip(ab, a))
+        j = T // 2
+        rn, an = dual_row(P, it2.phi_bar(j, TAU), it2.phi_bar(j + 1, TAU), r, a, SIGMA)
+        rnb, anb = dual_row(P, it2.phi_bar(j, TAU), it2.phi_bar(j + 1, TAU), r, a, SIGMA, idx=idx)
+        assert np.array_equal(rnb, rn[rows_]) and all(np.array_equal(x, y[rows_]) for x, y in zip(anb, an))
 
 
 def test_mode_weights_solve_the_tridiagonal_systems():

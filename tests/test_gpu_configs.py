@@ -323,7 +323,11 @@ FP64_CASES = {
     "c3_ws_T200": {"f64_xt": 1},
     "c3_fr_4096x256": {"f64_xt": 1, "dual64": 1},
     "c3_rows_ny4096": {"res64": 1, "dual64": 1},
-    "c2_x2048": {"dual64": 1},
+    "c2_x2048": {"dual64": 1, "f64_xt": 1},   # k_precond_xt_f64_2d<2048, 512, false, BPR> (round 5)
+    "c2_x2048+generic": {"dual64": 1, "f64_xt": 0},   # the generic runtime-radix kernel it replaced
+    "c2_x2048+v1": {"f64_xt": 1},   # the A/B shapes of the nx = 2048 kernel (PDHG_XT64_VAR)
+    "c2_x2048+v2": {"f64_xt": 1},
+    "c2_x2048+v3": {"f64_xt": 1},
     "c2_rows_ny2048": {"res64": 1, "dual64": 1},
     "c1_exact": {"glb_line": 1, "fs16": 1},   # the 16 x 4096 split on complex doubles (kernels_fs16.hpp)
     "c4_halfreal_x8192": {"f64_xt": 1, "half_real": 1, "dual64": 1},   # k_precond_xt_f64_2d<4096, 512, HR>
@@ -333,7 +337,8 @@ FP64_CASES = {
     "c3_rows_ny4096+fr": {"res64": 1, "dual64": 1, "fused_residual": 1, "dual_ypl": 2},
     "c2_rows_ny2048+fr": {"res64": 1, "dual64": 1, "fused_residual": 1, "dual_ypl": 2},
 }
-FP64_ENV = {"fr": {"PDHG_FUSE_RES": "1", "PDHG_SHORT_T": "0"}}
+FP64_ENV = {"fr": {"PDHG_FUSE_RES": "1", "PDHG_SHORT_T": "0"}, "generic": {"PDHG_XT64": "0"},
+           "v1": {"PDHG_XT64_VAR": "1"}, "v2": {"PDHG_XT64_VAR": "2"}, "v3": {"PDHG_XT64_VAR": "3"}}
 FP64_BAR = 1e-9
 
 
