@@ -29,6 +29,8 @@ CASES = [
     (1, 512, 2048, 8, 2, 1, {"res64": 1}),                    # 4-row residual kernels, halo row split off
     (2, 512, 2048, 12, 3, 2, {"res64": 1}),                   # two buffer sets, dual sub-iterations
     (2, 4096, 2048, 8, 2, 1, {"res64": 1, "f64_xt": 1}),      # C3's x extent with the 4-row row kernels
+    # C3's whole plane (what bench.py --gpus N runs per slab): the fused fp64 sweep inside the slabs by default
+    (2, 4096, 4096, 16, 2, 1, {"res64": 1, "f64_xt": 1, "fused_residual": 1, "dual_ypl": 2}),
 ]
 
 
