@@ -175,7 +175,10 @@ def PDHG_multi_step(fn_update_primal, fn_update_dual, fns_dict, g, x_arr, ndim, 
         # the last saved window's entries.  Here that window is solved again: every window's phi0 repeats one row
         # (:123, and the warm start adds the same row to every row, :201-203), and that row is phi_all[-1][0]
         # (row 0 never changes, utils_precond.py:139/177), so its start state is known exactly -- rho / alp from
-        # the window before it (or the initial ones) -- and the run continues as the uninterrupted one.
+        # the window before it (or the initial ones).  The 5-entry list holds no step size: the re-solved window
+        # and those after it start from the CALLER's stepsz_param, so the run matches the uninterrupted one only
+        # when no earlier window backed off (after a NaN back-off the uninterrupted run had continued at the
+        # reduced step; tests/test_host.py::test_resume_5_entry_list_after_backoff).
         middle = load_middle_solution(load_middle_dir, load_middle_prefix)
         max_iters, phi_all, rho_all, alp_all, errs_all = [middle[0]] + [list(m) for m in middle[1:5]]
         init_t = len(phi_all)

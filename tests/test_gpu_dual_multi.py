@@ -27,6 +27,7 @@ CASES = [
     (2, 2, 16, 512, 4, 1e-3),
     (3, 2, 24, 256, 2, 0.0),
     (2, 2, 64, 256, 1, 0.1),
+    (2, 2, 512, 256, 8, 1e-3),   # time chunks of 2 rows (jchunk_d = 2 < T, gzd = 4) on a 512-row grid
 ]
 IDS = ["e{}_{}x{}_T{}_eps{}".format(c[0], c[2], c[3], c[4], c[5]) for c in CASES]
 

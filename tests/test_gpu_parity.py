@@ -552,14 +552,23 @@ def test_fp64_nx4096_x_transform(native, case):
     assert abs(st["err1"] - e1_o) <= 1e-8 * e1_o and abs(st["err2"] - e2_o) <= 1e-8 * e2_o
 
 
-def test_marching_window_counts_fp64(native):
+@pytest.mark.parametrize("head,k1", [("1", "1"), ("0", "1"), ("1", "0"), ("0", "0")],
+                         ids=["default", "head0", "k1outer0", "head0_k1outer0"])
+def test_marching_window_counts_fp64(native, monkeypatch, parity_log, head, k1):
     """The marching default's per-window stop iterations (PDHG_multi_step, utils_pdhg_solver.py:97-225; T = 1
     windows, rho_alp_iters = 10, eps 1e-6, NaN back-off) in the reference's arithmetic: the fp64 device driver
     against the float64 oracle's counts at C2's dt on 64^2 (tests/golden/marching_c2dt_64.json, window 1 backs
     off to stepsz 0.09).  Counts within one iteration, the same step size per window, the final state to 1e-8.
+    With the dual loop's head form and the outer-sum skip after a one-sub-iteration loop on (the defaults) and off
+    (PDHG_DUAL_HEAD=0: every sub-iteration per-sub-iteration; PDHG_K1_OUTER=0: always the outer-sum pass), the
+    counts are logged per variant (parity_log) -- both shortcuts change sums by rounding only.
     (fp32 stops elsewhere: err1 < 1e-6 is within a few float32 ulps of relative change)"""
     import json
     from pdhg_amd import set_fns, utils_pdhg_solver as S
+    from pdhg_amd import update_fns_in_pdhg as U
+    monkeypatch.setenv("PDHG_DUAL_HEAD", head)
+    monkeypatch.setenv("PDHG_K1_OUTER", k1)
+    U.clear_cache()
     F = json.load(open(os.path.join(HERE, "golden", "marching_c2dt_64.json")))
     nx, ny, ndim, egno = F["nx"], F["ny"], F["ndim"], F["egno"]
     fns = set_fns.set_up_example_fns(egno, ndim, 0)
@@ -580,6 +589,9 @@ def test_marching_window_counts_fp64(native):
         iters.append(int(st["window_iters"]))
         stepsz.append(s - 0.01 * nan_attempts)
     assert len(iters) == F["windows"], stats
+    parity_log("test_marching_window_counts_fp64", "head{}_k1outer{}".format(head, k1),
+               {"max_count_diff": max(abs(a - b) for a, b in zip(iters, F["window_iters"]))}, {"max_count_diff": 1},
+               iters=iters, oracle_iters=F["window_iters"])
     assert all(abs(a - b) <= 1 for a, b in zip(iters, F["window_iters"])), (iters, F["window_iters"])
     assert np.allclose(stepsz, F["window_stepsz"], rtol=0, atol=1e-12), (stepsz, F["window_stepsz"])
     _, phi, rho, _ = res[0]

@@ -209,6 +209,48 @@ def test_resume_after_backoff_keeps_the_schedule(tmp_path, monkeypatch):
         assert a.shape == b.shape and np.array_equal(a, b)
 
 
+def test_resume_5_entry_list_after_backoff(tmp_path, monkeypatch):
+    """The reference's 5-entry middle list holds no step size (utils_pdhg_solver.py:211-212).  Resuming from it after
+    a NaN back-off (window 0: 0.1 -> 0.09) re-solves the last saved window (1) and continues at the CALLER's step
+    size, 0.1, where the uninterrupted run had continued at 0.09: window 0 comes back from the file bit for bit,
+    window 1 is re-solved at 0.1 (so its state is not the uninterrupted run's), window 2 backs off 0.1 -> 0.07."""
+    nx, nt = 8, 5
+    x, fns, g, fv = _setup(nx, nt)
+    primal, dual = O.make_update_fns(1, 0, rho_alp_iters=1)
+    tried = {"s": [], "r": []}
+
+    def mk(key):
+        def p2(phi, rho, c, alp, tau, dt, ds, f, fv_, epsl, xa, t):
+            step = round(tau * 1.5, 12)
+            w = int(round(float(np.asarray(t).ravel()[0]) / dt)) - 1
+            if not tried[key] or tried[key][-1] != (w, step):
+                tried[key].append((w, step))
+            out = primal(phi, rho, c, alp, tau, dt, ds, f, fv_, epsl, xa, t)
+            thr = {0: 0.095, 2: 0.075}.get(w, 1.0)
+            return out * np.nan if step > thr else out
+        return p2
+    kw = dict(time_step_per_PDHG=2, stepsz_param=0.1, n_ctrl=1, fv=fv, N_maxiter=40, print_freq=10, eps=1e-6,
+              verbose=False)
+    real_save = S.save
+
+    def save_and_snapshot(d, prefix, results):
+        real_save(d, prefix, results)
+        if len(results[1]) == 2:
+            real_save(d, "ref5", list(results[:5]))
+    monkeypatch.setattr(S, "save", save_and_snapshot)
+    res_s, _ = S.PDHG_multi_step(mk("s"), dual, fns, g, x, 1, nt, (nx,), 0.25, (2.0 / nx,), 70.0,
+                                 save_middle_dir=str(tmp_path), save_middle_prefix="mid", **kw)
+    assert [s for w, s in tried["s"] if w == 1] == [0.09]
+    res_r, _ = S.PDHG_multi_step(mk("r"), dual, fns, g, x, 1, nt, (nx,), 0.25, (2.0 / nx,), 70.0,
+                                 load_middle_dir=str(tmp_path), load_middle_prefix="ref5", **kw)
+    assert [s for w, s in tried["r"] if w == 1] == [0.1]
+    assert [s for w, s in tried["r"] if w == 2] == [0.1, 0.09, 0.08, 0.07]
+    assert not any(w == 0 for w, _ in tried["r"])                       # window 0 restored, not re-solved
+    phi_s, phi_r = res_s[0][1], res_r[0][1]
+    assert np.array_equal(phi_r[0], phi_s[0])                          # window 0's rows from the file
+    assert not np.array_equal(res_r[0][2][1], res_s[0][2][1])          # window 1 re-solved at another step
+
+
 def test_dropin_default_precision_is_fp64():
     """The drop-ins compute in float64 unless asked otherwise, as the reference (update_fns_in_pdhg.py:10)."""
     from pdhg_amd import update_fns_in_pdhg as U
