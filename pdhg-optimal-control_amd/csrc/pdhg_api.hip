@@ -287,6 +287,11 @@ struct Impl : ImplBase {
       int nyp = 2;
       while (nyp < ny) nyp <<= 1;
       if (B > nyp) B = nyp;
+      // fp64 nx = 512 / 1024 with T > 1: one column pair per block (B = 2) for the fp64 x kernel below (the generic
+      // kernel would take B = 8 / 4 with its carries in global memory); T = 1 keeps the one-row kernel's B
+      const bool f64_small = sizeof(R) == 8 && pb.bc_x == 0 && !xslab && T > 1 && (nxg == 1024 || nxg == 512) &&
+                             ny % 2 == 0 && [] { const char* e = getenv("PDHG_XT64"); return !e || atoi(e) != 0; }();
+      if (f64_small) B = 2;
       // fp32 nx = 8192 (C4): one real column per block, packed into a 4096-point FFT (half_real)
       // fp64 nx = 8192 (C4's grid in the reference's precision): the same half-real split in k_precond_xt_f64_2d<HR>
       half_real = nxg == 8192 && pb.bc_x == 0 && (sizeof(R) == 4 || !xslab);
@@ -297,7 +302,7 @@ struct Impl : ImplBase {
       // fp64 nx = 2048 (C2's grid): the same kernel with b' in registers (BPR) instead of the generic runtime-radix
       // kernel's global carries (10.97 ms at C2, 0.15 of the HBM roofline, round 4)
       f64_xt = sizeof(R) == 8 && pb.bc_x == 0 && !xslab &&
-               (((nxg == 4096 || nxg == 2048) && B == 2) || (nxg == 8192 && half_real));
+               (((nxg == 4096 || nxg == 2048) && B == 2) || (nxg == 8192 && half_real) || f64_small);
       if (const char* e = getenv("PDHG_XT64")) f64_xt = f64_xt && atoi(e) != 0;   // A/B: 0 = generic kernel
       if (const char* e = getenv("PDHG_XT64_VAR")) xt64_var = atoi(e);              // A/B: nx = 2048 shapes
       // fp64 one-row windows at a power-of-two nx: the carry-free transform needs only the padded lines
@@ -996,6 +1001,21 @@ struct Impl : ImplBase {
           const size_t lds = (size_t)(Pad<4096>::LINE + TwLds<4096>::SIZE + 4096 + 128) * sizeof(C);
           if ((rc = ensure_lds(k_precond_xt_f64_2d<4096, 512, true>, lds))) return rc;
           hipLaunchKernelGGL((k_precond_xt_f64_2d<4096, 512, true>), dim3(nblk), dim3(512), lds, stream, p, twx);
+          HIP_TRY(hipGetLastError());
+          return PDHG_OK;
+        }
+        if (p.nx == 1024 || p.nx == 512) {   // b' in registers, 4 items per thread
+          const size_t lds = (size_t)((p.nx == 1024 ? Pad<1024>::LINE + TwLds<1024>::SIZE : Pad<512>::LINE +
+                                       TwLds<512>::SIZE)) * sizeof(C);
+          auto go = [&](auto kern, int nt) -> int {
+            int r2;
+            if ((r2 = ensure_lds(kern, lds))) return r2;
+            hipLaunchKernelGGL(kern, dim3(nblk), dim3(nt), lds, stream, p, twx);
+            return (int)PDHG_OK;
+          };
+          rc = p.nx == 1024 ? go(k_precond_xt_f64_2d<1024, 256, false, true>, 256)
+                            : go(k_precond_xt_f64_2d<512, 128, false, true>, 128);
+          if (rc) return rc;
           HIP_TRY(hipGetLastError());
           return PDHG_OK;
         }

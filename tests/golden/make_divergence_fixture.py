@@ -32,6 +32,12 @@ random signs (np.random.default_rng(7)), at the same sample points -> divergence
 distance to the "points" fixture is how far two float64 runs of the reference algorithm that differ by one rounding
 drift apart through the instability: the spread any float64 implementation has against the oracle pointwise.
 
+Other-FFT-library variant (argument "points_npfft", round 5): the same float64 run with every FFT of the oracle
+through numpy.fft instead of scipy.fft (a different pocketfft build: the two differ by ~4e-16 relative on one
+transform) -> divergence_c3_plane_T4_points_npfft.npz.  It is the like-for-like spread of the reference algorithm
+on another FFT library -- what the reference itself (XLA's FFT) could differ from the oracle by -- without the
+one-ulp perturbation of every input entry that "points_ulp" applies.
+
 Pointwise variant (argument "points"): the float64 oracle's phi' and rho' at NPTS fixed sample points of the plane
 (rows 1..T of phi', every row of rho'; indices from np.random.default_rng(20250117)) after each of the first
 max_iters iterations -> divergence_c3_plane_T{T}_points.npz.  tests/test_gpu_divergence.py compares the fp64
@@ -135,12 +141,22 @@ if __name__ == "__main__":
     T = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     max_iters = int(sys.argv[2]) if len(sys.argv) > 2 else 24
     f32 = len(sys.argv) > 3 and sys.argv[3] == "f32"   # the float32 oracle (until its first NaN)
-    points = len(sys.argv) > 3 and sys.argv[3] in ("points", "points_ulp")
+    points = len(sys.argv) > 3 and sys.argv[3] in ("points", "points_ulp", "points_npfft")
     ulp = len(sys.argv) > 3 and sys.argv[3] == "points_ulp"
+    npfft = len(sys.argv) > 3 and sys.argv[3] == "points_npfft"
+    if npfft:   # the oracle's FFTs through numpy.fft (periodic bc: fft2 / ifft2 only)
+        import types
+        sf = O.sfft
+        O.sfft = types.SimpleNamespace(
+            fft2=lambda a, axes=(-2, -1), workers=None: np.fft.fft2(a, axes=axes),
+            ifft2=lambda a, axes=(-2, -1), workers=None: np.fft.ifft2(a, axes=axes),
+            fft=lambda a, axis=-1, workers=None: np.fft.fft(a, axis=axis),
+            ifft=lambda a, axis=-1, workers=None: np.fft.ifft(a, axis=axis),
+            dct=sf.dct, idct=sf.idct)
     nx = ny = 4096
     S = setup(nx, ny, T, 1.0 / 200, 0.1, np.float32 if f32 else np.float64)
     out = os.path.join(HERE, "divergence_c3_plane_T{}{}.npz".format(
-        T, "_f32" if f32 else "_points_ulp" if ulp else "_points" if points else ""))
+        T, "_f32" if f32 else "_points_ulp" if ulp else "_points_npfft" if npfft else "_points" if points else ""))
     if points:
         S.update(points=sample_points(T, nx, ny), phi_pts=[], rho_pts=[])
     if ulp:

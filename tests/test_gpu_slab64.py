@@ -20,7 +20,7 @@ TOL = 1e-11
 
 CASES = [
     # (egno, nx, ny, T, P, k, expected path_info)
-    (1, 512, 256, 6, 2, 1, {"f64_xt": 0, "res64": 0}),        # generic x kernel, generic row kernels
+    (1, 512, 256, 6, 2, 1, {"f64_xt": 1, "res64": 0}),        # fp64 x kernel at nx = 512 (B = 2), generic rows
     (2, 4096, 256, 50, 2, 1, {"f64_xt": 1}),                  # 25-row slabs (C3's on 8 GPUs): fp64 nx = 4096 kernel
     (2, 4096, 256, 11, 3, 1, {"f64_xt": 1}),                  # 4 + 4 + 3 rows
     (2, 8192, 256, 5, 2, 1, {"f64_xt": 1, "half_real": 1}),   # C4's nx: half-real split
@@ -90,6 +90,16 @@ def test_fp64_slabs_match_single_context(native, parity_log, egno, nx, ny, T, nr
     parity_log("test_fp64_slabs_match_single_context", "e{}_{}x{}_T{}_P{}_k{}".format(egno, nx, ny, T, nr, k), m,
                bounds)
     assert all(m[key] <= bounds[key] for key in m), m
+
+
+def test_fp64_slabs_generic_x_kernel(native, parity_log, monkeypatch):
+    """The generic runtime-radix x kernel's slab phases in fp64 (PDHG_XT64=0: 8 columns per block at nx = 512)."""
+    monkeypatch.setenv("PDHG_XT64", "0")
+    P = make_problem(2, 2, 512, 256, 7, 0.0)
+    st, st_ref, got, want = _run_pair(P, 3, 1, 6, {"f64_xt": 0})
+    m = _metrics(st, st_ref, got, want)
+    parity_log("test_fp64_slabs_generic_x_kernel", "e2_512x256_T7_P3", m, {key: TOL for key in m})
+    assert all(v <= TOL for v in m.values()), m
 
 
 @pytest.mark.parametrize("nx,ny,T,nr", [(512, 2048, 16, 2), (512, 2048, 9, 3)], ids=["T16_P2", "T9_P3"])

@@ -1,0 +1,40 @@
+"""The fp64 x transform + t-solve kernel (kernels_xt_f64.hpp) at every nx it runs -- 512, 1024 (one column pair per
+block, b' in registers) and 2048 (C2's, BPR) -- against the generic runtime-radix kernel it replaced (PDHG_XT64=0: 2 / 4 / 8 columns per block, carries in global memory) and against the float64 oracle
+(H1_precond_2d, jaxsrc/utils/utils_precond.py:142-178, through update_primal_2d).  Same float64 arithmetic up to
+the transform's association: states within 1e-12 of each other, 1e-9 of the oracle.  (nx = 4096 has no generic
+fp64 kernel to compare with -- 5 M reals of LDS -- and is pinned by the C3 fixtures of test_gpu_configs.py.)"""
+import numpy as np
+import pytest
+
+from _problems import device_ctx, make_problem, oracle_fns, rel
+
+pytestmark = pytest.mark.gpu
+
+TAU, SIGMA = 0.1 / 1.5, 0.1 * 1.5
+
+
+@pytest.mark.parametrize("egno,nx,ny,T", [(1, 512, 256, 12), (2, 1024, 256, 9), (2, 2048, 128, 7)],
+                         ids=["e1_512", "e2_1024", "e2_2048"])
+def test_fp64_x_kernel(native, monkeypatch, parity_log, egno, nx, ny, T):
+    P = make_problem(egno, 2, nx, ny, T, 0.0, seeded=True)
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("PDHG_XT64", flag)
+        ctx = device_ctx(P, "fp64")
+        try:
+            assert ctx.path_info("f64_xt") == int(flag), (flag, ctx.path_info("f64_xt"))
+            ctx.set_state(P["phi"], P["rho"], P["alp"])
+            ctx.update_primal(TAU)
+            phi1 = ctx.get_state(rho=False, alp=False)[0]
+            st = ctx.iterate(3, TAU, SIGMA, -1.0, 1)
+            out[flag] = (phi1, ctx.get_state(), st)
+        finally:
+            ctx.close()
+    primal, _ = oracle_fns(P)
+    phi_o = primal(P["phi"], P["rho"], 70.0, P["alp"], TAU, P["dt"], P["dsp"], P["fns"], P["fv"], 0.0, P["x_arr"], None)
+    (p1, s1, st1), (p0, s0, st0) = out["1"], out["0"]
+    m = {"primal_vs_oracle": rel(p1, phi_o), "primal_vs_generic": rel(p1, p0), "phi": rel(s1[0], s0[0]),
+         "rho": rel(s1[1], s0[1]), "err1": abs(st1["err1"] - st0["err1"]) / st0["err1"]}
+    b = {"primal_vs_oracle": 1e-9, "primal_vs_generic": 1e-12, "phi": 1e-12, "rho": 1e-12, "err1": 1e-10}
+    parity_log("test_fp64_x_kernel", "e{}_{}x{}_T{}".format(egno, nx, ny, T), m, b)
+    assert all(m[k] <= b[k] for k in m), m
