@@ -15,6 +15,16 @@
 // vmcnt is in issue order on gfx9: the wait for S leaves only the stores issued after its DMA outstanding.
 // Barriers are s_barrier + lgkmcnt only (lds_sync), so the DMA spans them.
 // grid: nb; block 1024 (IT = 4 items per thread, the batched kernel's pairing: 16-B global accesses).
+//
+// HR ("half real", nx = 2N = 8192, C4's x extent; B = 1 real column per block): the block row is ONE real column of
+// 2N points, packed as z[m] = x[2m] + i x[2m+1] -- the same N float2 of a row as a column pair's, so the DMA staging
+// and the first radix-16 pass are unchanged -- and split after the transform with realsplit_padded (item k carries
+// the modes k and k + N, as the warp-specialised HR kernel's items); the inverse stages x of both modes at their real
+// positions k and k + N and splits again into the spatial values x[k], x[k + N].  lamx of the modes k + N: the
+// periodic symbol is even, lam(k + N) = lam(2N - k - N) = lam(N - k) (k >= 1; lam(N) = -4/dx^2), so LDS keeps only
+// the first N of the host's values and reads mode k + N's from position N - k -- the host's value itself (forming it
+// as -4/dx^2 - lam(k) cancels: 40 % off for the lowest modes).  The split twiddles W_2N^k come from two 64-entry
+// tables (W^(k mod 64) W^(64 (k / 64))).
 #pragma once
 #include <type_traits>
 #include "kernels_xt_batch.hpp"
@@ -64,12 +74,12 @@ __device__ __forceinline__ void s_read_items(unsigned a, float2 (&v)[2][4]) {
     }
 }
 
-template <int N>
+template <int N, bool HR = false>
 __global__ void __launch_bounds__(1024) k_precond_xt_dma_2d(KP<float> p, const float2* __restrict__ twx) {
   using C = float2;
   constexpr int NT = 1024, RB = 2, NL = 1;
   constexpr int NI = N * NL, IT = NI / NT;
-  constexpr int B = 2 * NL;
+  constexpr int B = 2 * NL;   // reals per item in a row (HR: x[2m], x[2m+1] of the one column)
   constexpr int LINE = Pad<N>::LINE;
   static_assert(N == 4096 && IT == 4, "one 4096-point line per block");
   if (p.ctrl->done) return;
@@ -79,8 +89,11 @@ __global__ void __launch_bounds__(1024) k_precond_xt_dma_2d(KP<float> p, const f
   __shared__ __align__(16) C S[RB * NI];     // RB rows, lane-linear (float2 item i of row r at S[r * NI + i])
   __shared__ __align__(16) C twl[TwLds<N>::SIZE];
   __shared__ float lxs[N];                   // lamx per item: dd is recomputed per row (8 VGPRs fewer)
-  fill_twlds<C, N>(twl, twx);
+  __shared__ C rsw[HR ? 128 : 1];            // HR: W_2N^j and W_2N^(64 j), j < 64
+  fill_twlds<C, N>(twl, twx, HR ? 2 : 1);    // HR: twx holds W_2N
   for (int i = threadIdx.x; i < N; i += NT) lxs[i] = p.lamx[i];
+  if constexpr (HR)
+    for (int i = threadIdx.x; i < 128; i += NT) rsw[i] = twx[i < 64 ? i : 64 * (i - 64)];
   __syncthreads();   // lxs (read by the converged-pivot rows below)
   const int T = p.T, tid = threadIdx.x;
   // the wave index in an SGPR and the lane from mbcnt: the laundered thread index costs no VGPR between uses
@@ -90,16 +103,33 @@ __global__ void __launch_bounds__(1024) k_precond_xt_dma_2d(KP<float> p, const f
   float* wb = p.work + (size_t)b * M;
   const size_t kstride = (size_t)p.nb * M;
   const float inv_ae = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, 1.f / p.ae)));
-  const float ly0 = p.lamy[b * B], ly1 = p.lamy[b * B + 1], Cc = p.C;
+  const float ly0 = p.lamy[HR ? b : b * B], ly1 = p.lamy[HR ? b : b * B + 1], Cc = p.C;
+  // HR: lam(N) (mode N of the 2N-point column, item 0's second mode): the host's value, a uniform load (SGPR)
+  const float lam_n = HR ? p.lamx[N] : 0.f;
+  auto lx_hi = [&](int item) { return item == 0 ? lam_n : lxs[N - item]; };   // HR: lam(item + N)
   auto dd_of = [&](int item) {
     const float lx = lxs[item];
-    return make_float2((Cc - lx - ly0) * inv_ae, (Cc - lx - ly1) * inv_ae);
+    if constexpr (HR) return make_float2((Cc - lx - ly0) * inv_ae, (Cc - lx_hi(item) - ly0) * inv_ae);
+    else return make_float2((Cc - lx - ly0) * inv_ae, (Cc - lx - ly1) * inv_ae);
+    (void)ly1;
+  };
+  // the item's pair of modes from a transformed line: Hartley pair of the two packed columns, or (HR) the real
+  // split of the one column (modes k and k + N)
+  auto unpack2 = [&](const C* line, int k, float& h0, float& h1) {
+    if constexpr (HR) realsplit_padded<C, float>(line, N, k, cmul(rsw[k & 63], rsw[64 + (k >> 6)]), h0, h1);
+    else hartley_padded<C, float>(line, N, k, h0, h1);
   };
   // the thread index is laundered once per batch (tl), so the unrolled loops' LDS / global addresses are
   // recomputed there instead of being hoisted out of the row loops into registers (which spills)
   int tl = tid;
   auto launder = [&]() {
-    tl = wave * 64 + (int)__lane_id();
+    if constexpr (HR) {   // the lane id itself from asm: else the compiler keeps wave*64 + lane live (spilled: HR is
+      int l;              // at 128 VGPRs) as the one input of every launder
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+      tl = wave * 64 + l;
+    } else {
+      tl = wave * 64 + (int)__lane_id();
+    }
     asm volatile("" : "+v"(tl));
   };
   auto item_of = [&](int i) { return 2 * (tl + (i >> 1) * NT) + (i & 1); };
@@ -152,9 +182,8 @@ __global__ void __launch_bounds__(1024) k_precond_xt_dma_2d(KP<float> p, const f
     // last (Neumann) row of the window: u_{T-1} = ae (dd + h_{T-2})
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
-      const float lx = p.lamx[item_of(i)];
-      const float d0 = (Cc - lx - ly0) * inv_ae, d1 = (Cc - lx - ly1) * inv_ae;
-      c2[i] = make_float2(h_entry(d0, p.j0), h_entry(d1, p.j0));
+      const float2 d = dd_of(item_of(i));   // (HR: modes k and k + N)
+      c2[i] = make_float2(h_entry(d.x, p.j0), h_entry(d.y, p.j0));
       c3[i] = make_float2(0.f, 0.f);
     }
     constexpr int nR = N / 16;
@@ -192,7 +221,7 @@ __global__ void __launch_bounds__(1024) k_precond_xt_dma_2d(KP<float> p, const f
 #pragma unroll
           for (int i = 0; i < IT; ++i) {
             float ha, hb;
-            hartley_padded<C, float>(A + r * LINE, N, item_of(i), ha, hb);
+            unpack2(A + r * LINE, item_of(i), ha, hb);
             if (kg >= kf[i]) {   // converged: g = e^-th (in c2 from row kf on: h is no longer needed)
               if (kg == max(kf[i], p.j0)) {   // the first converged row of this sweep (a slab may start past kf)
                 const float2 dd = dd_of(item_of(i));
@@ -213,7 +242,7 @@ __global__ void __launch_bounds__(1024) k_precond_xt_dma_2d(KP<float> p, const f
 #pragma unroll
           for (int i = 0; i < IT; ++i) {
             float ha, hb;
-            hartley_padded<C, float>(A + r * LINE, N, item_of(i), ha, hb);
+            unpack2(A + r * LINE, item_of(i), ha, hb);
             const float2 dd = dd_of(item_of(i));
             if (max(kf[i], p.j0) < kg) {   // converged on an earlier row: dd + h = (1 - g) / g
               const float2 g = c2[i];
@@ -305,8 +334,18 @@ __global__ void __launch_bounds__(1024) k_precond_xt_dma_2d(KP<float> p, const f
           c2[i] = E1;
         }
       }
+      if constexpr (HR) {   // modes k and k + N -> their real positions (float f at element f/2, part f%2)
+        float* Af = reinterpret_cast<float*>(A + r * LINE);
 #pragma unroll
-      for (int i = 0; i < IT; ++i) A[r * LINE + pix(item_of(i))] = c3[i];
+        for (int i = 0; i < IT; ++i) {
+          const int f0 = item_of(i), f1 = item_of(i) + N;
+          Af[2 * pix(f0 >> 1) + (f0 & 1)] = c3[i].x;
+          Af[2 * pix(f1 >> 1) + (f1 & 1)] = c3[i].y;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < IT; ++i) A[r * LINE + pix(item_of(i))] = c3[i];
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -318,15 +357,28 @@ __global__ void __launch_bounds__(1024) k_precond_xt_dma_2d(KP<float> p, const f
       const int k = kt - r;
       if (!FULL && k < 0) break;
       C* wk = row_ptr(k);
-      C o[IT];
+      if constexpr (HR) {   // spatial x[k], x[k + N] of the real column: items 2m, 2m+1 -> float2 at 2m and 2m + N
+        float* wf = reinterpret_cast<float*>(wk);
 #pragma unroll
-      for (int i = 0; i < IT; ++i) {
-        float ha, hb;
-        hartley_padded<C, float>(A + r * LINE, N, item_of(i), ha, hb);
-        o[i] = make_float2(ha, hb);
+        for (int j = 0; j < IT / 2; ++j) {   // pair by pair (fewer values live: the kernel is at 128 VGPRs)
+          float a0, b0, a1, b1;
+          unpack2(A + r * LINE, item_of(2 * j), a0, b0);
+          unpack2(A + r * LINE, item_of(2 * j + 1), a1, b1);
+          const int m2 = 2 * (tl + j * NT);
+          *reinterpret_cast<float2*>(wf + m2) = make_float2(a0, a1);
+          *reinterpret_cast<float2*>(wf + m2 + N) = make_float2(b0, b1);
+        }
+      } else {
+        C o[IT];
+#pragma unroll
+        for (int i = 0; i < IT; ++i) {
+          float ha, hb;
+          unpack2(A + r * LINE, item_of(i), ha, hb);
+          o[i] = make_float2(ha, hb);
+        }
+#pragma unroll
+        for (int j = 0; j < IT / 2; ++j) st_pair(wk, j, o[2 * j], o[2 * j + 1]);
       }
-#pragma unroll
-      for (int j = 0; j < IT / 2; ++j) st_pair(wk, j, o[2 * j], o[2 * j + 1]);
       __builtin_amdgcn_sched_barrier(0);
     }
   };

@@ -158,6 +158,7 @@ struct Impl : ImplBase {
   int xt_rpre = 0;
   bool xt_pair = false;           // batched x transform as 2 rows x 512 threads, two workgroups per CU
   bool xt_dma = false;            // x transform with the rows staged HBM -> LDS by DMA (k_precond_xt_dma_2d)
+  bool xt_dma_hr = false;         // ... its half-real form at nx = 8192 (C4)
   bool t1_xt64 = false;           // fp64 T = 1 windows: k_precond_x_t1_2d<..., double> (shares PDHG_T1_XT)
   bool f64_xt = false;            // fp64 nx = 4096: in-place line + register carries (k_precond_xt_f64_2d)
   int xt64_var = 0;               // nx = 2048 shape of it (threads, b' in registers or LDS)
@@ -357,6 +358,10 @@ struct Impl : ImplBase {
       if (half_real && sizeof(R) == 4) {
         fast_xt = true;
         ws_xt = true;
+        // the LDS-DMA staged x transform on half-real blocks (k_precond_xt_dma_2d<4096, true>) for windows of >= 4
+        // rows: c4w50 x transform 28.4 ms with the warp-specialised kernel (round 4, 1.9 TB/s)
+        xt_dma_hr = T >= 4;
+        if (const char* e = getenv("PDHG_XT_DMA_HR")) xt_dma_hr = atoi(e) != 0;   // A/B: 0 = warp-specialised
         lds_fast_xt = (size_t)(2 * (4096 + 4096 / 16) + 816 + 4096) * sizeof(C);   // + split twiddles
       } else if (sizeof(R) == 4 && plx.pow2 && nxg * (B / 2) == 4096 && nxg >= 512 && pb.bc_x == 0) {
         fast_xt = true;
@@ -1081,6 +1086,8 @@ struct Impl : ImplBase {
             case 512: rc = gob(k_precond_xt_batch_2d<512, 8>); break;
             default: rc = fail(PDHG_ERR_UNSUPPORTED, "no batched x kernel for nx=%d", p.nx);
           }
+        } else if (half_real && xt_dma_hr) {   // static LDS (kernels_xt_dma.hpp, HR)
+          hipLaunchKernelGGL((k_precond_xt_dma_2d<4096, true>), g, dim3(1024), 0, stream, p, twx);
         } else if (ws_xt) {
           switch (p.nx) {
             case 8192: rc = go(k_precond_xt_ws_2d<4096, 1, true>); break;
@@ -2400,7 +2407,9 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
     else if (k == "fast_dual") *value = im.fast_dual ? im.dual_rx : -1;
     else if (k == "dual_ypl") *value = im.fast_dual && im.dual_rx ? im.dual_ypl : 0;
     else if (k == "fast_xt")
-      *value = im.fast_xt ? (im.batch_xt && !im.half_real ? (im.xt_dma && im.pb.nx == 4096 ? 4 : 3) : im.ws_xt ? 2 : 1) : 0;
+      *value = im.fast_xt ? (im.half_real && im.xt_dma_hr ? 5 : im.batch_xt && !im.half_real
+                                                                    ? (im.xt_dma && im.pb.nx == 4096 ? 4 : 3)
+                                                                    : im.ws_xt ? 2 : 1) : 0;
     else if (k == "half_real") *value = im.half_real ? 1 : 0;
     else if (k == "fourstep") *value = im.fourstep ? 1 : 0;
     else if (k == "glb_line") *value = im.glb_line ? 1 : 0;

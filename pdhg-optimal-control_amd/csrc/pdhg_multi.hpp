@@ -42,6 +42,11 @@ __global__ void k_multi_fold(SumPtrs in, int n, double* __restrict__ out) {
   for (int q = 0; q < n; ++q) t += in.p[q][s];
   out[s] = t;
 }
+// same-device plane copy as a kernel (PDHG_MULTI_KCOPY=1; diagnostic against the runtime's D2D copy engine)
+__global__ void k_multi_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n16) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
 __global__ void k_multi_sum(const double* __restrict__ in, int n, double* __restrict__ out) {
   const int s = threadIdx.x;   // one thread per sum, slabs in order (fixed-order, deterministic)
   if (s >= pdhg::kNumSums) return;
@@ -81,7 +86,15 @@ struct pdhg_multi {
   double* gather = nullptr;   // slab 0's device: [P][16] sums, then the folded [16] (no peer access)
   hipEvent_t folded = nullptr;
   bool peer_fold = false;     // every pair of devices has peer access: per-device folds of the contributions
+  bool kcopy = false;         // same-device plane copies as a kernel (PDHG_MULTI_KCOPY=1)
+  int sync_mask = 0;          // diagnostic: full barrier at these step() marks (PDHG_MULTI_SYNC, bit i = mark i)
+  bool one_stream = false;    // diagnostic: planes received on the main stream (PDHG_MULTI_ONESTREAM=1)
+  // step fence (diagnostic, PDHG_MULTI_STEP_FENCE=1): every stream of every slab starts an outer iteration only
+  // after every slab's main stream finished the previous one (events, no host sync)
+  bool step_fence = false;
+  std::vector<hipEvent_t> step_end;   // per slab, recorded on its main stream at the end of step()
   unsigned round = 0;         // allreduces so far (peer fold: which contribution buffer)
+  bool stepped = false;       // step_end holds a recorded event
   std::vector<void*> allocs;  // (device, pointer) freed at destroy
   std::vector<int> alloc_dev;
   std::vector<hipEvent_t> all_events;   // (created on the device of the slab that records them)
@@ -125,7 +138,12 @@ struct pdhg_multi {
   // copy on stream s_ of slab rd (the receiver)
   int copy(int rd, hipStream_t s_, void* dst, int rs, const void* src, size_t bytes) {
     if (on(rd)) return fail(PDHG_ERR_HIP, "hipSetDevice");
-    if (dev[rd] == dev[rs]) HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s_));
+    if (dev[rd] == dev[rs] && kcopy && bytes % 16 == 0 && ((uintptr_t)dst | (uintptr_t)src) % 16 == 0) {
+      const size_t n16 = bytes / 16;
+      hipLaunchKernelGGL(pdhg::k_multi_copy, dim3((unsigned)std::min<size_t>((n16 + 255) / 256, 4096)), dim3(256), 0, s_,
+                         static_cast<const uint4*>(src), static_cast<uint4*>(dst), n16);
+      HIP_TRY(hipGetLastError());
+    } else if (dev[rd] == dev[rs]) HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s_));
     else HIP_TRY(hipMemcpyPeerAsync(dst, dev[rd], src, dev[rs], bytes, s_));
     return PDHG_OK;
   }
@@ -139,6 +157,10 @@ struct pdhg_multi {
     return PDHG_OK;
   }
   int mark(int i) {
+    if (sync_mask & (1 << i)) {   // diagnostic (PDHG_MULTI_SYNC): drain every stream at this phase boundary
+      int rc = full_barrier();
+      if (rc) return rc;
+    }
     if (!prof) return PDHG_OK;
     if (i == 0) {
       if (marks_used == marks.size()) {
@@ -201,6 +223,10 @@ struct pdhg_multi {
     const int T = prob.T;
     if (P < 1 || P > T) return fail(PDHG_ERR_ARG, "need 1 <= ndev <= T (ndev %d, T %d)", P, T);
     if (const char* e = getenv("PDHG_MULTI_PARTS")) parts = std::max(1, atoi(e));   // tuning override
+    if (const char* e = getenv("PDHG_MULTI_KCOPY")) kcopy = atoi(e) != 0;            // diagnostic
+    if (const char* e = getenv("PDHG_MULTI_SYNC")) sync_mask = (int)strtol(e, nullptr, 0);   // diagnostic
+    if (const char* e = getenv("PDHG_MULTI_ONESTREAM")) one_stream = atoi(e) != 0;          // diagnostic
+    if (const char* e = getenv("PDHG_MULTI_STEP_FENCE")) step_fence = atoi(e) != 0;
     const int base = T / P, extra = T % P;
     for (int q = 0, j = 0; q < P; ++q) {   // pdhg_amd.slab.slab_bounds
       const int n = base + (q < extra ? 1 : 0);
@@ -238,7 +264,8 @@ struct pdhg_multi {
       if ((rc = pdhg_create_slab(&q, j0[r], T, dev[r], &s[r]))) return rc;
       if (on(r)) return fail(PDHG_ERR_HIP, "hipSetDevice");
       HIP_TRY(hipStreamCreateWithFlags(&st[r], hipStreamNonBlocking));
-      HIP_TRY(hipStreamCreateWithFlags(&ss[r], hipStreamNonBlocking));
+      if (one_stream) ss[r] = st[r];   // diagnostic (PDHG_MULTI_ONESTREAM=1): receives on the main stream
+      else HIP_TRY(hipStreamCreateWithFlags(&ss[r], hipStreamNonBlocking));
       if ((rc = pdhg_set_stream(s[r], st[r]))) return rc;
       Buf& x = b[r];
       for (hipEvent_t* e : {&x.rho, &x.rho_in, &x.longp, &x.long_in, &x.pb, &x.pb_in, &x.sum})
@@ -249,6 +276,9 @@ struct pdhg_multi {
         if ((rc = event(r, &x.ds[q])) || (rc = event(r, &x.carry_in[q]))) return rc;
     }
     if ((rc = event(0, &folded))) return rc;
+    step_end.assign(P, nullptr);
+    for (int r = 0; r < P; ++r)
+      if ((rc = event(r, &step_end[r]))) return rc;
     unsigned long long a = 0, c = 0;
     if ((rc = pdhg_slab_plane_size(s[0], &a, &c))) return rc;
     sp = a;
@@ -300,7 +330,7 @@ struct pdhg_multi {
     }
     for (int r = 0; r < P; ++r) {
       if (r < (int)st.size() && st[r]) { hipSetDevice(dev[r]); hipStreamDestroy(st[r]); }
-      if (r < (int)ss.size() && ss[r]) { hipSetDevice(dev[r]); hipStreamDestroy(ss[r]); }
+      if (r < (int)ss.size() && ss[r] && ss[r] != st[r]) { hipSetDevice(dev[r]); hipStreamDestroy(ss[r]); }
     }
     magic = 0;
   }
@@ -309,6 +339,13 @@ struct pdhg_multi {
   int step(double tau, double sigma, double eps, int k) {
     int rc;
     const size_t pbytes = sp * es;
+    if (step_fence && stepped) {   // the previous step's end on every slab's main stream, for every stream
+      for (int r = 0; r < P; ++r)
+        for (int q = 0; q < P; ++q) {
+          if (q != r && (rc = wait(r, st[r], step_end[q]))) return rc;
+          if (ss[r] != st[r] && (rc = wait(r, ss[r], step_end[q]))) return rc;
+        }
+    }
     if ((rc = mark(0))) return rc;
     // rho halo (row 0 of slab r+1 -> slab r) on the receiver's side stream || the residual rows without it
     for (int r = 0; r < P; ++r)
@@ -399,6 +436,9 @@ struct pdhg_multi {
     if (k > 1 && (rc = allreduce())) return rc;
     for (int r = 0; r < P; ++r)
       if ((rc = pdhg_slab_outer_finalize(s[r], eps, k, b[r].sums))) return rc;
+    for (int r = 0; r < P; ++r)
+      if ((rc = rec(step_end[r], r, st[r]))) return rc;
+    stepped = true;
     return mark(6);
   }
 

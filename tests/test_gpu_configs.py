@@ -70,7 +70,9 @@ CASES = {
     "c2_x2048": ({"PDHG_FUSE_RES": "1", "PDHG_XT_BATCH": "0"}, {"fast_xt": 1, "fused_residual": 1, "rows_rw": 8}),
     "c2_rows_ny2048": ({"PDHG_FUSE_RES": "1"}, {"fused_residual": 1, "rows_rw": 8, "res_threads": 512,
                                                 "upd_threads": 512}),
-    "c4_halfreal_x8192": ({"PDHG_FUSE_RES": "0"}, {"fast_xt": 2, "half_real": 1, "fused_residual": 0}),
+    "c4_halfreal_x8192": ({"PDHG_FUSE_RES": "0"}, {"fast_xt": 5, "half_real": 1, "fused_residual": 0}),
+    # the warp-specialised half-real x transform (the default before round 5; PDHG_XT_DMA_HR=0)
+    "c4_halfreal_x8192@ws": ({"PDHG_FUSE_RES": "0", "PDHG_XT_DMA_HR": "0"}, {"fast_xt": 2, "half_real": 1}),
     "c4_rows_ny8192": ({"PDHG_FUSE_RES": "0"}, {"rows_rw": 4, "fused_residual": 0, "res_threads": 1024,
                                                 "upd_threads": 1024}),
     # the fused residual at ny = 8192: 4-row half-tile tasks of the 8-row sweep (k_res_fwdy_fused_2d<.., 8192, 4, 512>)
@@ -191,7 +193,8 @@ ONE_STEP = {
     "ws_fr_4096x256": (2, 4096, 256, 4, {"PDHG_XT_BATCH": "0", "PDHG_XT_WS": "1", "PDHG_FUSE_RES": "1"},
                        {"fast_xt": 2, "fused_residual": 1}),
     "rows_ny4096_fr": (2, 64, 4096, 4, {"PDHG_FUSE_RES": "1"}, {"fused_residual": 1, "res_threads": 512}),
-    "halfreal_x8192": (2, 8192, 16, 4, {}, {"fast_xt": 2, "half_real": 1}),
+    "halfreal_x8192": (2, 8192, 16, 4, {}, {"fast_xt": 5, "half_real": 1}),
+    "halfreal_x8192_ws": (2, 8192, 16, 4, {"PDHG_XT_DMA_HR": "0"}, {"fast_xt": 2, "half_real": 1}),
     "rows_ny8192": (2, 64, 8192, 4, {}, {"rows_rw": 4}),
     "batch_fr_4096x256": (2, 4096, 256, 8, {"PDHG_XT_BATCH": "1", "PDHG_XT_DMA": "0", "PDHG_FUSE_RES": "1"},
                           {"fast_xt": 3, "fused_residual": 1}),
@@ -220,6 +223,27 @@ def test_batched_x_transform_matches_ws(native, monkeypatch, nx, T):
         finally:
             ctx.close()
     assert rel(out[1][0], out[0][0]) < 1e-6 and rel(out[1][1], out[0][1]) < 1e-6
+
+
+@pytest.mark.parametrize("T", [50, 9, 5, 4])
+def test_dma_halfreal_matches_ws(native, monkeypatch, T):
+    """The LDS-DMA half-real x transform (k_precond_xt_dma_2d<4096, true>, C4's nx = 8192) against the
+    warp-specialised half-real kernel on the same state: the same modes per item (k, k + N) and Thomas algebra,
+    lam(k + N) formed on the device as -4/dx^2 - lam(k) (an ulp from the host's value); 3 iterations, fp32 <= 1e-6."""
+    P = make_problem(2, 2, 8192, 64, T, 0.0, seeded=True)
+    out = []
+    for dma in ("0", "1"):
+        monkeypatch.setenv("PDHG_XT_DMA_HR", dma)
+        ctx = device_ctx(P, "fp32")
+        try:
+            assert ctx.path_info("fast_xt") == (5 if dma == "1" else 2) and ctx.path_info("half_real") == 1
+            ctx.set_state(*_f32_state(P))
+            ctx.iterate(3, TAU, SIGMA, -1.0, 1)
+            out.append(ctx.get_state())
+        finally:
+            ctx.close()
+    assert rel(out[1][0], out[0][0]) < 1e-6 and rel(out[1][1], out[0][1]) < 1e-6
+    assert rel(np.stack(out[1][2]), np.stack(out[0][2])) < 1e-5
 
 
 @pytest.mark.parametrize("T", [37, 8, 5, 4])

@@ -22,7 +22,8 @@ CASES = [
     (1, 4096, 256, 4, 3, 2),
     (2, 4096, 256, 50, 2, 1),    # 25-row slabs (C3's slab length on 8 GPUs): LDS-DMA x transform
     (2, 4096, 256, 11, 2, 1),    # 6 + 5 rows: LDS-DMA x transform with partial last batches
-    (2, 8192, 256, 5, 2, 1),    # half-real x blocks (C4's nx)
+    (2, 8192, 256, 5, 2, 1),    # half-real x blocks (C4's nx): warp-specialised (slabs < 4 rows)
+    (2, 8192, 256, 16, 2, 1),   # half-real LDS-DMA x transform's slab phases (8-row slabs)
     (1, 512, 256, 3, 3, 1),     # one-row slabs: the halo row is the whole slab
     (2, 512, 256, 19, 2, 1),    # residual tiles of 8 rows + untiled remainder rows
     (2, 512, 256, 40, 4, 1),    # 10-row slabs: short-range modes take the neighbour-only carries
