@@ -444,7 +444,7 @@ def main():
         import torch
         from pdhg_amd.xslab import XSlabContext
         ctx = XSlabContext(rank, world, egno, nx, ny, T, 2.0 / nx, 2.0 / ny, dt, xs, ys, epsl=epsl,
-                           rho_alp_iters=k, device=torch.cuda.current_device())
+                           precision=args.precision, rho_alp_iters=k, device=torch.cuda.current_device())
     elif world > 1:
         from pdhg_amd.slab import DistComm, SlabContext, SlabRunner
         ctx = SlabContext(rank, world, T, egno, nx, ny, 2.0 / nx, 2.0 / ny, dt, xs, ys, epsl=epsl,

@@ -290,7 +290,7 @@ struct Impl : ImplBase {
       if (B > nyp) B = nyp;
       // fp64 nx = 512 / 1024 with T > 1: one column pair per block (B = 2) for the fp64 x kernel below (the generic
       // kernel would take B = 8 / 4 with its carries in global memory); T = 1 keeps the one-row kernel's B
-      const bool f64_small = sizeof(R) == 8 && pb.bc_x == 0 && !xslab && T > 1 && (nxg == 1024 || nxg == 512) &&
+      const bool f64_small = sizeof(R) == 8 && pb.bc_x == 0 && T > 1 && (nxg == 1024 || nxg == 512) &&
                              ny % 2 == 0 && [] { const char* e = getenv("PDHG_XT64"); return !e || atoi(e) != 0; }();
       if (f64_small) B = 2;
       // fp32 nx = 8192 (C4): one real column per block, packed into a 4096-point FFT (half_real)
@@ -302,12 +302,12 @@ struct Impl : ImplBase {
       // (t-slab phases too: kernels_xt_f64.hpp)
       // fp64 nx = 2048 (C2's grid): the same kernel with b' in registers (BPR) instead of the generic runtime-radix
       // kernel's global carries (10.97 ms at C2, 0.15 of the HBM roofline, round 4)
-      f64_xt = sizeof(R) == 8 && pb.bc_x == 0 && !xslab &&
+      f64_xt = sizeof(R) == 8 && pb.bc_x == 0 &&
                (((nxg == 4096 || nxg == 2048) && B == 2) || (nxg == 8192 && half_real) || f64_small);
       if (const char* e = getenv("PDHG_XT64")) f64_xt = f64_xt && atoi(e) != 0;   // A/B: 0 = generic kernel
       if (const char* e = getenv("PDHG_XT64_VAR")) xt64_var = atoi(e);              // A/B: nx = 2048 shapes
       // fp64 one-row windows at a power-of-two nx: the carry-free transform needs only the padded lines
-      t1_xt64 = sizeof(R) == 8 && T == 1 && pb.bc_x == 0 && !half_real && !xslab && !slab && plx.pow2 &&
+      t1_xt64 = sizeof(R) == 8 && T == 1 && pb.bc_x == 0 && !half_real && !slab && plx.pow2 &&
                 nxg >= 512 && nxg <= 4096 && nxg * (B / 2) == (nxg == 4096 ? 4096 : 2048);
       if (!half_real && !f64_xt && (size_t)nxg * B > cap)
         return fail(PDHG_ERR_UNSUPPORTED, "nx=%d too large for the x-transform slab (max %zu in this precision)", nxg,
@@ -386,7 +386,7 @@ struct Impl : ImplBase {
       // per-point kernel, which re-reads every phi_bar neighbour (fp64 C3: 248 GB fetched for 161 GB of reads).
       // Measured at fp64 C3 (same box, profiles/r04_ab_dual64_*.json): 52.7 vs 59.3 ms per dual, 6.61 vs 6.44
       // it/s.  PDHG_DUAL64=0 keeps the generic kernel.  The LDS-row and fused variants are fp32.
-      const bool dual64_ok = sizeof(R) == 8 && ny % 256 == 0 && !xslab;
+      const bool dual64_ok = sizeof(R) == 8 && ny % 256 == 0;
       bool dual64 = dual64_ok;
       if (const char* e = getenv("PDHG_DUAL64")) dual64 = dual64_ok && atoi(e) != 0;
       if ((sizeof(R) == 4 || dual64) && ny % 256 == 0) {
@@ -437,7 +437,7 @@ struct Impl : ImplBase {
       // fp64 residual: the fast row kernel on 4-row groups (2 complex lines of 4096 doubles = 136 KiB of LDS),
       // rows read once per group over the sliding 3-row window, instead of the generic row-pair kernel's
       // per-point neighbour re-reads (fp64 C3: 204 GB moved against 80.5 GB algorithmic)
-      if (sizeof(R) == 8 && ply.pow2 && (ny == 2048 || ny == 4096) && nx % 4 == 0 && !xslab) {
+      if (sizeof(R) == 8 && ply.pow2 && (ny == 2048 || ny == 4096) && nx % 4 == 0) {
         res64 = true;
         if (const char* e = getenv("PDHG_RES64")) res64 = atoi(e) != 0;   // tuning override
         if (res64) {
@@ -531,9 +531,11 @@ struct Impl : ImplBase {
     p.xl0 = xslab ? 8 : 0;
     p.xl1 = xslab ? 8 + xs_nloc : nx;
     if (xslab) {
-      if (!(is2d && sizeof(R) == 4 && fast_rows && fast_dual && (pb.bc_x == 0 || pb.bc_x == 1) && pb.bc_y == 0))
-        return fail(PDHG_ERR_UNSUPPORTED, "x-slab decomposition needs ndim 2, fp32, bc (0,0) or (1,0) and a "
-                                          "power-of-two ny in [256, 8192] (fast row and dual kernels)");
+      // the row kernels that skip the ghost / padding rows: fp32 fast rows (ny in [256, 8192]), fp64 4-row kernels
+      if (!(is2d && (sizeof(R) == 4 ? fast_rows : res64) && fast_dual && (pb.bc_x == 0 || pb.bc_x == 1) &&
+            pb.bc_y == 0))
+        return fail(PDHG_ERR_UNSUPPORTED, "x-slab decomposition needs ndim 2, bc (0,0) or (1,0) and a power-of-two ny "
+                                          "in [256, 8192] (fp32) or ny = 2048 / 4096 (fp64) (fast row and dual kernels)");
       if (p.nb % xs_P) return fail(PDHG_ERR_UNSUPPORTED, "%d column blocks do not split over %d ranks", p.nb, xs_P);
       xs_nbs = p.nb / xs_P;
     }
@@ -2588,7 +2590,6 @@ int pdhg_create_xslab(const pdhg_problem* prob, int rank, int nranks, int device
   if (!prob || !out) return fail(PDHG_ERR_ARG, "null argument");
   *out = nullptr;
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail(PDHG_ERR_ARG, "rank %d of %d", rank, nranks);
-  if (prob->precision != 4) return fail(PDHG_ERR_UNSUPPORTED, "x-slab decomposition is fp32 only");
   if (prob->ndim != 2) return fail(PDHG_ERR_UNSUPPORTED, "x-slab decomposition is 2-D only");
   // bc (0,0), or egno 3's (1,0): Neumann x edges -- the first / last slab's outer ghost row replicates its own edge
   // row (nb_index bc 1), the transposed x lines take the DCT of the generic x kernel
@@ -2605,26 +2606,34 @@ int pdhg_create_xslab(const pdhg_problem* prob, int rank, int nranks, int device
   pdhg_destroy(probe);
   const int nloc = prob->nx / nranks, nxl = nloc + 16, x0 = rank * nloc;
   auto box = std::make_unique<CtxBox>();
-  box->precision = 4;
-  auto im = std::make_unique<Impl<float>>();
-  im->xslab = true;
-  im->xs_rank = rank;
-  im->xs_P = nranks;
-  im->xs_nxg = prob->nx;
-  im->xs_nloc = nloc;
-  im->xs_x0 = x0;
-  im->xs_local.resize(nxl);
-  for (int i = 0; i < nxl; ++i) {   // local row i = global row x0 - 8 + i (periodic; clamped at Neumann edges)
-    const int gi = x0 - 8 + i;
-    const int g = prob->bc_x == 1 ? std::min(std::max(gi, 0), prob->nx - 1) : ((gi % prob->nx) + prob->nx) % prob->nx;
-    im->xs_local[i] = prob->xs[g];
-  }
-  im->pb = *prob;
-  im->pb.nx = nxl;
-  im->pb.xs = im->xs_local.data();
-  im->device = device;
-  rc = im->setup();
-  box->impl = std::move(im);
+  box->precision = prob->precision;
+  // fp32, or fp64 = the reference's arithmetic (jaxsrc/update_fns_in_pdhg.py:10): the x-slab kernels, the fp64 row
+  // kernels (ny = 2048 / 4096) and the fp64 duals honour the live-row bounds; the column blocks go through the
+  // generic x kernel
+  auto build = [&](auto tag) {
+    using Rt = decltype(tag);
+    auto im = std::make_unique<Impl<Rt>>();
+    im->xslab = true;
+    im->xs_rank = rank;
+    im->xs_P = nranks;
+    im->xs_nxg = prob->nx;
+    im->xs_nloc = nloc;
+    im->xs_x0 = x0;
+    im->xs_local.resize(nxl);
+    for (int i = 0; i < nxl; ++i) {   // local row i = global row x0 - 8 + i (periodic; clamped at Neumann edges)
+      const int gi = x0 - 8 + i;
+      const int g = prob->bc_x == 1 ? std::min(std::max(gi, 0), prob->nx - 1) : ((gi % prob->nx) + prob->nx) % prob->nx;
+      im->xs_local[i] = prob->xs[g];
+    }
+    im->pb = *prob;
+    im->pb.nx = nxl;
+    im->pb.xs = im->xs_local.data();
+    im->device = device;
+    const int r = im->setup();
+    box->impl = std::move(im);
+    return r;
+  };
+  rc = prob->precision == 8 ? build(0.0) : build(0.f);
   if (rc) return rc;
   *out = reinterpret_cast<pdhg_ctx*>(box.release());
   return PDHG_OK;

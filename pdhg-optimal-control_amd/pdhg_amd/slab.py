@@ -52,6 +52,12 @@ class PhaseOps:
     _dual_finalize / _outer / _outer_finalize / _status, pdhg_set_stream).  Tensor arguments are device
     tensors (float64[16] sums)."""
 
+    @property
+    def plane_dtype(self):
+        """Element type of the device planes / halos / wires exchanged between slabs (the context's precision)."""
+        import torch
+        return torch.float64 if self.precision in ("fp64", 8) else torch.float32
+
     def set_stream(self, stream_handle):
         N.check(self._lib.pdhg_set_stream(self._h, ctypes.c_void_p(stream_handle)))
 
@@ -97,11 +103,6 @@ class SlabContext(PhaseOps, PDHGContext):
         h = ctypes.c_void_p()
         N.check(self._lib.pdhg_create_slab(ctypes.byref(prob), self.j0, self.T_total, device, ctypes.byref(h)))
         return h
-
-    @property
-    def plane_dtype(self):
-        import torch
-        return torch.float64 if self.precision in ("fp64", 8) else torch.float32
 
     @property
     def last(self):

@@ -30,8 +30,9 @@ ROWS_OUT, COLS_IN, COLS_OUT, ROWS_IN = 0, 1, 2, 3   # pdhg_xslab_wire stages
 
 
 class XSlabContext(PhaseOps, PDHGContext):
-    """Slab `rank` of `nranks` of the global nx rows (fp32, 2-D, bc (0,0) or egno 3's (1,0)).  nx / xs describe the
-    global grid."""
+    """Slab `rank` of `nranks` of the global nx rows (2-D, bc (0,0) or egno 3's (1,0); precision "fp32", or "fp64" =
+    the reference's arithmetic, jaxsrc/update_fns_in_pdhg.py:10, at ny = 2048 / 4096).  nx / xs describe the global
+    grid.  Halo and wire buffers are in the slab's precision (plane_dtype)."""
 
     def __init__(self, rank, nranks, egno, nx, ny, T, dx, dy, dt, xs, ys, device=0, **kw):
         self.rank, self.nranks, self.nx_global = int(rank), int(nranks), int(nx)
@@ -101,7 +102,9 @@ class XSlabRunner:
         self.slabs, self.comm = list(slabs), comm
         dev = torch.device("cuda", torch.cuda.current_device())
         handle = torch.cuda.current_stream().cuda_stream
-        f32 = torch.float32
+        f32 = self.slabs[0].plane_dtype   # halos and wires in the slabs' precision; sums fp64
+        if any(s.plane_dtype != f32 for s in self.slabs):
+            raise ValueError("slabs of one runner must share a precision")
         self.b = []
         for s in self.slabs:
             s.set_stream(handle)

@@ -95,8 +95,8 @@ def test_null_context_calls(lib):
 
 
 def test_xslab_create_validates_before_device(lib):
-    """pdhg_create_xslab checks the decomposition (rank range, precision, ndim, bc, row split) before it
-    touches a device."""
+    """pdhg_create_xslab checks the decomposition (rank range, ndim, bc, row split) and pdhg_create's problem
+    checks (here an unknown precision; fp32 and fp64 are both x-slab precisions) before it touches a device."""
     L = lib.load()
     xs = np.linspace(0, 2, 64, endpoint=False)
     ys = np.linspace(0, 2, 256, endpoint=False)
@@ -112,7 +112,7 @@ def test_xslab_create_validates_before_device(lib):
 
     h = ctypes.c_void_p()
     for (rank, nranks, kw, code) in [(2, 2, {}, lib.PDHG_ERR_ARG), (0, 0, {}, lib.PDHG_ERR_ARG),
-                                     (0, 2, {"precision": 8}, lib.PDHG_ERR_UNSUPPORTED),
+                                     (0, 2, {"precision": 2}, lib.PDHG_ERR_ARG),
                                      (0, 2, {"ndim": 1, "ny": 1}, lib.PDHG_ERR_UNSUPPORTED),
                                      (0, 2, {"bc_x": 2}, lib.PDHG_ERR_UNSUPPORTED),   # Dirichlet x edges
                                      (0, 3, {}, lib.PDHG_ERR_UNSUPPORTED),      # 64 rows / 3
