@@ -264,14 +264,16 @@ int pdhg_slab_update(pdhg_ctx* ctx, double tau, double* sums);            /* inv
  * halo_out: [2][nq][T][ny] (nq = 1 + live controls for which 0 = rho/alp of the current set, 1 for
  * which 1 = phi_bar rows 1..T); side 0 = the first live row (to the left neighbour), side 1 = the last.
  * halo_in takes the left neighbour's and the right neighbour's halo_out buffers (periodic ring).
- * wire: [nranks][T][nb/nranks][nloc][B] floats (pdhg_xslab_sizes), chunk q = for / from rank q; stage 0
+ * wire: [nranks][T][nb/nranks][nloc][B] elements (pdhg_xslab_sizes), chunk q = for / from rank q; stage 0
  * packs the y-transformed rows, 1 unpacks the received rows into whole x lines, 2 packs the
- * preconditioned lines, 3 unpacks them back into rows.  fp32, ndim 2, bc (0,0) or egno 3's (1,0) (the outer slabs' outer ghost rows replicate their edge row), power-of-two ny in
- * [256, 8192], (ny/B) % nranks == 0. */
+ * preconditioned lines, 3 unpacks them back into rows.  Halo and wire elements are in the context's precision
+ * (float for p->precision 4, double for 8 = the reference's arithmetic).  ndim 2, bc (0,0) or egno 3's (1,0) (the
+ * outer slabs' outer ghost rows replicate their edge row), (ny/B) % nranks == 0; fp32: a power-of-two ny in
+ * [256, 8192]; fp64: ny = 2048 or 4096 (the fp64 4-row row kernels) and nx != 8192. */
 int pdhg_create_xslab(const pdhg_problem* p, int rank, int nranks, int device, pdhg_ctx** out);
 int pdhg_xslab_layout(pdhg_ctx* ctx, int* x0, int* nloc, int* nx_local, int* xl0);
 int pdhg_xslab_sizes(pdhg_ctx* ctx, unsigned long long* wire, unsigned long long* halo_state,
-                     unsigned long long* halo_phibar);                     /* float counts */
+                     unsigned long long* halo_phibar);                     /* element counts */
 int pdhg_xslab_halo_out(pdhg_ctx* ctx, int which, void* dst);
 int pdhg_xslab_halo_in(pdhg_ctx* ctx, int which, const void* from_left, const void* from_right);
 int pdhg_xslab_residual(pdhg_ctx* ctx);                                    /* residual + y-DHT, local rows */
