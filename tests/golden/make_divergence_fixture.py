@@ -38,6 +38,12 @@ transform) -> divergence_c3_plane_T4_points_npfft.npz.  It is the like-for-like 
 on another FFT library -- what the reference itself (XLA's FFT) could differ from the oracle by -- without the
 one-ulp perturbation of every input entry that "points_ulp" applies.
 
+Device-t-solve variant (argument "points_devthomas", round 5): the same float64 run with the oracle's Thomas solve
+(utils_precond.py:10-40, complex Thomas scan) replaced by the device's algebra for the same tridiagonal systems
+(kernels_xt_f64.hpp: cancellation-free pivot recurrence s = dd + h, g = 1/(1+s), h = s g forward, closed-form pivots
+g_k = e^-th E_{k+1}/E_{k+2} backward) -> divergence_c3_plane_T4_points_devthomas.npz: the spread of the reference
+algorithm under another, equally exact float64 formulation of one of its steps.
+
 Pointwise variant (argument "points"): the float64 oracle's phi' and rho' at NPTS fixed sample points of the plane
 (rows 1..T of phi', every row of rho'; indices from np.random.default_rng(20250117)) after each of the first
 max_iters iterations -> divergence_c3_plane_T{T}_points.npz.  tests/test_gpu_divergence.py compares the fp64
@@ -141,7 +147,35 @@ if __name__ == "__main__":
     T = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     max_iters = int(sys.argv[2]) if len(sys.argv) > 2 else 24
     f32 = len(sys.argv) > 3 and sys.argv[3] == "f32"   # the float32 oracle (until its first NaN)
-    points = len(sys.argv) > 3 and sys.argv[3] in ("points", "points_ulp", "points_npfft")
+    points = len(sys.argv) > 3 and sys.argv[3] in ("points", "points_ulp", "points_npfft", "points_devthomas")
+    devth = len(sys.argv) > 3 and sys.argv[3] == "points_devthomas"
+    if devth:
+        def dev_thomas(dl, d, du, b):
+            """M x = b with M = ae tridiag(-1, dd + 2, -1), last diagonal dd + 1 (H1_precond_2d's systems), in the
+            device's algebra (kernels_xt_f64.hpp)."""
+            ae = -float(np.real(dl[1]))
+            dd = (np.real(d[0]) - 2.0 * ae) / ae
+            T = b.shape[0]
+            h = np.ones_like(dd)
+            bp = np.zeros_like(b[0])
+            bps = []
+            for k in range(T - 1):
+                s_ = dd + h
+                g_ = 1.0 / (1.0 + s_)
+                h = s_ * g_
+                bp = (b[k] / ae + bp) * g_
+                bps.append(bp)
+            x = (b[T - 1] / ae + bp) / (dd + h)
+            out = [None] * T
+            out[T - 1] = x
+            dl_ = 0.5 * dd
+            th = np.maximum(np.log1p(dl_ + np.sqrt(dl_ * (dl_ + 2.0))), 1e-300)
+            for k in range(T - 2, -1, -1):
+                g_ = np.exp(-th) * np.expm1(-2.0 * th * (k + 1)) / np.expm1(-2.0 * th * (k + 2))
+                x = bps[k] + g_ * x
+                out[k] = x
+            return np.stack(out)
+        O.tridiagonal_solve = dev_thomas
     ulp = len(sys.argv) > 3 and sys.argv[3] == "points_ulp"
     npfft = len(sys.argv) > 3 and sys.argv[3] == "points_npfft"
     if npfft:   # the oracle's FFTs through numpy.fft (periodic bc: fft2 / ifft2 only)
@@ -156,7 +190,8 @@ if __name__ == "__main__":
     nx = ny = 4096
     S = setup(nx, ny, T, 1.0 / 200, 0.1, np.float32 if f32 else np.float64)
     out = os.path.join(HERE, "divergence_c3_plane_T{}{}.npz".format(
-        T, "_f32" if f32 else "_points_ulp" if ulp else "_points_npfft" if npfft else "_points" if points else ""))
+        T, "_f32" if f32 else "_points_ulp" if ulp else "_points_npfft" if npfft else "_points_devthomas" if devth
+        else "_points" if points else ""))
     if points:
         S.update(points=sample_points(T, nx, ny), phi_pts=[], rho_pts=[])
     if ulp:
