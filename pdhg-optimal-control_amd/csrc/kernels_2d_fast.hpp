@@ -341,6 +341,9 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<R> p, const cplx<R>*
 // fp64 (R = double): the sweep's strips are 128 columns wide (k_dual_lds_2d<.., double, YPL = 2>) and 4 rows of
 // complex double fill the LDS, so a task is half a sweep tile (RW = 4, NH = 2): the first half adds row x0's
 // p.ex term, the second row x0+RW-1's.  fp32 at ny = 8192 (C4) likewise: 4 rows of 8192 floats fill the LDS.
+// fp64 at ny = 8192 (C4's grid in the reference's precision): one line of 8192 complex doubles (136 KiB) per task,
+// i.e. a quarter of a sweep tile (RW = 2, NH = 4; the first quarter adds row x0's p.ex term, the last row x0+7's);
+// with C4's half-real spectrum (B = 1) a chunk is the two rows' values at one ky (one 16-B store).
 // grid: G <= T * nx/RW; block NT (N/4 % NT == 0); LDS RW/2 * (N + N/16) * sizeof(C) (+ 2 * RW * N/YW reals).
 template <int EGNO, int N, int RW, int NT, typename R = float>
 __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<R> p, const cplx<R>* __restrict__ twy) {
@@ -353,8 +356,10 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<R> p, const cplx<R>
   constexpr int GPT = (N / 4) / NT;
   constexpr int YW = sizeof(R) == 4 ? 256 : 128, NSTRIP = N / YW;
   constexpr int NEY = RW * NSTRIP * 2;   // strip-edge terms of one task
-  static_assert((RW == 8 || RW == 4) && (sizeof(R) == 4 || RW == 4) && N % YW == 0 && (N / 4) % NT == 0,
-                "fused residual tasks: 8 or 4 (fp64, fp32 ny = 8192) rows of the sweep's 8-row x YW-column tiles");
+  static_assert((RW == 8 || RW == 4 || RW == 2) && (sizeof(R) == 4 || RW <= 4) && (RW != 2 || (sizeof(R) == 8 &&
+                N == 8192)) && N % YW == 0 && (N / 4) % NT == 0,
+                "fused residual tasks: 8, 4 (fp64, fp32 ny = 8192) or 2 (fp64 ny = 8192) rows of the sweep's 8-row x "
+                "YW-column tiles");
   static_assert(NEY <= NT, "one strip-edge term per thread");
   if (p.ctrl->done) return;
   extern __shared__ __align__(16) unsigned char smem_raw[];
@@ -394,8 +399,9 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<R> p, const cplx<R>
   // (N = 8192: none -- the 8192-point transform's registers leave no room for rows held across it)
   constexpr int RSPLIT = (N > 4096) ? 0 : (NT >= 1024) ? RW / 2 : RW;
   auto load_edges = [&](int task) {
-    const int jt = task / ngx, j = p.row_base + jt, tk = task - jt * ngx, tile = tk / NH;
+    const int jt = task / ngx, j = p.row_base + jt, tk = task - jt * ngx, tile = tk / NH, sub = tk & (NH - 1);
     const R* E = p.ex + ((size_t)j * (ngx / NH) + tile) * 2 * N;
+    if (NH > 2 && sub != 0 && sub != NH - 1) return;   // inner quarters of a tile: no edge row (uniform)
 #pragma unroll
     for (int gi = 0; gi < GPT; ++gi) {
       const int y = 4 * (tid + gi * NT);
@@ -403,11 +409,18 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<R> p, const cplx<R>
         e0[gi] = ld4(E + y);
         e1[gi] = ld4(E + N + y);
       } else {
-        e0[gi] = ld4(E + ((tk & 1) ? N : 0) + y);
+        e0[gi] = ld4(E + (sub == NH - 1 ? N : 0) + y);
       }
     }
   };
-  int task = blockIdx.x, buf = 0;
+  // fp64 C4 (2-row tasks, B = 1: 16-B chunks, 8 tasks per 128-B line of the spectrum): XCD-aware task order, the
+  // G / 8 workgroups of one XCD take consecutive tasks in every round, so a line's chunks are written through one
+  // L2.  Interleaved A/B (round 5, c4w50 fp64): residual 73.2 -> 60.4 ms; at C3's 64-B chunks (2 tasks per line)
+  // the same order measured slower (fp64 15.5 -> 17.8 ms, fp32 neutral), so only the 2-row tasks take it.
+  // (PDHG_DBG 1024: round-robin order, A/B timing only)
+  constexpr bool XCDO = RW == 2;
+  int task = (XCDO && (gridDim.x & 7) == 0 && !(p.dbg & 1024)) ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  int buf = 0;
   if (task < ntask) {
     load_rows(task, 0, RW);
     load_edges(task);
@@ -440,10 +453,10 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<R> p, const cplx<R>
           f4set(v[0], e, f4(v[0], e) + f4(e0[gi], e));
           f4set(v[RW - 1], e, f4(v[RW - 1], e) + f4(e1[gi], e));
         }
-      } else if (((task - jt * ngx) & 1) == 0) {
+      } else if (((task - jt * ngx) & (NH - 1)) == 0) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) f4set(v[0], e, f4(v[0], e) + f4(e0[gi], e));
-      } else {
+      } else if (((task - jt * ngx) & (NH - 1)) == NH - 1) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) f4set(v[RW - 1], e, f4(v[RW - 1], e) + f4(e0[gi], e));
       }
@@ -475,11 +488,19 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<R> p, const cplx<R>
     if constexpr (RSPLIT < RW) load_rows(nxt, RSPLIT, RW);
     load_edges(nxt);
     R* wk = p.work + (size_t)j * nb * nx * B;
-    for (int t = tid; t < nb * CS4 && !(p.dbg & 32); t += NT) {   // PDHG_DBG 32: no unpack / stores (timing)
-      const int b = t >> lCS4, part = t & (CS4 - 1);
-      const V v = unpack_chunk4<N, LN, R>(A, b, part, B, p.lB);
-      if (p.dbg & 512) st4(wk + (size_t)x0 * N + 4 * t, v);   // PDHG_DBG 512: task-contiguous stores (timing)
-      else st4(wk + ((size_t)b * nx + x0) * B + part * 4, v);
+    if (RW * B < 4) {   // RW = 2, B = 1 (fp64 C4): chunk b = rows x0, x0+1 at ky = b, one 16-B store
+      for (int b = tid; b < nb; b += NT) {
+        R ha, hb;
+        hartley_padded<C, R>(A, N, b, ha, hb);
+        *reinterpret_cast<C*>(wk + (size_t)b * nx + x0) = cmk<C>(ha, hb);
+      }
+    } else {
+      for (int t = tid; t < nb * CS4 && !(p.dbg & 32); t += NT) {   // PDHG_DBG 32: no unpack / stores (timing)
+        const int b = t >> lCS4, part = t & (CS4 - 1);
+        const V v = unpack_chunk4<N, LN, R>(A, b, part, B, p.lB);
+        if (p.dbg & 512) st4(wk + (size_t)x0 * N + 4 * t, v);   // PDHG_DBG 512: task-contiguous stores (timing)
+        else st4(wk + ((size_t)b * nx + x0) * B + part * 4, v);
+      }
     }
     lds_sync();
   }

@@ -48,6 +48,12 @@ int fail(int code, const char* fmt, ...) {
     hipError_t e_ = (expr);                                                                     \
     if (e_ != hipSuccess) return fail(PDHG_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
   } while (0)
+// stream-ordered host -> device copy inside Impl (Impl::h2d)
+#define H2D(d, s, n)                        \
+  do {                                      \
+    const int rc_h2d_ = h2d((d), (s), (n)); \
+    if (rc_h2d_) return rc_h2d_;            \
+  } while (0)
 
 constexpr size_t kLdsBytes = 160 * 1024;
 
@@ -239,6 +245,13 @@ struct Impl : ImplBase {
     return PDHG_OK;
   }
 
+  // Host -> device copies on the context's stream (stream-ordered): the stream is non-blocking, so a copy on the
+  // legacy null stream (hipMemcpy / hipMemset) has no ordering guarantee with the kernels enqueued on it
+  int h2d(void* dst, const void* src, size_t bytes) {
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    return PDHG_OK;
+  }
   size_t plane() const { return (size_t)pb.nx * (size_t)pb.ny; }
 
   int setup() {
@@ -455,8 +468,10 @@ struct Impl : ImplBase {
       // fp64: the sweep k_dual_lds_2d<.., double, YPL = 2> (128-column strips, 211 VGPRs) and the residual in
       // half-tile tasks of 4 rows (k_res_fwdy_fused_2d<.., 4, 512, double>, the lines + twiddles fill the LDS)
       // fp32 ny = 8192 (C4's y extent): the 4-row fast kernels, so the residual runs half-tile tasks as in fp64
+      // fp64 ny = 8192 (C4): the row pairs of the generic kernels (ip_rows) for the unfused residual and the update,
+      // the fused residual on quarter-tile tasks (one line of 8192 complex doubles)
       const bool fr_rows = sizeof(R) == 4 ? (fast_rows && (RWf == 8 || (RWf == 4 && ny == 8192)))
-                                          : (res64 && (ny == 4096 || ny == 2048));
+                                          : ((res64 && (ny == 4096 || ny == 2048)) || (ip_rows && ny == 8192));
       if (fast_dual && dual_rx == 8 && fr_rows && pb.bc_x == 0 && pb.bc_y == 0 && pb.egno != 3 && !two_sets &&
           !xslab) {
         // fp32 ny = 8192: off unless asked for (c4w50 A/B, round 4: residual 31.2 -> 25.9 ms, dual 26.7 -> 31.3 ms,
@@ -636,26 +651,26 @@ struct Impl : ImplBase {
     if ((rc = alloc(&d_ay, std::max(ny, 1)))) return rc;
     if ((rc = alloc(&d_lamx, nxg))) return rc;
     if ((rc = alloc(&d_d0, nxg))) return rc;
-    HIP_TRY(hipMemcpy(d_ax, ax.data(), nx * sizeof(R), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(d_ay, ay.data(), ay.size() * sizeof(R), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(d_lamx, lamx.data(), nxg * sizeof(R), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(d_d0, d0.data(), nxg * sizeof(R), hipMemcpyHostToDevice));
+    H2D(d_ax, ax.data(), nx * sizeof(R));
+    H2D(d_ay, ay.data(), ay.size() * sizeof(R));
+    H2D(d_lamx, lamx.data(), nxg * sizeof(R));
+    H2D(d_d0, d0.data(), nxg * sizeof(R));
     const int nyp = is2d ? p.nb * p.B : 1;
     std::vector<R> lamy(nyp, (R)0);
     if (is2d)
       for (int k = 0; k < ny; ++k) lamy[k] = (R)(-2.0 * (1.0 - std::cos(2.0 * M_PI * k / ny)) / (pb.dy * pb.dy));
     if ((rc = alloc(&d_lamy, nyp))) return rc;
-    HIP_TRY(hipMemcpy(d_lamy, lamy.data(), nyp * sizeof(R), hipMemcpyHostToDevice));
+    H2D(d_lamy, lamy.data(), nyp * sizeof(R));
     {
       R* d_cx;
       if ((rc = alloc(&d_cx, nxg))) return rc;
-      HIP_TRY(hipMemcpy(d_cx, cx.data(), nxg * sizeof(R), hipMemcpyHostToDevice));
+      H2D(d_cx, cx.data(), nxg * sizeof(R));
       p.cx = d_cx;
       p.dctw = nullptr;
       if (dct_x) {
         C* d_w;
         if ((rc = alloc(&d_w, nxg))) return rc;
-        HIP_TRY(hipMemcpy(d_w, dctw.data(), nxg * sizeof(C), hipMemcpyHostToDevice));
+        H2D(d_w, dctw.data(), nxg * sizeof(C));
         p.dctw = d_w;
       }
     }
@@ -668,17 +683,17 @@ struct Impl : ImplBase {
     {
       auto t = twiddles<R>(nxg);
       if ((rc = alloc(&twx, nxg))) return rc;
-      HIP_TRY(hipMemcpy(twx, t.data(), nxg * sizeof(C), hipMemcpyHostToDevice));
+      H2D(twx, t.data(), nxg * sizeof(C));
     }
     if (fourstep) {
       auto t = twiddles<R>(256);
       if ((rc = alloc(&tw256, 256))) return rc;
-      HIP_TRY(hipMemcpy(tw256, t.data(), 256 * sizeof(C), hipMemcpyHostToDevice));
+      H2D(tw256, t.data(), 256 * sizeof(C));
     }
     if (is2d) {
       auto t = twiddles<R>(ny);
       if ((rc = alloc(&twy, ny))) return rc;
-      HIP_TRY(hipMemcpy(twy, t.data(), ny * sizeof(C), hipMemcpyHostToDevice));
+      H2D(twy, t.data(), ny * sizeof(C));
     }
     return set_lds_attrs();
   }
@@ -810,7 +825,19 @@ struct Impl : ImplBase {
           }
           return (int)PDHG_OK;
         };
-        rc = pb.ny == 4096 ? go(std::integral_constant<int, 4096>{}) : go(std::integral_constant<int, 2048>{});
+        if (pb.ny == 8192) {   // quarter-tile tasks: one padded line of 8192 complex doubles (+ the strip-edge terms)
+          const dim3 g(std::min((pb.nx / 2) * (hi - lo), n_cu));
+          const size_t lds = (size_t)Pad<8192>::LINE * sizeof(C);
+          if (pb.egno == 1) {
+            if ((rc = ensure_lds(k_res_fwdy_fused_2d<1, 8192, 2, 512, double>, lds))) return rc;
+            hipLaunchKernelGGL((k_res_fwdy_fused_2d<1, 8192, 2, 512, double>), g, dim3(512), lds, stream, p, twy);
+          } else {
+            if ((rc = ensure_lds(k_res_fwdy_fused_2d<2, 8192, 2, 512, double>, lds))) return rc;
+            hipLaunchKernelGGL((k_res_fwdy_fused_2d<2, 8192, 2, 512, double>), g, dim3(512), lds, stream, p, twy);
+          }
+        } else {
+          rc = pb.ny == 4096 ? go(std::integral_constant<int, 4096>{}) : go(std::integral_constant<int, 2048>{});
+        }
         if (rc) return rc;
         HIP_TRY(hipGetLastError());
         return PDHG_OK;
@@ -1974,12 +2001,12 @@ struct Impl : ImplBase {
     };
     if (phi) {
       const R* src = src_of(phi, nphi);
-      HIP_TRY(hipMemcpy(kp.phi, src, nphi * sizeof(R), hipMemcpyHostToDevice));
-      HIP_TRY(hipMemcpy(kp.phibar, src, nphi * sizeof(R), hipMemcpyHostToDevice));
+      H2D(kp.phi, src, nphi * sizeof(R));
+      H2D(kp.phibar, src, nphi * sizeof(R));
       compute_row0_sq(std::vector<R>(src, src + npl));
     }
     const size_t n = (size_t)T * npl;
-    if (rho) HIP_TRY(hipMemcpy(kp.rho[cur], src_of(rho, n), n * sizeof(R), hipMemcpyHostToDevice));
+    if (rho) H2D(kp.rho[cur], src_of(rho, n), n * sizeof(R));
     if (alp) {
       const int nc = n_ctrl(), nar = n_alp_ref();
       for (int a = 0; a < nar; ++a)
@@ -1994,13 +2021,13 @@ struct Impl : ImplBase {
         for (int c = 0; c < nc; ++c) {
           if (!live(a, c, nc)) continue;
           for (size_t i = 0; i < n; ++i) buf[i] = (R)alp[((size_t)a * n + i) * nc + c];
-          HIP_TRY(hipMemcpy(kp.alp[cur][a], buf.get(), n * sizeof(R), hipMemcpyHostToDevice));
+          H2D(kp.alp[cur][a], buf.get(), n * sizeof(R));
         }
     }
     Ctrl h{};
     h.cur = cur;
     h.row0_sq = row0_sq;
-    HIP_TRY(hipMemcpy(kp.ctrl, &h, sizeof(Ctrl), hipMemcpyHostToDevice));
+    H2D(kp.ctrl, &h, sizeof(Ctrl));
     primal_done = false;
     return PDHG_OK;
   }
@@ -2009,7 +2036,7 @@ struct Impl : ImplBase {
     const size_t n = (size_t)(pb.T + 1) * plane();
     std::vector<R> buf(n);
     for (size_t i = 0; i < n; ++i) buf[i] = (R)pbar[i];
-    HIP_TRY(hipMemcpy(kp.phibar, buf.data(), n * sizeof(R), hipMemcpyHostToDevice));
+    H2D(kp.phibar, buf.data(), n * sizeof(R));
     return PDHG_OK;
   }
 
@@ -2104,7 +2131,7 @@ struct Impl : ImplBase {
     R* d_row;
     int rc;
     HIP_TRY(hipMalloc((void**)&d_row, npl * sizeof(R)));
-    HIP_TRY(hipMemcpy(d_row, row.data(), npl * sizeof(R), hipMemcpyHostToDevice));
+    H2D(d_row, row.data(), npl * sizeof(R));
     const int grid = 4096;
     hipLaunchKernelGGL((k_bcast_rows<R>), dim3(grid), dim3(256), 0, stream, kp.phi, d_row, npl, T + 1);
     hipLaunchKernelGGL((k_bcast_rows<R>), dim3(grid), dim3(256), 0, stream, kp.phibar, d_row, npl, T + 1);
@@ -2116,7 +2143,7 @@ struct Impl : ImplBase {
     hipFree(d_row);
     Ctrl h{};
     h.row0_sq = row0_sq;
-    HIP_TRY(hipMemcpy(kp.ctrl, &h, sizeof(Ctrl), hipMemcpyHostToDevice));
+    H2D(kp.ctrl, &h, sizeof(Ctrl));
     (void)rc;
     primal_done = false;
     return PDHG_OK;
@@ -2139,7 +2166,7 @@ struct Impl : ImplBase {
     h.inner_done = 0;
     h.inner_count = 0;
     h.kstar_found = 0;
-    HIP_TRY(hipMemcpy(kp.ctrl, &h, sizeof(Ctrl), hipMemcpyHostToDevice));
+    H2D(kp.ctrl, &h, sizeof(Ctrl));
     if ((rc = launch_dual((R)sigma, eps, k))) return rc;
     if (primal_done) {
       if ((rc = launch_outer(eps, k))) return rc;

@@ -112,7 +112,11 @@ struct pdhg_multi {
     void* q = nullptr;
     if (hipMalloc(&q, std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess)
       return fail(PDHG_ERR_HIP, "hipMalloc of %zu bytes on device %d", n * sizeof(T), dev[r]);
-    if (hipMemset(q, 0, std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess) return fail(PDHG_ERR_HIP, "hipMemset");
+    // zeroed on the slab's main stream: st / ss are non-blocking streams, which a legacy-stream hipMemset is not
+    // ordered with (a plane a slab never receives -- slab 0's D_left, the last slab's S1_right -- must read zero);
+    // setup() drains st / ss (full_barrier) before any exchange
+    if (hipMemsetAsync(q, 0, std::max<size_t>(n, 1) * sizeof(T), st[r]) != hipSuccess)
+      return fail(PDHG_ERR_HIP, "hipMemsetAsync");
     allocs.push_back(q);
     alloc_dev.push_back(dev[r]);
     *p = static_cast<T*>(q);

@@ -8,8 +8,10 @@ default threshold, =0 turns it off.  Bounds: the fp32 bounds of test_gpu_parity 
 10 iterations from the seeded state); fused vs unfused device runs agree to fp32 reassociation (1e-5).
 
 fp64 (ny = 2048 / 4096: the sweep k_dual_lds_2d<.., double, 2> on 128-column strips, the residual in 4-row
-half-tile tasks of k_res_fwdy_fused_2d<.., 4, 512, double>): against the float64 oracle at 1e-9 (phi, rho; the
-fp64 bar of test_gpu_configs) and against the unfused fp64 kernels at 1e-12.
+half-tile tasks of k_res_fwdy_fused_2d<.., 4, 512, double>; ny = 8192, C4's: 2-row quarter-tile tasks,
+k_res_fwdy_fused_2d<.., 8192, 2, 512, double>): against the float64 oracle at 1e-9 (phi, rho; the fp64 bar of
+test_gpu_configs) and against the unfused fp64 kernels at 1e-12; at C4's full 8192^2 plane (the half-real
+spectrum, one column per block: 16-B chunk stores) against the unfused kernels.
 """
 import numpy as np
 import pytest
@@ -39,6 +41,8 @@ FUSED64 = [
     (2, 2, 32, 2048, 4, 1e-5),
     (1, 2, 16, 2048, 3, 0.0),
     (2, 2, 24, 4096, 2, 1e-4),   # 3 tiles of 8 rows = 6 half-tile tasks per time row; 32 strips
+    (2, 2, 32, 8192, 3, 1e-5),   # ny = 8192: 4 quarter-tile tasks per tile, 64 strips
+    (1, 2, 24, 8192, 2, 0.0),
 ]
 IDS64 = ["e{}d{}_{}x{}_T{}_eps{}".format(*c) for c in FUSED64]
 
@@ -49,7 +53,8 @@ def _ctx(P, fuse, monkeypatch, precision="fp32"):
     ctx = device_ctx(P, precision)
     assert ctx.path_info("fused_residual") == (1 if fuse else 0)
     if precision == "fp64" and fuse:
-        assert ctx.path_info("dual_ypl") == 2 and ctx.path_info("res64") == 1
+        assert ctx.path_info("dual_ypl") == 2
+        assert ctx.path_info("res64" if P["ny"] < 8192 else "ip_rows") == 1
     return ctx
 
 
@@ -165,3 +170,17 @@ def test_dual_neighbour_sync_bitwise(native, monkeypatch, prec, case, fuse):
     for a, b in zip((s1[0], s1[1]) + tuple(s1[2]), (s0[0], s0[1]) + tuple(s0[2])):
         assert np.array_equal(a, b)
     assert st1["err1"] == st0["err1"] and st1["err2"] == st0["err2"]
+
+
+@pytest.mark.parametrize("epsl,n", [(0.0, 4), (0.1, 2)])
+def test_fused_fp64_c4_plane(native, monkeypatch, epsl, n):
+    """C4's 8192^2 plane in fp64 (T = 3): the half-real x blocks (B = 1), so every fused-residual chunk is the two
+    rows of a task at one ky (a 16-B store) -- against the unfused fp64 kernels (ip_rows): phi, rho within 1e-12.
+    The controls too at epsl = 0; at epsl = 0.1 (sigma*epsl/dx^2 = 2.5e5 at C4's dx) the residual's other
+    association (formed in the sweep) moves a few controls that sit at their clamp by more: 1e-8 (measured 2.8e-9)."""
+    P = make_problem(2, 2, 8192, 8192, 3, epsl)
+    (s0, st0), (s1, st1) = [_run(P, fuse, n, monkeypatch, "fp64") for fuse in (False, True)]
+    assert rel(s1[0], s0[0]) < 1e-12 and rel(s1[1], s0[1]) < 1e-12
+    for a, b in zip(s1[2], s0[2]):
+        assert rel(a, b) < (1e-12 if epsl == 0 else 1e-8)
+    assert abs(st1["err1"] - st0["err1"]) <= 1e-10 * st0["err1"]
