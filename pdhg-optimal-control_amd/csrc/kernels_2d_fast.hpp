@@ -140,14 +140,17 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<R> p, const cplx<R>*
   int j, gx;
   const int TJ = p.tile_j, ntiled = (p.row_cnt / TJ) * TJ * ngx;
   if (TJ > 1 && task < ntiled) {
-    // tiles of 4 row groups x TJ time rows: the ~32 tasks an XCD runs together share rho row j+1
+    // tiles of TW row groups x TJ time rows: the ~32 tasks an XCD runs together share rho row j+1
     // and the x-halo rows in that XCD's L2 (needs ngx % 4 == 0, checked on the host); the rows
-    // after the last whole tile fall back to the row-major order below
-    const int tsz = 4 * TJ, ngt = ngx >> 2;
+    // after the last whole tile fall back to the row-major order below.  Chunks of < 64 B (C4's half-real
+    // spectrum, B = 1): 8 row groups per tile, so one XCD writes whole 128-B lines of the spectrum
+    // (PDHG_DBG 2048: 4 groups, A/B timing only)
+    const int lTW = (RW * p.B * (int)sizeof(R) < 64 && (ngx & 7) == 0 && !(p.dbg & 2048)) ? 3 : 2;
+    const int tsz = TJ << lTW, ngt = ngx >> lTW;
     const int tile = task / tsz, w = task - tile * tsz;
     const int tjx = tile / ngt, tg = tile - tjx * ngt;
-    j = tjx * TJ + (w >> 2);
-    gx = tg * 4 + (w & 3);
+    j = tjx * TJ + (w >> lTW);
+    gx = (tg << lTW) + (w & ((1 << lTW) - 1));
   } else {
     const int t2 = task - (TJ > 1 ? ntiled : 0);
     j = t2 / ngx;
@@ -413,13 +416,13 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<R> p, const cplx<R>
       }
     }
   };
-  // fp64 C4 (2-row tasks, B = 1: 16-B chunks, 8 tasks per 128-B line of the spectrum): XCD-aware task order, the
+  // C4 (B = 1: 16-B chunks, 8 tasks per 128-B line of the spectrum; fp64 2-row, fp32 4-row tasks): XCD-aware order, the
   // G / 8 workgroups of one XCD take consecutive tasks in every round, so a line's chunks are written through one
   // L2.  Interleaved A/B (round 5, c4w50 fp64): residual 73.2 -> 60.4 ms; at C3's 64-B chunks (2 tasks per line)
   // the same order measured slower (fp64 15.5 -> 17.8 ms, fp32 neutral), so only the 2-row tasks take it.
   // (PDHG_DBG 1024: round-robin order, A/B timing only)
-  constexpr bool XCDO = RW == 2;
-  int task = (XCDO && (gridDim.x & 7) == 0 && !(p.dbg & 1024)) ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const bool xcdo = RW * p.B * (int)sizeof(R) < 64;   // 16-B chunks (B = 1, half-real x blocks)
+  int task = (xcdo && (gridDim.x & 7) == 0 && !(p.dbg & 1024)) ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
   int buf = 0;
   if (task < ntask) {
     load_rows(task, 0, RW);

@@ -474,9 +474,10 @@ struct Impl : ImplBase {
                                           : ((res64 && (ny == 4096 || ny == 2048)) || (ip_rows && ny == 8192));
       if (fast_dual && dual_rx == 8 && fr_rows && pb.bc_x == 0 && pb.bc_y == 0 && pb.egno != 3 && !two_sets &&
           !xslab) {
-        // fp32 ny = 8192: off unless asked for (c4w50 A/B, round 4: residual 31.2 -> 25.9 ms, dual 26.7 -> 31.3 ms,
-        // step 105.2 vs 104.7 -- the 4-row tasks' 16-B runs of the B = 1 spectrum, not the reads, bound the residual)
-        fuse_res = gxd * gyd >= 1024 && !(sizeof(R) == 4 && RWf == 4);
+        // fp32 ny = 8192 (4-row half-tile tasks, 16-B chunks of the B = 1 spectrum): round 4 measured it neutral
+        // (residual 31.2 -> 25.9 ms, dual 26.7 -> 31.3); with the XCD-ordered tasks (round 5, interleaved A/B at
+        // c4w50) the fused residual runs 22.9 ms against 30.3 unfused, step 88.25 -> 85.64 ms: on by default
+        fuse_res = gxd * gyd >= 1024;
         if (const char* e = getenv("PDHG_FUSE_RES")) fuse_res = atoi(e) != 0;
         if (fuse_res) {
           if (sizeof(R) == 8) {

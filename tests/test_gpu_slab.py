@@ -132,6 +132,7 @@ FUSED_CASES = [
     (2, 4096, 256, 16, 2),     # 8-row slabs: batched x transform
     (1, 512, 256, 3, 3),       # one-row slabs: the halo launch is the whole slab
     (2, 512, 256, 19, 2),      # residual tiles of 8 rows + remainder rows
+    (2, 64, 8192, 8, 2),       # ny = 8192 (C4): 4-row half-tile tasks, XCD-ordered
 ]
 
 
