@@ -127,6 +127,9 @@ struct Impl : ImplBase {
   int gx1 = 0, gx4 = 0, g4 = 1, gx5 = 0, g5 = 1, g_outer = 1;
   int nt_row = 256;   // threads of the generic 2-D row kernels (k_res_fwdy_2d, k_invy_update_2d)
   int rows_var = 0;                       // row-kernel shape variant (see with_fast_rows)
+  // fp64 fused residual threads at ny = 4096 (PDHG_RES64_NT=1024: GPT = 1, 128 VGPRs + 108 B of spills; interleaved
+  // A/B at C3 fp64, round 5: 17.1 vs 15.5 ms, so 512 stays)
+  int res64_nt = 512;
   int half_nt = 3;                        // ny = 4096 row kernels with 512 threads (bit 0 residual, bit 1 update)
   int upd_pf = 4;                         // update kernel (512 threads): old-phi row pairs in flight (1..4)
   bool fast_dual = false;                 // fp32 time-marching float4 dual kernel (k_dual_fast_2d)
@@ -425,6 +428,7 @@ struct Impl : ImplBase {
       }
       if (const char* e = getenv("PDHG_ROWS_VAR")) rows_var = atoi(e);   // tuning override
       if (const char* e = getenv("PDHG_HALF_NT")) half_nt = atoi(e);     // tuning: 1 fused residual, 2 update
+      if (const char* e = getenv("PDHG_RES64_NT")) res64_nt = atoi(e) == 1024 ? 1024 : 512;   // tuning
       if (const char* e = getenv("PDHG_UPD_PF")) upd_pf = atoi(e);       // tuning: update prefetch depth
       if (sizeof(R) == 4 && ply.pow2 && ny >= 256 && ny <= 8192) {
         RWf = (ny == 8192) ? 4 : 8;
@@ -817,6 +821,18 @@ struct Impl : ImplBase {
           constexpr int N_ = decltype(Nc)::value;
           const dim3 g(std::min((pb.nx / 4) * (hi - lo), n_cu));   // persistent, one workgroup per CU (LDS)
           int r2;
+          if constexpr (N_ == 4096) {
+            if (res64_nt == 1024) {   // A/B: 16 waves per CU (GPT = 1)
+              if (pb.egno == 1) {
+                if ((r2 = ensure_lds(k_res_fwdy_fused_2d<1, N_, 4, 1024, double>, lds_upd64))) return r2;
+                hipLaunchKernelGGL((k_res_fwdy_fused_2d<1, N_, 4, 1024, double>), g, dim3(1024), lds_upd64, stream, p, twy);
+              } else {
+                if ((r2 = ensure_lds(k_res_fwdy_fused_2d<2, N_, 4, 1024, double>, lds_upd64))) return r2;
+                hipLaunchKernelGGL((k_res_fwdy_fused_2d<2, N_, 4, 1024, double>), g, dim3(1024), lds_upd64, stream, p, twy);
+              }
+              return (int)PDHG_OK;
+            }
+          }
           if (pb.egno == 1) {
             if ((r2 = ensure_lds(k_res_fwdy_fused_2d<1, N_, 4, 512, double>, lds_upd64))) return r2;
             hipLaunchKernelGGL((k_res_fwdy_fused_2d<1, N_, 4, 512, double>), g, dim3(512), lds_upd64, stream, p, twy);
