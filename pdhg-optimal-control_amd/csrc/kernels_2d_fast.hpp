@@ -511,6 +511,7 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<R> p, const cplx<R>
 
 // G workgroups striding over the T * nx/RW row-group tasks; block NT; LDS RW/2 * (N + N/16) * 8 B.
 // sums: [0] sum (phi'-phi)^2, [1] sum phi^2 (old), [2] sum phi'^2
+// RW = 2 with B = 1 (fp64 at C4's ny = 8192 with the half-real x blocks): one line, 16-B chunks.
 template <int N, int RW, int NT, int PF = 1, typename R = float>
 __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<R> p, const cplx<R>* __restrict__ twy) {
   using C = cplx<R>;
@@ -548,6 +549,17 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<R> p, const cplx<
     // laundered per task so the 4*BATCH LDS addresses are not hoisted out of the task loop (registers).
     int tl = tid;
     asm volatile("" : "+v"(tl));
+    if (RW == 2 && B == 1) {   // fp64 C4 (half-real spectrum): chunk b = rows x0, x0+1 at ky = b, one 16-B load
+      constexpr int NC = N / NT, CB = NC < 8 ? NC : 8;
+#pragma unroll
+      for (int i0 = 0; i0 < NC; i0 += CB) {
+        C v[CB];
+#pragma unroll
+        for (int i = 0; i < CB; ++i) v[i] = *reinterpret_cast<const C*>(wk + (size_t)(tl + (i0 + i) * NT) * nx + x0);
+#pragma unroll
+        for (int i = 0; i < CB; ++i) A[pix(tl + (i0 + i) * NT)] = v[i];
+      }
+    } else
 #pragma unroll
     for (int i0 = 0; i0 < NLD; i0 += BATCH) {
       V v[BATCH];

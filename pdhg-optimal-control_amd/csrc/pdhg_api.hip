@@ -179,6 +179,7 @@ struct Impl : ImplBase {
   int RWf = 8, NTf = 1024, g_fast_upd = 1;
   size_t lds_fast = 0, lds_fast_tw = 0;
   bool res64 = false;      // fp64 residual and update through the fast row kernels (4-row groups)
+  bool upd8192 = false;    // fp64 ny = 8192, half-real x: update through the fast row kernel on 2-row tasks
   size_t lds_res64 = 0, lds_upd64 = 0;
   size_t partial_rows = 0;
   static constexpr int kFoldRows = 64;   // rows of the first fold level (k_fold_partials) after the table
@@ -341,6 +342,10 @@ struct Impl : ImplBase {
       // in place in one padded line (FFTIp, 136 KiB) instead of a Stockham ping-pong of two (256 KiB)
       ip_rows = sizeof(R) == 8 && ny == 8192 && lds_res > kLdsBytes && !xslab;
       if (ip_rows) lds_res = (size_t)Pad<8192>::LINE * csz;
+      // ... and the update through the fast row kernel on 2-row tasks when the x blocks are half-real (B = 1)
+      upd8192 = ip_rows && half_real && nx % 2 == 0;
+      if (const char* e = getenv("PDHG_UPD8192")) upd8192 = upd8192 && atoi(e) != 0;   // A/B: 0 = generic kernel
+      if (upd8192) g_fast_upd = std::min((nx / 2) * T, 2048);
       if (lds_res > kLdsBytes) return fail(PDHG_ERR_UNSUPPORTED, "ny=%d exceeds the LDS row transform", ny);
       {   // generic row kernels: when the LDS admits few workgroups per CU (fp64 ny = 4096: one), wider
           // workgroups keep >= 16 waves per CU in flight for the residual's scattered loads
@@ -1199,6 +1204,14 @@ struct Impl : ImplBase {
           rc = pb.ny == 4096 ? go(k_invy_update_fast_2d<4096, 4, 512, 4, double>)
                              : go(k_invy_update_fast_2d<2048, 4, 512, 4, double>);
           if (rc) return rc;
+          upd_done = true;
+        } else if (upd8192) {   // fp64 ny = 8192, half-real x blocks: 2-row tasks on one padded line
+          ProfScope ps(this, "update");
+          upd_rows = g_fast_upd;
+          const size_t lds = (size_t)Pad<8192>::LINE * sizeof(C);
+          if ((rc = ensure_lds(k_invy_update_fast_2d<8192, 2, 512, 2, double>, lds))) return rc;
+          hipLaunchKernelGGL((k_invy_update_fast_2d<8192, 2, 512, 2, double>), dim3(g_fast_upd), dim3(512), lds, stream,
+                             p, twy);
           upd_done = true;
         }
       }
@@ -2459,7 +2472,8 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
     else if (k == "half_real") *value = im.half_real ? 1 : 0;
     else if (k == "fourstep") *value = im.fourstep ? 1 : 0;
     else if (k == "glb_line") *value = im.glb_line ? 1 : 0;
-    else if (k == "ip_rows") *value = im.ip_rows ? 1 : 0;   // fp64 ny = 8192 row pairs in one padded line
+    else if (k == "ip_rows") *value = im.ip_rows ? 1 : 0;
+    else if (k == "upd8192") *value = im.upd8192 ? 1 : 0;   // fp64 ny = 8192: 2-row fast update   // fp64 ny = 8192 row pairs in one padded line
     else if (k == "thomas_chunk") *value = im.thomas_chunk ? 1 : 0;
     else if (k == "fs_wide") *value = (im.fourstep && im.fs_wide && !im.fs16) ? 1 : 0;
     else if (k == "fs16") *value = im.fs16 ? 1 : 0;

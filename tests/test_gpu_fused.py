@@ -184,3 +184,25 @@ def test_fused_fp64_c4_plane(native, monkeypatch, epsl, n):
     for a, b in zip(s1[2], s0[2]):
         assert rel(a, b) < (1e-12 if epsl == 0 else 1e-8)
     assert abs(st1["err1"] - st0["err1"]) <= 1e-10 * st0["err1"]
+
+
+def test_fp64_update_c4_plane_fast_vs_generic(native, monkeypatch):
+    """fp64 at C4's 8192^2 plane: the inverse DHT_y + update through the fast row kernel on 2-row tasks
+    (k_invy_update_fast_2d<8192, 2, ..., double>, 16-B chunks of the half-real spectrum) against the generic row-pair
+    kernel (PDHG_UPD8192=0): the same float64 arithmetic up to the transform's association, 1e-12 after 3 iterations."""
+    P = make_problem(2, 2, 8192, 8192, 3, 0.0)
+    out = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("PDHG_UPD8192", flag)
+        ctx = device_ctx(P, "fp64")
+        try:
+            assert ctx.path_info("upd8192") == int(flag) and ctx.path_info("half_real") == 1
+            ctx.set_state(P["phi"], P["rho"], P["alp"])
+            st = ctx.iterate(3, TAU, SIGMA, -1.0, 1)
+            out.append((ctx.get_state(), st))
+        finally:
+            ctx.close()
+    (s1, st1), (s0, st0) = out
+    for a, b in zip((s1[0], s1[1]) + tuple(s1[2]), (s0[0], s0[1]) + tuple(s0[2])):
+        assert rel(a, b) < 1e-12
+    assert abs(st1["err1"] - st0["err1"]) <= 1e-10 * st0["err1"]
