@@ -125,6 +125,7 @@ struct Impl : ImplBase {
   // launch geometry
   int NT2 = 512;
   int gx1 = 0, gx4 = 0, g4 = 1, gx5 = 0, g5 = 1, g_outer = 1;
+  int head_xrun = 4;   // x rows per workgroup of the head form's chunk passes (PDHG_HEAD_XRUN)
   int nt_row = 256;   // threads of the generic 2-D row kernels (k_res_fwdy_2d, k_invy_update_2d)
   int rows_var = 0;                       // row-kernel shape variant (see with_fast_rows)
   // fp64 fused residual threads at ny = 4096 (PDHG_RES64_NT=1024: GPT = 1, 128 VGPRs + 108 B of spills; interleaved
@@ -529,6 +530,8 @@ struct Impl : ImplBase {
       if (const char* e = getenv("PDHG_THOMAS_CHUNK")) thomas_chunk = thomas_chunk && atoi(e) != 0;   // override
     }
     g_outer = 2048;
+    if (const char* e = getenv("PDHG_G_OUTER")) g_outer = std::max(64, std::min(4096, atoi(e)));   // tuning override
+    if (const char* e = getenv("PDHG_HEAD_XRUN")) head_xrun = std::max(1, atoi(e));               // tuning override
     // rho_alp_iters > 1 on the row-per-thread dual grid, single contexts: the dual loop in chunk passes of
     // kMultiSub sub-iterations in registers (+ a final pass when the exit falls inside a chunk)
     // Only where a pass is bandwidth-bound: C2's T = 1 marching windows (4 M points, the loop exiting after a few
@@ -1473,7 +1476,7 @@ struct Impl : ImplBase {
   template <int EGNO>
   void launch_dual_multi_e(const KP<R>& p, int k, double eps, int slo0 = 0) {   // slo0 = 1: head form
     // head form: runs of 4 x rows per workgroup (its passes mostly return at once; fewer workgroups to retire)
-    const int xrun = (slo0 > 0 && pb.nx % 4 == 0) ? 4 : 1;
+    const int xrun = (slo0 > 0 && pb.nx % head_xrun == 0) ? head_xrun : 1;
     const int gx = (pb.nx + xrun - 1) / xrun;
     const dim3 g(gx, gyd, gzd);
     const int rows = gx * gyd * gzd;
