@@ -323,6 +323,12 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fast_2d(KP<R> p, const cplx<R>*
   const int CS4 = RW * B / 4;                 // V per chunk
   const int lCS4 = p.lB + (RW == 8 ? 1 : RW == 4 ? 0 : RW == 2 ? -1 : -2);   // log2(CS4), B power of two
   const int nb = p.nb;
+  if (p.rspec) {   // task order (tc_spec): the task's RW rows x all ky, one contiguous run
+    R* wt = p.rspec + (size_t)j * nb * nx * B + (size_t)x0 * nb * B;
+    for (int t = threadIdx.x; t < nb * CS4; t += NT)
+      st4(wt + 4 * t, unpack_chunk4<N, Pad<N>::LINE, R>(A, t >> lCS4, t & (CS4 - 1), B, p.lB));
+    return;
+  }
   R* wk = p.work + (size_t)j * nb * nx * B;
   for (int t = threadIdx.x; t < nb * CS4; t += NT) {
     const int b = t >> lCS4, part = t & (CS4 - 1);
@@ -491,7 +497,11 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<R> p, const cplx<R>
     if constexpr (RSPLIT < RW) load_rows(nxt, RSPLIT, RW);
     load_edges(nxt);
     R* wk = p.work + (size_t)j * nb * nx * B;
-    if (RW * B < 4) {   // RW = 2, B = 1 (fp64 C4): chunk b = rows x0, x0+1 at ky = b, one 16-B store
+    if (p.rspec) {   // task order (tc_spec): one contiguous run per task
+      R* wt = p.rspec + (size_t)j * nb * nx * B + (size_t)x0 * nb * B;
+      for (int t = tid; t < nb * CS4; t += NT)
+        st4(wt + 4 * t, unpack_chunk4<N, LN, R>(A, t >> lCS4, t & (CS4 - 1), B, p.lB));
+    } else if (RW * B < 4) {   // RW = 2, B = 1 (fp64 C4): chunk b = rows x0, x0+1 at ky = b, one 16-B store
       for (int b = tid; b < nb; b += NT) {
         R ha, hb;
         hartley_padded<C, R>(A, N, b, ha, hb);

@@ -56,7 +56,11 @@ __device__ __forceinline__ double theta_of(double dd) {
 // grid: nb column blocks; block NT; LDS (N + N/16 + TwLds<N> + N (+ 128 HR)) * 16 B.
 // BPR: b' / x of the thread's items in registers instead of the LDS array (nx <= 2048: IT <= 4 items leave the
 // registers for it, and the smaller LDS footprint admits a second workgroup per CU).
-template <int N, int NT, bool HR = false, bool BPR = false>
+// TC: the forward sweep reads the residual spectrum in task order (p.rspec: per 4-row task, 8 reals per column block
+// b = rows x0..x0+3 at columns 2b, 2b+1): item x = tid + i NT sits at 16 B x (x & 3) of its task's 64-B piece, so
+// the 4 lanes of a task read one contiguous 64-B piece (16 pieces per wave load instead of 1 KiB runs); b' and x go
+// to `work` (blocked) as always.
+template <int N, int NT, bool HR = false, bool BPR = false, bool TC = false>
 __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const double2* __restrict__ twx) {
   using C = double2;
   constexpr int IT = N / NT;
@@ -70,13 +74,17 @@ __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const do
   C* bp = twl + TwLds<N>::SIZE;   // b' / x per item (BPR: unused, none allocated)
   C* rsw = bp + (BPR ? 0 : N);    // HR: W_{2N}^j and W_{2N}^{64 j}, j < 64
   static_assert(!(BPR && HR), "half-real blocks keep b' in LDS");
+  static_assert(!TC || (!HR && !BPR && NT % 4 == 0), "task-order input: column pairs, 4-row tasks");
   fill_twlds<C, N>(twl, twx, HR ? 2 : 1);   // HR: twx holds W_{2N}
   if constexpr (HR) {
     static_assert(N == 4096, "split-twiddle tables sized for 2N = 8192");
     for (int i = threadIdx.x; i < 128; i += blockDim.x) rsw[i] = twx[i < 64 ? i : 64 * (i - 64)];
   }
   const int T = p.T, tid = threadIdx.x;
-  const int b = blockIdx.x + p.b0;   // t-slab carry exchange: blocks [b0, b0 + gridDim.x)
+  // t-slab carry exchange: blocks [b0, b0 + gridDim.x).  TC: XCD-aware order, the gridDim/8 workgroups of one XCD
+  // take consecutive column blocks, so the two blocks sharing each 128-B line of the task-order input (64 B each)
+  // read it through one L2 (round robin put them on different XCDs: every line fetched twice)
+  const int b = ((TC && !(p.dbg & 4096)) ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x) + p.b0;
   double* wb = p.work + (size_t)b * M;
   const size_t kstride = (size_t)p.nb * M;
   const double inv_ae = 1.0 / (double)p.ae;
@@ -107,7 +115,9 @@ __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const do
       A[pix(kx_of(i))] = x;
     }
   };
+  // item i of this thread at byte voff + ioff(i) of a blocked row
   const int voff = tid * (int)sizeof(C);
+  auto ioff = [&](int i) { return i * NT * (int)sizeof(C); };
   auto rowr = [&](int kk) { return row_rsrc(wb + (size_t)kk * kstride, M * (int)sizeof(double)); };
   // c1: forward dd, then e^-th once converged; backward theta.  c2: forward h = 1 - g; backward E_{k+2}, or
   // e^-th once converged.
@@ -136,7 +146,20 @@ __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const do
   auto ldrow = [&](int kk) {
     const auto r = rowr(kk);
 #pragma unroll
-    for (int i = 0; i < IT; ++i) pf[i] = buf_ld2(r, voff, i * NT * (int)sizeof(C));
+    for (int i = 0; i < IT; ++i) pf[i] = buf_ld2(r, voff, ioff(i));
+  };
+  // the forward sweep's input rows: `work` (blocked), or (TC) the task-order residual spectrum: row kk, block b,
+  // item x = tid + i NT at reals (x / 4) 4 ny + 8 b + 2 (x % 4)
+  const int ny_t = p.nb * 2;
+  auto ldrow_in = [&](int kk) {
+    if constexpr (TC) {
+      const auto r = row_rsrc(p.rspec + (size_t)kk * kstride + (size_t)8 * b, (int)(kstride * sizeof(double)) - 64 * b);
+      const int vin = 32 * ny_t * (tid >> 2) + 16 * (tid & 3);
+#pragma unroll
+      for (int i = 0; i < IT; ++i) pf[i] = buf_ld2(r, vin, 8 * ny_t * NT * i);
+    } else {
+      ldrow(kk);
+    }
   };
   const int j0 = p.j0;
   const bool slab = p.slab != 0;
@@ -153,13 +176,13 @@ __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const do
     //   last (Neumann) row of the window: x_{T-1} = (rhs/ae + b'_{T-2}) / (dd + h_{T-2})   [converged: dd + h = (1 - g)/g]
     // A t-slab indexes the pivots by the GLOBAL row j0 + k; only the window's last slab has the Neumann row, and
     // a slab stores every row (the backward sweep is a separate launch after the carry fix-up).
-    ldrow(0);
+    ldrow_in(0);
     for (int k = 0; k < T; ++k) {
       const int kg = j0 + k;
       const bool nrow = k == T - 1 && p.last_slab;   // the window's Neumann row
 #pragma unroll
       for (int i = 0; i < IT; ++i) A[pix(kx_of(i))] = pf[i];
-      if (k + 1 < T) ldrow(k + 1);
+      if (k + 1 < T) ldrow_in(k + 1);
       lds_sync();
       lds_fft_inplace_tl<C, N, 1, NT>(A, twl);
 #pragma unroll
@@ -185,11 +208,11 @@ __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const do
             bn = make_double2(r0 * g0, r1 * g1);
             c2[i] = make_double2(s0 * g0, s1 * g1);
           }
-          buf_st2(dst, voff, i * NT * (int)sizeof(C), bn);
+          buf_st2(dst, voff, ioff(i), bn);
         } else {
           if (fast) bn = make_double2(r0 * c1[i].x / (1.0 - c1[i].x), r1 * c1[i].y / (1.0 - c1[i].y));
           else bn = make_double2(r0 / (c1[i].x + c2[i].x), r1 / (c1[i].y + c2[i].y));
-          if (slab) buf_st2(dst, voff, i * NT * (int)sizeof(C), bn);   // re-read after the carry fix-up
+          if (slab) buf_st2(dst, voff, ioff(i), bn);   // re-read after the carry fix-up
         }
         bp_st(i, bn);
       }
@@ -254,7 +277,7 @@ __global__ void __launch_bounds__(NT) k_precond_xt_f64_2d(KP<double> p, const do
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, ha), wk, tid * 8, i * NT * 8, 0);
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, hb), wk, tid * 8, (i * NT + N) * 8, 0);
       } else {
-        buf_st2(wk, voff, i * NT * (int)sizeof(C), make_double2(ha, hb));
+        buf_st2(wk, voff, ioff(i), make_double2(ha, hb));
       }
     }
     lds_sync();

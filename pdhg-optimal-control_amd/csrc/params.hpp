@@ -32,6 +32,10 @@ struct KP {
   R* phi;                  // [T+1][nx][ny]
   R* phibar;               // [T+1][nx][ny]
   R* work;                 // spectral work buffer
+  // residual spectrum in task order (fp64 C3, tc_spec): the row kernels store each task's RW rows x all ky as one
+  // contiguous run [T][nx/RW][N/B][RW][B] instead of RW*B-real chunks of the blocked layout; the x kernel's forward
+  // sweep reads it and writes b' into `work` (blocked).  nullptr: the residual goes to `work` directly
+  R* rspec;
   R* rho[2];               // [T][nx][ny]
   R* alp[2][4];            // live control components, each [T][nx][ny]
   double* partials;        // [blocks][kNumSums]

@@ -181,6 +181,7 @@ struct Impl : ImplBase {
   size_t lds_fast = 0, lds_fast_tw = 0;
   bool res64 = false;      // fp64 residual and update through the fast row kernels (4-row groups)
   bool upd8192 = false;    // fp64 ny = 8192, half-real x: update through the fast row kernel on 2-row tasks
+  bool tc_spec = false;    // fp64 C3: residual spectrum in task order (KP::rspec)
   size_t lds_res64 = 0, lds_upd64 = 0;
   size_t partial_rows = 0;
   static constexpr int kFoldRows = 64;   // rows of the first fold level (k_fold_partials) after the table
@@ -471,6 +472,10 @@ struct Impl : ImplBase {
           g_fast_upd = std::min((nx / 4) * T, 2048);
         }
       }
+      // fp64 C3 shape: the residual spectrum handed to the x transform in task order (p.rspec; one contiguous run per
+      // 4-row task instead of 64-B chunks of the blocked layout), the x kernel's forward sweep reading it
+      tc_spec = sizeof(R) == 8 && res64 && ny == 4096 && f64_xt && !half_real && nxg == 4096 && B == 2 && !xslab;
+      if (const char* e = getenv("PDHG_TC_SPEC")) tc_spec = tc_spec && atoi(e) != 0;   // A/B: 0 = blocked layout
       // fused residual: fp32 fast kernels with 8-row tiles on both sides, rho_alp_iters = 1 (in place),
       // periodic bc, egno 1/2, single context; each dual workgroup must march the whole window (the
       // residual row j needs rho'_{j+1}), so only grids with enough (x, y) tiles to fill the chip
@@ -601,10 +606,17 @@ struct Impl : ImplBase {
       p.gscr = g;
     }
     p.res = p.ex = p.ey = nullptr;
+    p.rspec = nullptr;
     if (fuse_res) {
       if ((rc = alloc(&p.res, (size_t)T * npl))) return rc;
       if ((rc = alloc(&p.ex, (size_t)T * (nx / 8) * 2 * ny))) return rc;
       if ((rc = alloc(&p.ey, (size_t)T * nx * (ny / (64 * dual_ypl)) * 2))) return rc;
+    }
+    // the task-order spectrum reuses the fused residual's R plane: a task's spectrum run [x0 rows, all ky] is exactly
+    // the region its R rows occupy, and the residual kernel holds those rows in registers before it stores the run
+    if (tc_spec) {
+      if (fuse_res) p.rspec = p.res;
+      else if ((rc = alloc(&p.rspec, nwork))) return rc;
     }
     if (xslab && (rc = alloc(&colwork, (size_t)T * xs_nbs * nxg * p.B))) return rc;
     if (slab) {
@@ -1096,8 +1108,14 @@ struct Impl : ImplBase {
           return PDHG_OK;
         }
         const size_t lds = (size_t)(Pad<4096>::LINE + TwLds<4096>::SIZE + 4096) * sizeof(C);
-        if ((rc = ensure_lds(k_precond_xt_f64_2d<4096, 512>, lds))) return rc;
-        hipLaunchKernelGGL((k_precond_xt_f64_2d<4096, 512>), dim3(nblk), dim3(512), lds, stream, p, twx);
+        if (p.rspec) {   // task-order residual spectrum in (tc_spec; b' / x rows in `work` as always)
+          if ((rc = ensure_lds(k_precond_xt_f64_2d<4096, 512, false, false, true>, lds))) return rc;
+          hipLaunchKernelGGL((k_precond_xt_f64_2d<4096, 512, false, false, true>), dim3(nblk), dim3(512), lds, stream, p,
+                             twx);
+        } else {
+          if ((rc = ensure_lds(k_precond_xt_f64_2d<4096, 512>, lds))) return rc;
+          hipLaunchKernelGGL((k_precond_xt_f64_2d<4096, 512>), dim3(nblk), dim3(512), lds, stream, p, twx);
+        }
         HIP_TRY(hipGetLastError());
         return PDHG_OK;
       }
@@ -2476,7 +2494,8 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
     else if (k == "fourstep") *value = im.fourstep ? 1 : 0;
     else if (k == "glb_line") *value = im.glb_line ? 1 : 0;
     else if (k == "ip_rows") *value = im.ip_rows ? 1 : 0;
-    else if (k == "upd8192") *value = im.upd8192 ? 1 : 0;   // fp64 ny = 8192: 2-row fast update   // fp64 ny = 8192 row pairs in one padded line
+    else if (k == "upd8192") *value = im.upd8192 ? 1 : 0;   // fp64 ny = 8192: 2-row fast update
+    else if (k == "tc_spec") *value = im.tc_spec ? 1 : 0;   // fp64 C3: task-order residual spectrum   // fp64 ny = 8192 row pairs in one padded line
     else if (k == "thomas_chunk") *value = im.thomas_chunk ? 1 : 0;
     else if (k == "fs_wide") *value = (im.fourstep && im.fs_wide && !im.fs16) ? 1 : 0;
     else if (k == "fs16") *value = im.fs16 ? 1 : 0;

@@ -38,3 +38,31 @@ def test_fp64_x_kernel(native, monkeypatch, parity_log, egno, nx, ny, T):
     b = {"primal_vs_oracle": 1e-9, "primal_vs_generic": 1e-12, "phi": 1e-12, "rho": 1e-12, "err1": 1e-10}
     parity_log("test_fp64_x_kernel", "e{}_{}x{}_T{}".format(egno, nx, ny, T), m, b)
     assert all(m[k] <= b[k] for k in m), m
+
+
+@pytest.mark.parametrize("fuse", ["1", "0"], ids=["fused", "unfused"])
+def test_fp64_task_order_spectrum(native, monkeypatch, parity_log, fuse):
+    """fp64 at C3's extents (4096^2): the residual spectrum handed to the x transform in task order (PDHG_TC_SPEC,
+    one contiguous run per 4-row task; the x kernel's forward sweep reads 64-B groups) against the blocked layout --
+    the same arithmetic on the same values, so the states agree to the last bit up to the compiler's contraction of
+    the two x-kernel instantiations (bound 1e-13; measured values to parity_log)."""
+    monkeypatch.setenv("PDHG_FUSE_RES", fuse)
+    P = make_problem(2, 2, 4096, 4096, 6, 0.0, seeded=True)
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("PDHG_TC_SPEC", flag)
+        ctx = device_ctx(P, "fp64")
+        try:
+            assert ctx.path_info("tc_spec") == int(flag) and ctx.path_info("fused_residual") == int(fuse)
+            ctx.set_state(P["phi"], P["rho"], P["alp"])
+            st = ctx.iterate(4, TAU, SIGMA, -1.0, 1)
+            out[flag] = (ctx.get_state(), st)
+        finally:
+            ctx.close()
+    (s1, st1), (s0, st0) = out["1"], out["0"]
+    m = {"phi": rel(s1[0], s0[0]), "rho": rel(s1[1], s0[1]),
+         "alp": max(rel(a, b) for a, b in zip(s1[2], s0[2])),
+         "err1": abs(st1["err1"] - st0["err1"]) / st0["err1"],
+         "bitwise": float(np.array_equal(s1[0], s0[0]) and np.array_equal(s1[1], s0[1]))}
+    parity_log("test_fp64_task_order_spectrum", "c3_4096x4096_T6_fuse" + fuse, m, {k: 1e-13 for k in m if k != "bitwise"})
+    assert all(m[k] <= 1e-13 for k in m if k != "bitwise"), m
