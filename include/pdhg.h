@@ -149,11 +149,12 @@ int pdhg_device_bytes(pdhg_ctx* ctx, unsigned long long* bytes);
 
 /* Which kernel variant a context selected (no reference counterpart; tests and benches assert the fast
  * paths engaged): "fused_residual" 1/0 (the dual sweep forms the next residual, k_dual_lds_2d FR; fp32 and
- * fp64 -- fp64 on 128-column strips with 4-row residual tasks; fp32 ny = 8192 only with PDHG_FUSE_RES=1),
+ * fp64 -- fp64 on 128-column strips with 4-row residual tasks, 2-row tasks at ny = 8192; fp32 ny = 8192 on 4-row
+ * tasks),
  * "fast_rows" 1/0 (fp32 8/4-row y-transform kernels), "fast_dual" (-1 generic, 0 row-per-thread,
  * RX rows through LDS), "dual_ypl" (y per lane of the LDS dual: 4, or 2 for fp64 with PDHG_DUAL_YPL=2;
  * 0 without it), "fast_xt" (0 generic, 1 single-role, 2 warp-specialised, 3 row-batched,
- * 4 row-batched with LDS-DMA staging x-transform), "half_real", "fourstep", "fs16" (1-D nx = 65536 as
+ * 4 row-batched with LDS-DMA staging x-transform, 5 its half-real form at nx = 8192), "half_real", "fourstep", "fs16" (1-D nx = 65536 as
  * 16 x 4096, fp32 and fp64), "fs_wide", "glb_line", "thomas_chunk" (1-D t-solve in chunks: 32 rows per wave
  * fp32, 16 rows per half-wave fp64), "rows_rw", "res_threads", "upd_threads",
  * "row_threads" (threads of the generic row kernels), "res64" 1/0 (fp64 residual and update through the
@@ -161,7 +162,10 @@ int pdhg_device_bytes(pdhg_ctx* ctx, unsigned long long* bytes);
  * from a physically contiguous allocation to hipMalloc; environment PDHG_ALLOC=contig|none overrides the
  * contiguous-for-fp32-2-D default), "dual64" 1/0 (fp64 contexts: the row-per-thread time-marching dual
  * k_dual_fast_2d<EGNO, double>, or with nx % 8 == 0 and T >= 3 the LDS-row sweep k_dual_lds_2d<EGNO, 8, .., double>;
- * default on where ny % 256 == 0, environment PDHG_DUAL64=0 selects the generic per-point kernel), "f64_xt" 1/0 (fp64 nx = 4096: k_precond_xt_f64_2d), "t1_xt64" 1/0 (fp64 one-row windows at a power-of-two nx in
+ * default on where ny % 256 == 0, environment PDHG_DUAL64=0 selects the generic per-point kernel), "f64_xt" 1/0 (fp64
+ * nx = 512 ... 8192: k_precond_xt_f64_2d; PDHG_XT64=0 the generic kernel), "ip_rows" 1/0 (fp64 ny = 8192: row pairs in
+ * one padded line), "upd8192" 1/0 (fp64 ny = 8192 with half-real x blocks: the 2-row fast update), "tc_spec" 1/0
+ * (fp64 C3 shape: the residual spectrum in task order), "t1_xt64" 1/0 (fp64 one-row windows at a power-of-two nx in
  * 512..4096: the carry-free k_precond_x_t1_2d<..., double>; PDHG_T1_XT=0 off), "graph" 1/0 (pdhg_iterate replays
  * windows of iterations from a captured HIP graph; default on, environment PDHG_GRAPH=0 launches every
  * iteration eagerly), "graph_window" (iterations per replayed graph). */
