@@ -165,7 +165,7 @@ int pdhg_device_bytes(pdhg_ctx* ctx, unsigned long long* bytes);
  * default on where ny % 256 == 0, environment PDHG_DUAL64=0 selects the generic per-point kernel), "f64_xt" 1/0 (fp64
  * nx = 512 ... 8192: k_precond_xt_f64_2d; PDHG_XT64=0 the generic kernel), "ip_rows" 1/0 (fp64 ny = 8192: row pairs in
  * one padded line), "upd8192" 1/0 (fp64 ny = 8192 with half-real x blocks: the 2-row fast update), "tc_spec" 1/0
- * (fp64 C3 shape: the residual spectrum in task order), "t1_xt64" 1/0 (fp64 one-row windows at a power-of-two nx in
+ * (fp64 C3 shape, windows of >= 100 rows: the residual spectrum in task order), "t1_xt64" 1/0 (fp64 one-row windows at a power-of-two nx in
  * 512..4096: the carry-free k_precond_x_t1_2d<..., double>; PDHG_T1_XT=0 off), "graph" 1/0 (pdhg_iterate replays
  * windows of iterations from a captured HIP graph; default on, environment PDHG_GRAPH=0 launches every
  * iteration eagerly), "graph_window" (iterations per replayed graph). */

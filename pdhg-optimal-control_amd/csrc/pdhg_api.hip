@@ -474,8 +474,11 @@ struct Impl : ImplBase {
       }
       // fp64 C3 shape: the residual spectrum handed to the x transform in task order (p.rspec; one contiguous run per
       // 4-row task instead of 64-B chunks of the blocked layout), the x kernel's forward sweep reading it
-      tc_spec = sizeof(R) == 8 && res64 && ny == 4096 && f64_xt && !half_real && nxg == 4096 && B == 2 && !xslab;
-      if (const char* e = getenv("PDHG_TC_SPEC")) tc_spec = tc_spec && atoi(e) != 0;   // A/B: 0 = blocked layout
+      // Interleaved A/B (round 5): C3's T = 200 118.8 -> 118.3 ms; its 25-row slab share (8 GPUs) 16.05 -> 16.35 ms
+      // (the x kernel's 64-B reads cost relatively more on short windows), so windows of >= 100 rows only
+      const bool tc_ok = sizeof(R) == 8 && res64 && ny == 4096 && f64_xt && !half_real && nxg == 4096 && B == 2 && !xslab;
+      tc_spec = tc_ok && T >= 100;
+      if (const char* e = getenv("PDHG_TC_SPEC")) tc_spec = tc_ok && atoi(e) != 0;   // A/B: 0 blocked, 1 task order
       // fused residual: fp32 fast kernels with 8-row tiles on both sides, rho_alp_iters = 1 (in place),
       // periodic bc, egno 1/2, single context; each dual workgroup must march the whole window (the
       // residual row j needs rho'_{j+1}), so only grids with enough (x, y) tiles to fill the chip

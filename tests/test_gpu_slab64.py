@@ -179,3 +179,15 @@ def test_fp64_multi_context_small(native, parity_log):
          "err1": abs(st["err1"] - st_ref["err1"]) / st_ref["err1"]}
     parity_log("test_fp64_multi_context_small", "e2_4096x256_T24_P3", m, {k: TOL for k in m})
     assert all(v <= TOL for v in m.values()), m
+
+
+def test_fp64_slabs_task_order_spectrum(native, parity_log, monkeypatch):
+    """The task-order residual spectrum (PDHG_TC_SPEC=1, the default of windows of >= 100 rows at C3's extents,
+    i.e. of 2-slab C3 runs) inside fp64 t-slabs: row-range residual launches and the x kernel's forward-sweep parts
+    read it; against the single fp64 context with the same layout, 1e-11."""
+    monkeypatch.setenv("PDHG_TC_SPEC", "1")
+    P = make_problem(2, 2, 4096, 4096, 16, 0.0)
+    st, st_ref, got, want = _run_pair(P, 2, 1, 6, {"tc_spec": 1, "fused_residual": 1})
+    m = _metrics(st, st_ref, got, want)
+    parity_log("test_fp64_slabs_task_order_spectrum", "e2_4096x4096_T16_P2", m, {key: TOL for key in m})
+    assert all(v <= TOL for v in m.values()), m
