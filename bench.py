@@ -47,6 +47,7 @@ CONFIGS = {
     # one GPU's share of the 8-GPU t-slab runs as a window of its own (C3: 200 / 8 rows, C4: 400 / 8 rows; the
     # per-GPU compute term of the multi-GPU cost model)
     "c3w25": (2, 2, 0.1, 4096, 4096, 26),
+    "c3w100": (2, 2, 0.1, 4096, 4096, 101),   # C3's per-GPU share at 2 GPUs
     "c4w50": (2, 2, 0.1, 8192, 8192, 51),
 }
 
