@@ -330,6 +330,40 @@ def dual_passes(inner_mean, nsub=5):
     return float(chunks + (0 if abs(q - round(q)) < 1e-9 else 1))
 
 
+EXCH_KEYS = ("halo_rho", "halo_phibar", "carry_planes", "carry_long", "allreduce",
+             "exposed_halo_rho", "exposed_halo_phibar", "exposed_carry_planes")
+KERNEL_CLASSES = ("residual", "precond", "update", "dual")
+
+
+def scale_report(dist, backend, el_s, iters, kern, exch):
+    """The N > 1 line's self-check (a collective: every rank calls it).  Gathers each rank's wall time, kernel time
+    per class and exchange / exposed-wait times (SlabRunner.exchange_times(), ms per iteration) to every rank, so the
+    driver's first multi-GPU run can be read against the cost model of DESIGN.md section 7: per rank, step ms =
+    kernel ms + exposed exchange ms + launch gaps.  Returns the report (identical on every rank)."""
+    import torch
+    world = dist.get_world_size()
+    n = max(iters, 1)
+    row = [el_s * 1e3 / n] + [kern.get(c, {}).get("avg_ms", 0.0) * kern.get(c, {}).get("launches", 0) / n
+                              for c in KERNEL_CLASSES] + [float((exch or {}).get(c, 0.0)) for c in EXCH_KEYS]
+    dev = "cuda" if backend == "nccl" else "cpu"
+    mine = torch.tensor(row, dtype=torch.float64, device=dev)
+    allr = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    tab = np.array([t.cpu().numpy() for t in allr])
+    step = tab[:, 0]
+    kms = tab[:, 1:1 + len(KERNEL_CLASSES)]
+    ex = tab[:, 1 + len(KERNEL_CLASSES):]
+    exposed = ex[:, [EXCH_KEYS.index(c) for c in EXCH_KEYS if c.startswith("exposed_")]].sum(axis=1)
+    return {"world_size_reported": world, "backend": backend,
+            "ms_per_step_by_rank": step.tolist(), "ms_per_step_max": float(step.max()),
+            "slowest_rank": int(step.argmax()),
+            "kernel_ms_per_step_by_rank": {c: kms[:, i].tolist() for i, c in enumerate(KERNEL_CLASSES)},
+            "exchange_ms_per_step_by_rank": {c: ex[:, i].tolist() for i, c in enumerate(EXCH_KEYS)},
+            "exposed_exchange_ms_by_rank": exposed.tolist(),
+            # what the kernels + exposed waits do not explain: launch / event gaps and host stalls
+            "unexplained_ms_by_rank": (step - kms.sum(axis=1) - exposed).tolist()}
+
+
 def _free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
@@ -607,6 +641,10 @@ def main():
     it_bytes_hbm = it_bytes + ctx.algorithmic_bytes(k, "dual") * world * (dual_pass - k) if (k > 1 and "passes" in
                                                                                            kern.get("dual", {})) else it_bytes
     ms_per_step = el_max / max(iters, 1) * 1e3
+    report = None
+    if dist is not None:   # every rank: collective
+        report = scale_report(dist, backend, el, iters, kern,
+                              {c: v / max(iters, 1) for c, v in (exch or {}).items()})
     if exch is not None:
         exch = {c: max_over_ranks(v) / max(iters, 1) for c, v in sorted(exch.items())}
 
@@ -652,6 +690,7 @@ def main():
     if world > 1:
         out["world"] = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
                         "dominant_kernel_ms_max_over_ranks": dom_ms_max}
+        out["scale_check"] = report
     if runner is not None:
         from pdhg_amd.slab import slab_bounds
         out["slab"] = {"rows_per_slab": [j1 - j0 for j0, j1 in slab_bounds(T, world)],

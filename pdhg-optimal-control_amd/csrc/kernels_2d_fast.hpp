@@ -497,10 +497,18 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<R> p, const cplx<R>
     if constexpr (RSPLIT < RW) load_rows(nxt, RSPLIT, RW);
     load_edges(nxt);
     R* wk = p.work + (size_t)j * nb * nx * B;
-    if (p.rspec) {   // task order (tc_spec): one contiguous run per task
+    if (p.rspec) {   // task order (tc_spec; C4's to_c4): one contiguous run per task
       R* wt = p.rspec + (size_t)j * nb * nx * B + (size_t)x0 * nb * B;
-      for (int t = tid; t < nb * CS4; t += NT)
-        st4(wt + 4 * t, unpack_chunk4<N, LN, R>(A, t >> lCS4, t & (CS4 - 1), B, p.lB));
+      if (RW * B < 4) {   // RW = 2, B = 1 (fp64 C4): element b = rows x0, x0+1 at ky = b, 16 B, consecutive in b
+        for (int b = tid; b < nb; b += NT) {
+          R ha, hb;
+          hartley_padded<C, R>(A, N, b, ha, hb);
+          *reinterpret_cast<C*>(wt + 2 * (size_t)b) = cmk<C>(ha, hb);
+        }
+      } else {
+        for (int t = tid; t < nb * CS4; t += NT)
+          st4(wt + 4 * t, unpack_chunk4<N, LN, R>(A, t >> lCS4, t & (CS4 - 1), B, p.lB));
+      }
     } else if (RW * B < 4) {   // RW = 2, B = 1 (fp64 C4): chunk b = rows x0, x0+1 at ky = b, one 16-B store
       for (int b = tid; b < nb; b += NT) {
         R ha, hb;
@@ -517,6 +525,35 @@ __global__ void __launch_bounds__(NT) k_res_fwdy_fused_2d(KP<R> p, const cplx<R>
     }
     lds_sync();
   }
+}
+
+// C4's task-order spectrum (to_c4) into the x kernel's blocked layout.  With half-real x blocks (B = 1) a blocked
+// chunk is one row task's RW values at one ky: 16 B (fp64 RW = 2, fp32 RW = 4), so the fused residual writing the
+// blocked layout directly stores 16 B per 64-KiB stride (round 5: fp64 c4w50 residual 55-60 ms for 61 GB, PMC 1.5x).
+// It now stores each task's spectrum as one contiguous run, [row j][task xq][ky] of 16-B elements, and this kernel
+// transposes every row's [XQ][NK] element matrix into [NK][XQ] (the blocked [j][b = ky][x]): 32 x 64 element tiles
+// through LDS, 1-KiB contiguous reads (a wave = one task row of 64 ky) and 512-B contiguous writes (32 tasks of one
+// ky).  2N reals of extra traffic (one read + one write of the spectrum) for full-line accesses on both sides.
+// grid (NK/64, XQ/32, row_cnt); block 256; rows [row_base, row_base + row_cnt).
+template <typename R>
+__global__ void __launch_bounds__(256) k_res_fwdy_fused_transpose_2d(KP<R> p, int XQ, int NK) {
+  if (p.ctrl->done) return;
+  __shared__ uint4 tile[32][65];
+  const int k0 = blockIdx.x * 64, q0 = blockIdx.y * 32;
+  const size_t rowsz = (size_t)XQ * NK;
+  const size_t j = (size_t)p.row_base + blockIdx.z;
+  const uint4* in = reinterpret_cast<const uint4*>(p.rspec) + j * rowsz;
+  uint4* out = reinterpret_cast<uint4*>(p.work) + j * rowsz;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint4 v[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) v[r] = in[(size_t)(q0 + w + 4 * r) * NK + k0 + lane];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) tile[w + 4 * r][lane] = v[r];
+  __syncthreads();
+  const int q = threadIdx.x & 31, kb = threadIdx.x >> 5;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) out[(size_t)(k0 + kb + 8 * r) * XQ + q0 + q] = tile[q][kb + 8 * r];
 }
 
 // G workgroups striding over the T * nx/RW row-group tasks; block NT; LDS RW/2 * (N + N/16) * 8 B.

@@ -182,6 +182,7 @@ struct Impl : ImplBase {
   bool res64 = false;      // fp64 residual and update through the fast row kernels (4-row groups)
   bool upd8192 = false;    // fp64 ny = 8192, half-real x: update through the fast row kernel on 2-row tasks
   bool tc_spec = false;    // fp64 C3: residual spectrum in task order (KP::rspec)
+  bool to_c4 = false;      // C4 (half-real x blocks): fused residual in task order + k_res_fwdy_fused_transpose_2d
   size_t lds_res64 = 0, lds_upd64 = 0;
   size_t partial_rows = 0;
   static constexpr int kFoldRows = 64;   // rows of the first fold level (k_fold_partials) after the table
@@ -309,7 +310,9 @@ struct Impl : ImplBase {
       if (B > nyp) B = nyp;
       // fp64 nx = 512 / 1024 with T > 1: one column pair per block (B = 2) for the fp64 x kernel below (the generic
       // kernel would take B = 8 / 4 with its carries in global memory); T = 1 keeps the one-row kernel's B
-      const bool f64_small = sizeof(R) == 8 && pb.bc_x == 0 && T > 1 && (nxg == 1024 || nxg == 512) &&
+      // (a t-slab takes the window's row count, so every slab of one window gets the same layout: a 1-row slab of a
+      // longer window must not keep B = 8 / 4 while its neighbours exchange B = 2 carry planes)
+      const bool f64_small = sizeof(R) == 8 && pb.bc_x == 0 && (slab ? slab_Tg : T) > 1 && (nxg == 1024 || nxg == 512) &&
                              ny % 2 == 0 && [] { const char* e = getenv("PDHG_XT64"); return !e || atoi(e) != 0; }();
       if (f64_small) B = 2;
       // fp32 nx = 8192 (C4): one real column per block, packed into a 4096-point FFT (half_real)
@@ -476,7 +479,9 @@ struct Impl : ImplBase {
       // 4-row task instead of 64-B chunks of the blocked layout), the x kernel's forward sweep reading it
       // Interleaved A/B (round 5): C3's T = 200 118.8 -> 118.3 ms; its 25-row slab share (8 GPUs) 16.05 -> 16.35 ms
       // (the x kernel's 64-B reads cost relatively more on short windows), so windows of >= 100 rows only
-      const bool tc_ok = sizeof(R) == 8 && res64 && ny == 4096 && f64_xt && !half_real && nxg == 4096 && B == 2 && !xslab;
+      // (never on one-row windows: the T = 1 x kernel reads the blocked work buffer)
+      const bool tc_ok = sizeof(R) == 8 && res64 && ny == 4096 && f64_xt && !half_real && nxg == 4096 && B == 2 &&
+                         !xslab && T > 1 && !t1_xt64;
       tc_spec = tc_ok && T >= 100;
       if (const char* e = getenv("PDHG_TC_SPEC")) tc_spec = tc_ok && atoi(e) != 0;   // A/B: 0 blocked, 1 task order
       // fused residual: fp32 fast kernels with 8-row tiles on both sides, rho_alp_iters = 1 (in place),
@@ -506,6 +511,11 @@ struct Impl : ImplBase {
           gzd = 1;
         }
       }
+      // C4 (ny = 8192 with half-real x blocks, B = 1): the fused residual's task-order spectrum + a transpose into the
+      // blocked layout instead of 16-B chunk stores (fp64 RW = 2 / fp32 RW = 4 tasks: 16-B elements)
+      to_c4 = fuse_res && half_real && B == 1 && ny == 8192 && !xslab &&
+              (sizeof(R) == 8 ? ip_rows : (fast_rows && RWf == 4)) && (nx % (sizeof(R) == 8 ? 64 : 128)) == 0;
+      if (const char* e = getenv("PDHG_C4_TO")) to_c4 = to_c4 && atoi(e) != 0;   // A/B: 0 = blocked 16-B chunks
     } else {
       p.B = 1;
       p.lB = 0;
@@ -830,6 +840,94 @@ struct Impl : ImplBase {
     }
   };
 
+  // the fused residual kernel over time rows [lo, hi) (launch_residual's fused branch)
+  int launch_fused_residual(KP<R> p, int lo, int hi) {
+    int rc = PDHG_OK;
+    if constexpr (sizeof(R) == 8) {
+      auto go = [&](auto Nc) {
+        constexpr int N_ = decltype(Nc)::value;
+        const dim3 g(std::min((pb.nx / 4) * (hi - lo), n_cu));   // persistent, one workgroup per CU (LDS)
+        int r2;
+        if constexpr (N_ == 4096) {
+          if (res64_nt == 1024) {   // A/B: 16 waves per CU (GPT = 1)
+            if (pb.egno == 1) {
+              if ((r2 = ensure_lds(k_res_fwdy_fused_2d<1, N_, 4, 1024, double>, lds_upd64))) return r2;
+              hipLaunchKernelGGL((k_res_fwdy_fused_2d<1, N_, 4, 1024, double>), g, dim3(1024), lds_upd64, stream, p, twy);
+            } else {
+              if ((r2 = ensure_lds(k_res_fwdy_fused_2d<2, N_, 4, 1024, double>, lds_upd64))) return r2;
+              hipLaunchKernelGGL((k_res_fwdy_fused_2d<2, N_, 4, 1024, double>), g, dim3(1024), lds_upd64, stream, p, twy);
+            }
+            return (int)PDHG_OK;
+          }
+        }
+        if (pb.egno == 1) {
+          if ((r2 = ensure_lds(k_res_fwdy_fused_2d<1, N_, 4, 512, double>, lds_upd64))) return r2;
+          hipLaunchKernelGGL((k_res_fwdy_fused_2d<1, N_, 4, 512, double>), g, dim3(512), lds_upd64, stream, p, twy);
+        } else {
+          if ((r2 = ensure_lds(k_res_fwdy_fused_2d<2, N_, 4, 512, double>, lds_upd64))) return r2;
+          hipLaunchKernelGGL((k_res_fwdy_fused_2d<2, N_, 4, 512, double>), g, dim3(512), lds_upd64, stream, p, twy);
+        }
+        return (int)PDHG_OK;
+      };
+      if (pb.ny == 8192) {   // quarter-tile tasks: one padded line of 8192 complex doubles (+ the strip-edge terms)
+        const dim3 g(std::min((pb.nx / 2) * (hi - lo), n_cu));
+        const size_t lds = (size_t)Pad<8192>::LINE * sizeof(C);
+        if (pb.egno == 1) {
+          if ((rc = ensure_lds(k_res_fwdy_fused_2d<1, 8192, 2, 512, double>, lds))) return rc;
+          hipLaunchKernelGGL((k_res_fwdy_fused_2d<1, 8192, 2, 512, double>), g, dim3(512), lds, stream, p, twy);
+        } else {
+          if ((rc = ensure_lds(k_res_fwdy_fused_2d<2, 8192, 2, 512, double>, lds))) return rc;
+          hipLaunchKernelGGL((k_res_fwdy_fused_2d<2, 8192, 2, 512, double>), g, dim3(512), lds, stream, p, twy);
+        }
+      } else {
+        rc = pb.ny == 4096 ? go(std::integral_constant<int, 4096>{}) : go(std::integral_constant<int, 2048>{});
+      }
+      if (rc) return rc;
+      HIP_TRY(hipGetLastError());
+      return PDHG_OK;
+    }
+    rc = with_fast_rows([&](auto Nc, auto RWc, auto NTc) {
+      constexpr int N_ = decltype(Nc)::value, RW_ = decltype(RWc)::value, NT_ = decltype(NTc)::value;
+      int r2;
+      if constexpr (sizeof(R) == 4 && (RW_ == 8 || (RW_ == 4 && N_ == 8192)) && N_ % 256 == 0 &&
+                    (N_ / 4) % NT_ == 0) {
+        const dim3 g(std::min((pb.nx / RW_) * (hi - lo), n_cu));   // persistent, one workgroup per CU (LDS)
+        auto go = [&](auto ntc) {
+          constexpr int NTF = decltype(ntc)::value;
+          int r3;
+          if (pb.egno == 1) {
+            if ((r3 = ensure_lds(k_res_fwdy_fused_2d<1, N_, RW_, NTF>, lds_fast_tw))) return r3;
+            hipLaunchKernelGGL((k_res_fwdy_fused_2d<1, N_, RW_, NTF>), g, dim3(NTF), lds_fast_tw, stream, p, twy);
+          } else {
+            if ((r3 = ensure_lds(k_res_fwdy_fused_2d<2, N_, RW_, NTF>, lds_fast_tw))) return r3;
+            hipLaunchKernelGGL((k_res_fwdy_fused_2d<2, N_, RW_, NTF>), g, dim3(NTF), lds_fast_tw, stream, p, twy);
+          }
+          return (int)PDHG_OK;
+        };
+        if constexpr (NT_ == 1024) {
+          if (half_nt & 1) return go(std::integral_constant<int, 512>{});
+        }
+        return go(std::integral_constant<int, NT_>{});
+      }
+      return fail(PDHG_ERR_STATE, "fused residual without 8-row fast kernels (ny=%d)", pb.ny);
+    });
+    if (rc) return rc;
+    HIP_TRY(hipGetLastError());
+    return PDHG_OK;
+  }
+
+  // C4's task-order residual spectrum (p.rspec) of time rows [lo, hi) into the blocked layout of `work`
+  int launch_spec_to_blocked(const KP<R>& p, int lo, int hi) {
+    const int RWt = sizeof(R) == 8 ? 2 : 4, XQ = pb.nx / RWt, NK = p.nb;   // 16-B elements: RWt reals
+    if (XQ % 32 || NK % 64) return fail(PDHG_ERR_STATE, "task-order transpose needs nx/%d %% 32 == 0", RWt);
+    KP<R> q = p;
+    q.row_base = lo;
+    hipLaunchKernelGGL(k_res_fwdy_fused_transpose_2d<R>, dim3(NK / 64, XQ / 32, hi - lo), dim3(256), 0, stream, q,
+                       XQ, NK);
+    HIP_TRY(hipGetLastError());
+    return PDHG_OK;
+  }
+
   // residual + forward y transform over time rows [lo, hi) (2-D).  The generic kernels only run the
   // whole window (lo = 0, hi = T).
   int launch_residual(KP<R> p, int lo, int hi) {
@@ -837,78 +935,18 @@ struct Impl : ImplBase {
     int rc = PDHG_OK;
     if (fuse_res && res_valid && (slab || (lo == 0 && hi == pb.T))) {
       ProfScope ps(this, "residual");
+      // C4 (half-real x blocks, B = 1): the fused residual stores its spectrum in task order over the R rows it was
+      // formed from (full 128-B lines instead of 16-B chunks of the blocked layout), and k_spec_to_blocked_2d
+      // transposes it into the x kernel's blocked layout
+      if (to_c4) p.rspec = p.res;
+      // the task-order spectrum is stored over the R rows it was formed from (p.rspec == p.res): once the launch
+      // that ends the window has run, R is gone until the next fused dual sweep forms it again
+      if (p.rspec != nullptr && p.rspec == p.res && hi == pb.T) res_valid = false;
       p.row_base = lo;
       p.row_cnt = hi - lo;
-      if constexpr (sizeof(R) == 8) {
-        auto go = [&](auto Nc) {
-          constexpr int N_ = decltype(Nc)::value;
-          const dim3 g(std::min((pb.nx / 4) * (hi - lo), n_cu));   // persistent, one workgroup per CU (LDS)
-          int r2;
-          if constexpr (N_ == 4096) {
-            if (res64_nt == 1024) {   // A/B: 16 waves per CU (GPT = 1)
-              if (pb.egno == 1) {
-                if ((r2 = ensure_lds(k_res_fwdy_fused_2d<1, N_, 4, 1024, double>, lds_upd64))) return r2;
-                hipLaunchKernelGGL((k_res_fwdy_fused_2d<1, N_, 4, 1024, double>), g, dim3(1024), lds_upd64, stream, p, twy);
-              } else {
-                if ((r2 = ensure_lds(k_res_fwdy_fused_2d<2, N_, 4, 1024, double>, lds_upd64))) return r2;
-                hipLaunchKernelGGL((k_res_fwdy_fused_2d<2, N_, 4, 1024, double>), g, dim3(1024), lds_upd64, stream, p, twy);
-              }
-              return (int)PDHG_OK;
-            }
-          }
-          if (pb.egno == 1) {
-            if ((r2 = ensure_lds(k_res_fwdy_fused_2d<1, N_, 4, 512, double>, lds_upd64))) return r2;
-            hipLaunchKernelGGL((k_res_fwdy_fused_2d<1, N_, 4, 512, double>), g, dim3(512), lds_upd64, stream, p, twy);
-          } else {
-            if ((r2 = ensure_lds(k_res_fwdy_fused_2d<2, N_, 4, 512, double>, lds_upd64))) return r2;
-            hipLaunchKernelGGL((k_res_fwdy_fused_2d<2, N_, 4, 512, double>), g, dim3(512), lds_upd64, stream, p, twy);
-          }
-          return (int)PDHG_OK;
-        };
-        if (pb.ny == 8192) {   // quarter-tile tasks: one padded line of 8192 complex doubles (+ the strip-edge terms)
-          const dim3 g(std::min((pb.nx / 2) * (hi - lo), n_cu));
-          const size_t lds = (size_t)Pad<8192>::LINE * sizeof(C);
-          if (pb.egno == 1) {
-            if ((rc = ensure_lds(k_res_fwdy_fused_2d<1, 8192, 2, 512, double>, lds))) return rc;
-            hipLaunchKernelGGL((k_res_fwdy_fused_2d<1, 8192, 2, 512, double>), g, dim3(512), lds, stream, p, twy);
-          } else {
-            if ((rc = ensure_lds(k_res_fwdy_fused_2d<2, 8192, 2, 512, double>, lds))) return rc;
-            hipLaunchKernelGGL((k_res_fwdy_fused_2d<2, 8192, 2, 512, double>), g, dim3(512), lds, stream, p, twy);
-          }
-        } else {
-          rc = pb.ny == 4096 ? go(std::integral_constant<int, 4096>{}) : go(std::integral_constant<int, 2048>{});
-        }
-        if (rc) return rc;
-        HIP_TRY(hipGetLastError());
-        return PDHG_OK;
-      }
-      rc = with_fast_rows([&](auto Nc, auto RWc, auto NTc) {
-        constexpr int N_ = decltype(Nc)::value, RW_ = decltype(RWc)::value, NT_ = decltype(NTc)::value;
-        int r2;
-        if constexpr (sizeof(R) == 4 && (RW_ == 8 || (RW_ == 4 && N_ == 8192)) && N_ % 256 == 0 &&
-                      (N_ / 4) % NT_ == 0) {
-          const dim3 g(std::min((pb.nx / RW_) * (hi - lo), n_cu));   // persistent, one workgroup per CU (LDS)
-          auto go = [&](auto ntc) {
-            constexpr int NTF = decltype(ntc)::value;
-            int r3;
-            if (pb.egno == 1) {
-              if ((r3 = ensure_lds(k_res_fwdy_fused_2d<1, N_, RW_, NTF>, lds_fast_tw))) return r3;
-              hipLaunchKernelGGL((k_res_fwdy_fused_2d<1, N_, RW_, NTF>), g, dim3(NTF), lds_fast_tw, stream, p, twy);
-            } else {
-              if ((r3 = ensure_lds(k_res_fwdy_fused_2d<2, N_, RW_, NTF>, lds_fast_tw))) return r3;
-              hipLaunchKernelGGL((k_res_fwdy_fused_2d<2, N_, RW_, NTF>), g, dim3(NTF), lds_fast_tw, stream, p, twy);
-            }
-            return (int)PDHG_OK;
-          };
-          if constexpr (NT_ == 1024) {
-            if (half_nt & 1) return go(std::integral_constant<int, 512>{});
-          }
-          return go(std::integral_constant<int, NT_>{});
-        }
-        return fail(PDHG_ERR_STATE, "fused residual without 8-row fast kernels (ny=%d)", pb.ny);
-      });
-      if (rc) return rc;
+      if ((rc = launch_fused_residual(p, lo, hi))) return rc;
       HIP_TRY(hipGetLastError());
+      if (to_c4) return launch_spec_to_blocked(p, lo, hi);
       return PDHG_OK;
     }
     if constexpr (sizeof(R) == 8) {
@@ -2496,9 +2534,10 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
     else if (k == "half_real") *value = im.half_real ? 1 : 0;
     else if (k == "fourstep") *value = im.fourstep ? 1 : 0;
     else if (k == "glb_line") *value = im.glb_line ? 1 : 0;
-    else if (k == "ip_rows") *value = im.ip_rows ? 1 : 0;
+    else if (k == "ip_rows") *value = im.ip_rows ? 1 : 0;   // fp64 ny = 8192 row pairs in one padded line
     else if (k == "upd8192") *value = im.upd8192 ? 1 : 0;   // fp64 ny = 8192: 2-row fast update
-    else if (k == "tc_spec") *value = im.tc_spec ? 1 : 0;   // fp64 C3: task-order residual spectrum   // fp64 ny = 8192 row pairs in one padded line
+    else if (k == "tc_spec") *value = im.tc_spec ? 1 : 0;   // fp64 C3: task-order residual spectrum
+    else if (k == "to_c4") *value = im.to_c4 ? 1 : 0;       // C4: task-order residual spectrum + transpose
     else if (k == "thomas_chunk") *value = im.thomas_chunk ? 1 : 0;
     else if (k == "fs_wide") *value = (im.fourstep && im.fs_wide && !im.fs16) ? 1 : 0;
     else if (k == "fs16") *value = im.fs16 ? 1 : 0;

@@ -361,7 +361,8 @@ class SlabRunner:
 
     def exchange_times(self, reset=True):
         """{category: total ms} of the exchanges since timing was switched on (halo_rho, halo_phibar,
-        carry_planes, carry_long, allreduce); side-stream exchanges overlap the kernels of the main stream."""
+        carry_planes, carry_long, allreduce); side-stream exchanges overlap the kernels of the main stream, and
+        exposed_<cat> is the time the main stream waited for them (halo_rho, halo_phibar, carry_planes)."""
         self.torch.cuda.synchronize()
         out = {c: sum(a.elapsed_time(b) for a, b in evs) for c, evs in self._tev.items()}
         if reset:
@@ -379,9 +380,17 @@ class SlabRunner:
         with torch.cuda.stream(self.side):
             self._timed(cat, lambda: shift(*planes), self.side)
 
-    def _join(self):
-        if self.side is not None:
-            self.torch.cuda.current_stream().wait_stream(self.side)
+    def _join(self, cat=None):
+        """Main stream waits for the side stream.  With timing on, events on the main stream either side of the
+        wait measure how long the kernels stood still for the exchange: the exposed part of `cat`
+        (exchange_times() key "exposed_<cat>")."""
+        if self.side is None:
+            return
+        main = self.torch.cuda.current_stream()
+        if cat is not None and self.timing:
+            self._timed("exposed_" + cat, lambda: main.wait_stream(self.side), main)
+        else:
+            main.wait_stream(self.side)
 
     def step(self, tau, sigma, eps, k):
         S, B, C = self.slabs, self.b, self.comm
@@ -392,7 +401,7 @@ class SlabRunner:
         self._halo(C.shift_up, [b["rho_send"] for b in B], [b["rho_recv"] for b in B], cat="halo_rho")
         for s in S:
             s.residual(INTERIOR)
-        self._join()
+        self._join("halo_rho")
         for s, b in zip(S, B):
             if not s.last:
                 s.plane_in(RHO_HALO, b["rho_recv"])
@@ -412,7 +421,7 @@ class SlabRunner:
             self._halo(C.shift_both, [b["DS"][:spec] for b in B], [b["Dl"] for b in B],
                        [b["DS"][spec:] for b in B], [b["S1r"] for b in B], cat="carry_planes")
             allLong = self._timed("carry_long", lambda: C.allgather([b["LONG"] for b in B]))
-            self._join()
+            self._join("carry_planes")
             for i, s in enumerate(S):
                 s.fixup_nb(B[i]["Dl"], B[i]["S1r"], allLong[i], self.allGS[i])
                 s.backward(tau, B[i]["sums"])
@@ -443,8 +452,12 @@ class SlabRunner:
         for s, b in zip(S, B):
             s.plane_out(CARRY_LONG, b["LONG"])
         allLong = self._timed("carry_long", lambda: C.allgather([b["LONG"] for b in B]))
+        main = torch.cuda.current_stream()
         for q in range(self.parts):
-            torch.cuda.current_stream().wait_event(done[q])
+            if self.timing:
+                self._timed("exposed_carry_planes", lambda: main.wait_event(done[q]), main)
+            else:
+                main.wait_event(done[q])
             for i, s in enumerate(S):
                 s.fixup_nb_part(B[i]["Dl"], B[i]["S1r"], allLong[i], self.allGS[i], q, self.parts)
                 s.backward_part(tau, q, self.parts)
@@ -466,7 +479,7 @@ class SlabRunner:
             for s, b in zip(S, B):
                 s.dual(sigma, k, sub, b["sums"], INTERIOR if sub == 0 else INTERIOR | EDGE)
             if sub == 0:
-                self._join()
+                self._join("halo_phibar")
                 for s, b in zip(S, B):
                     if s.rank > 0:
                         s.plane_in(PHIBAR_ROW0, b["pb_recv"])

@@ -101,16 +101,23 @@ class Iteration2:
         W = (c_on_rho - r) / dt           # the last row's extra term
         Q = R1[-1] - W                    # an interior row (rho_{j+1} = rho_j)
         del R1
-        self.Qh = sfft.fft2(Q, workers=_W)
-        self.Wh = sfft.fft2(W, workers=_W)
-        self.dd = (C - np.asarray(P["fv"]).real) * dt * dt
+        # Q, W real and the symbol even in both axes: the half spectrum (rfft2 / irfft2) carries every mode
+        self.Qh = sfft.rfft2(Q, workers=_W)
+        self.Wh = sfft.rfft2(W, workers=_W)
+        self.shape = Q.shape
+        self.dd = ((C - np.asarray(P["fv"]).real) * dt * dt)[:, :Q.shape[1] // 2 + 1]
         self.dt, self.T, self.g = dt, P["T"], P["g"]
+        self._cache = {}   # the last few rows' U (phi'' and phi_bar'' of a row share it)
 
     def U(self, k):
         if k == 0:
             return np.zeros_like(self.g)
-        u1, u2 = mode_weights(self.dd, self.T, k)
-        return sfft.ifft2(self.Qh * u1 + self.Wh * u2, workers=_W).real * (self.dt * self.dt)
+        if k not in self._cache:
+            u1, u2 = mode_weights(self.dd, self.T, k)
+            if len(self._cache) >= 3:
+                self._cache.pop(next(iter(self._cache)))
+            self._cache[k] = sfft.irfft2(self.Qh * u1 + self.Wh * u2, s=self.shape, workers=_W) * (self.dt * self.dt)
+        return self._cache[k]
 
     def phi(self, k, tau):
         return self.g + tau * self.U(k)

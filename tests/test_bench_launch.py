@@ -38,6 +38,46 @@ def test_gpus_mismatch_with_launcher_env_fails():
     assert p.returncode != 0 and "WORLD_SIZE=1" in (p.stderr + p.stdout)
 
 
+def _scale_worker(rank, world, port, out_path):
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    import bench
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{}".format(port), rank=rank, world_size=world)
+    try:
+        iters = 4
+        # synthetic per-rank numbers: rank r is 1 ms slower per step, its exposed rho halo 0.1 * r ms per step
+        kern = {c: {"avg_ms": 2.0 + i, "launches": iters} for i, c in enumerate(bench.KERNEL_CLASSES)}
+        exch = {"halo_rho": 1.0, "exposed_halo_rho": 0.1 * rank, "exposed_carry_planes": 0.05, "allreduce": 0.02}
+        rep = bench.scale_report(dist, "gloo", (20.0 + rank) * iters * 1e-3, iters, kern, exch)
+        if rank == 0:
+            with open(out_path, "w") as fh:
+                json.dump(rep, fh)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_scale_report_gloo_world4(tmp_path):
+    """The N > 1 bench line's self-check keys: world size as the process group reports it, per-rank
+    step times and their max, kernel / exchange / exposed-wait times per rank, and the unexplained remainder --
+    gathered over gloo at world size 4 with synthetic per-rank numbers."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = str(tmp_path / "rep.json")
+    mp.spawn(_scale_worker, args=(4, port, out), nprocs=4, join=True)
+    with open(out) as fh:
+        rep = json.load(fh)
+    assert rep["world_size_reported"] == 4 and rep["backend"] == "gloo"
+    assert rep["ms_per_step_by_rank"] == [20.0, 21.0, 22.0, 23.0]
+    assert rep["ms_per_step_max"] == 23.0 and rep["slowest_rank"] == 3
+    assert rep["kernel_ms_per_step_by_rank"]["dual"] == [5.0] * 4        # 2 + 3 ms per launch, one launch per step
+    assert max(abs(a - 0.1 * r) for r, a in enumerate(rep["exchange_ms_per_step_by_rank"]["exposed_halo_rho"])) < 1e-12
+    assert abs(rep["exposed_exchange_ms_by_rank"][2] - 0.25) < 1e-12
+    assert abs(rep["unexplained_ms_by_rank"][3] - (23.0 - 14.0 - 0.35)) < 1e-9
+
+
 def test_dual_passes_of_the_chunked_loop():
     """The chunked dual (kernels_dual_multi.hpp) moves one sub-iteration's bytes per pass: ceil(inner / 5) chunk
     passes + the final re-run when the exit falls inside a chunk -- what bench.py prices the dual class with, so no

@@ -47,6 +47,15 @@ BOUNDS64 = {0.0: {"phi": 1e-12, "rho": 1e-12, "alp": 1e-12}, 0.1: {"phi": 1e-12,
 PATH64 = {4096: {"f64_xt": 1}, 8192: {"f64_xt": 1, "half_real": 1}}
 CASES = [(n, "fp32") for n in DECOMP] + [(n, "fp64") for n in DECOMP]
 IDS = ["{}@{}".format(n, p) for n, p in CASES]
+# The default tier runs each driver in the arithmetic it is run in (the bench's SlabRunner in fp64 at both configs'
+# own epsl = 0.1 decompositions) plus one case per other driver / precision (the multi-device context at C3 in fp32
+# and at C4 in fp64); the full cross product is the extended tier (PDHG_TESTS=full)
+KEEP = {"slabrunner": {("c3_p8_eps", "fp64"), ("c4_p8_eps", "fp64")},
+        "multi": {("c3_p8", "fp32"), ("c4_p8_eps", "fp64")}}
+
+
+def _cases(driver):
+    return [c if c in KEEP[driver] else pytest.param(*c, marks=pytest.mark.extended) for c in CASES]
 
 
 def _grid(egno, nx, ny, T, epsl):
@@ -77,7 +86,7 @@ def _check(name, got, want, st, st_ref, epsl, parity_log, driver, prec="fp32"):
     assert all(m[k] <= bounds[k] for k in m), (name, driver, m, bounds)
 
 
-@pytest.mark.parametrize("name,prec", CASES, ids=IDS)
+@pytest.mark.parametrize("name,prec", _cases("slabrunner"), ids=IDS)
 def test_slab_runner_at_config_decomposition(native, name, prec, parity_log):
     import torch
     from pdhg_amd.slab import LocalComm, SlabContext, SlabRunner, join_state
@@ -106,7 +115,7 @@ def test_slab_runner_at_config_decomposition(native, name, prec, parity_log):
     _check(name, got, want, st, st_ref, epsl, parity_log, "slabrunner", prec)
 
 
-@pytest.mark.parametrize("name,prec", CASES, ids=IDS)
+@pytest.mark.parametrize("name,prec", _cases("multi"), ids=IDS)
 def test_multi_context_at_config_decomposition(native, name, prec, parity_log):
     from pdhg_amd.multi import MultiContext
     egno, nx, ny, T, nr, epsl, n, _ = DECOMP[name]

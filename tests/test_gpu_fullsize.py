@@ -12,12 +12,9 @@ window-sized array (tests/_fullsize.py, pinned against the oracle by tests/test_
 The other parity tests run reduced grids; this one is what catches an index or offset that overflows at the
 bench's size.  Bounds: fp64 (the reference's arithmetic) 1e-10 relative L2 on phi'', 1e-8 on the update
 phi'' - g, 1e-9 on rho / alp (measured at C3: 8e-13, 1.4e-10, 4e-13).  fp32 at epsl = 0 (C3's grid): phi'' 1e-6.
-fp32 at epsl = 0 (C3's and C4's grids, the same kernels and offsets) carries the tight fp32 check.  fp32 at
-epsl = 0.1 is held only at the size that separates an indexing fault (O(1) in phi'') from the float32 limit
-DESIGN.md section 6 documents: the residual's epsl*Lap(rho) turns rho's float32 rounding into high-frequency content
-that dominates |R| while U lives in the low modes, so the float32 rounding of R bounds phi'' (measured phi'' 7.6e-5
-and update 2e-2 at C3; 2.2e-3 and 0.41 at C4, whose 1/dx^2 is 4x C3's), and sigma*epsl*Lap(phi_bar) bounds rho /
-alp (1.2e-4 / 3e-4).  The host dual steps run on two bands of
+fp32 at epsl = 0 (C3's and C4's grids, the same kernels and offsets) carries the tight fp32 check; fp32 at
+epsl = 0.1 is not run at full size (there the float32 rounding of R bounds phi'', so the bound
+could only separate an indexing fault).  The host dual steps run on two bands of
 32 x rows (x = 0.. and ..nx - 1; tests/_fullsize.py band()), the phi'' rows on whole planes.  Progress lines go to
 gpurun_out/progress.log (the checker takes a minute or two at C4's plane)."""
 import os
@@ -39,11 +36,14 @@ CASES = {
     "c4w50": (2, 8192, 8192, 50, 0.1),
     "c4w50e0": (2, 8192, 8192, 50, 0.0),
 }
-RUNS = [("c3", "fp64"), ("c4w50", "fp64"), ("c3e0", "fp32"), ("c4w50e0", "fp32"), ("c3", "fp32"), ("c4w50", "fp32")]
+# fp32 at epsl = 0.1 is not run at full size (its bounds, 1e-2 on phi'' and 1.0 on the update, say
+# nothing the epsl = 0 fp32 runs on the same kernels and offsets do not); C4's fp32 window is the extended tier
+RUNS = [("c3", "fp64"), ("c4w50", "fp64"), ("c3e0", "fp32"),
+        pytest.param("c4w50e0", "fp32", marks=pytest.mark.extended)]
+RUN_IDS = ["c3-fp64", "c4w50-fp64", "c3e0-fp32", "c4w50e0-fp32"]
 BOUNDS = {
     "fp64": {"phi": 1e-10, "dphi": 1e-8, "rho": 1e-9, "alp": 1e-9},
     ("fp32", 0.0): {"phi": 1e-6, "dphi": 1e-3, "rho": 1e-5, "alp": 1e-4},
-    ("fp32", 0.1): {"phi": 1e-2, "dphi": 1.0, "rho": 1e-3, "alp": 1e-2},
 }
 
 
@@ -71,7 +71,7 @@ def _rows(nx, ny, T, es):
     return sorted(r for r in rows if 1 <= r <= T)
 
 
-@pytest.mark.parametrize("name,prec", RUNS, ids=["{}-{}".format(*r) for r in RUNS])
+@pytest.mark.parametrize("name,prec", RUNS, ids=RUN_IDS)
 def test_full_window_first_two_iterations(native, parity_log, name, prec):
     from pdhg_amd.context import PDHGContext
     egno, nx, ny, T, epsl = CASES[name]

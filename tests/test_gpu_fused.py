@@ -47,6 +47,15 @@ FUSED64 = [
 IDS64 = ["e{}d{}_{}x{}_T{}_eps{}".format(*c) for c in FUSED64]
 
 
+def _c4_plane(T, epsl):
+    """C4's 8192^2 plane with a window of T rows, without window-sized host state: the grid and g (a one-row
+    make_problem), the reference initial state formed on the device (init_state), and a seeded rough rho (set_state)."""
+    P = make_problem(2, 2, 8192, 8192, 1, epsl, seeded=False)
+    P.update(T=T, dt=1.0 / max(T, 40), g=P["g"][0])
+    rho = 70.0 * np.random.default_rng(11).uniform(0.5, 1.5, (T, 8192, 8192))
+    return P, rho
+
+
 def _ctx(P, fuse, monkeypatch, precision="fp32"):
     monkeypatch.setenv("PDHG_FUSE_RES", "1" if fuse else "0")
     monkeypatch.setenv("PDHG_SHORT_T", "0")   # these windows are short: keep the 8-row (fusable) dual
@@ -172,7 +181,7 @@ def test_dual_neighbour_sync_bitwise(native, monkeypatch, prec, case, fuse):
     assert st1["err1"] == st0["err1"] and st1["err2"] == st0["err2"]
 
 
-@pytest.mark.parametrize("epsl,n", [(0.0, 4), (0.1, 2)])
+@pytest.mark.parametrize("epsl,n", [pytest.param(0.0, 4, marks=pytest.mark.extended), (0.1, 2)])
 def test_fused_fp64_c4_plane(native, monkeypatch, epsl, n):
     """C4's 8192^2 plane in fp64 (T = 3): the half-real x blocks (B = 1), so every fused-residual chunk is the two
     rows of a task at one ky (a 16-B store) -- against the unfused fp64 kernels (ip_rows): phi, rho within 1e-12.
@@ -190,19 +199,44 @@ def test_fp64_update_c4_plane_fast_vs_generic(native, monkeypatch):
     """fp64 at C4's 8192^2 plane: the inverse DHT_y + update through the fast row kernel on 2-row tasks
     (k_invy_update_fast_2d<8192, 2, ..., double>, 16-B chunks of the half-real spectrum) against the generic row-pair
     kernel (PDHG_UPD8192=0): the same float64 arithmetic up to the transform's association, 1e-12 after 3 iterations."""
-    P = make_problem(2, 2, 8192, 8192, 3, 0.0)
+    P, rho = _c4_plane(3, 0.0)
     out = []
     for flag in ("1", "0"):
         monkeypatch.setenv("PDHG_UPD8192", flag)
         ctx = device_ctx(P, "fp64")
         try:
             assert ctx.path_info("upd8192") == int(flag) and ctx.path_info("half_real") == 1
-            ctx.set_state(P["phi"], P["rho"], P["alp"])
+            ctx.init_state(P["g"])
+            ctx.set_state(rho=rho)
             st = ctx.iterate(3, TAU, SIGMA, -1.0, 1)
-            out.append((ctx.get_state(), st))
+            out.append((ctx.get_state(alp=False), st))
         finally:
             ctx.close()
     (s1, st1), (s0, st0) = out
-    for a, b in zip((s1[0], s1[1]) + tuple(s1[2]), (s0[0], s0[1]) + tuple(s0[2])):
-        assert rel(a, b) < 1e-12
+    assert rel(s1[0], s0[0]) < 1e-12 and rel(s1[1], s0[1]) < 1e-12
     assert abs(st1["err1"] - st0["err1"]) <= 1e-10 * st0["err1"]
+    assert abs(st1["err2"] - st0["err2"]) <= 1e-10 * st0["err2"]   # err2 sums the controls' changes too
+
+
+@pytest.mark.parametrize("prec", ["fp64", "fp32"])
+def test_c4_task_order_spectrum_bitwise(native, monkeypatch, prec):
+    """C4's 8192^2 plane (half-real x blocks, B = 1): the fused residual's spectrum in task order + the LDS-tiled
+    transpose into the blocked layout (to_c4, k_res_fwdy_fused_transpose_2d) against the fused residual's direct
+    16-B chunk stores (PDHG_C4_TO=0): the same values moved another way, so the states agree bit for bit."""
+    P, rho = _c4_plane(3, 0.1)
+    out = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("PDHG_C4_TO", flag)
+        ctx = _ctx(P, True, monkeypatch, prec)
+        try:
+            assert ctx.path_info("to_c4") == int(flag) and ctx.path_info("half_real") == 1
+            ctx.init_state(P["g"])
+            ctx.set_state(rho=rho)
+            st = ctx.iterate(3, TAU, SIGMA, -1.0, 1)
+            out.append((ctx.get_state(alp=False), st))
+        finally:
+            ctx.close()
+    (s1, st1), (s0, st0) = out
+    assert np.array_equal(s1[0], s0[0]) and np.array_equal(s1[1], s0[1])
+    # err1 / err2 sum every state array (the controls included): equal sums, bit for bit
+    assert st1["err1"] == st0["err1"] and st1["err2"] == st0["err2"]

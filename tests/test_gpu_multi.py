@@ -21,9 +21,14 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("fold", ["1", "0"], ids=["peer_fold", "gather_fold"])
-@pytest.mark.parametrize("egno,nx,ny,T,nr,k", CASES, ids=[f"e{c[0]}_{c[1]}x{c[2]}_T{c[3]}_P{c[4]}_k{c[5]}"
-                                                         for c in CASES])
+# the peer-pointer fold (opt-in, PDHG_MULTI_PEER_FOLD=1) on the first case by default, on all in the extended tier
+PARAMS = [pytest.param(*c, f, marks=() if (f == "0" or i == 0) else (pytest.mark.extended,))
+          for i, c in enumerate(CASES) for f in ("1", "0")]
+IDS = [f"e{c[0]}_{c[1]}x{c[2]}_T{c[3]}_P{c[4]}_k{c[5]}-{'peer' if f == '1' else 'gather'}_fold"
+       for c in CASES for f in ("1", "0")]
+
+
+@pytest.mark.parametrize("egno,nx,ny,T,nr,k,fold", PARAMS, ids=IDS)
 def test_multi_matches_single_context(native, egno, nx, ny, T, nr, k, fold, monkeypatch):
     """fold 1: every slab folds the P sum vectors itself from their owners' buffers (peer pointers; on one GPU
     local ones), alternating contribution buffers; fold 0: gather on slab 0, fold, copy back."""

@@ -40,10 +40,18 @@ def _slabs(P, nranks, k):
                         epsl=P["epsl"], rho_alp_iters=k) for r in range(nranks)]
 
 
-@pytest.mark.parametrize("overlap,exchange", [(True, "neighbour"), (False, "neighbour"), (True, "allgather")],
-                         ids=["overlap-nb", "serial-nb", "overlap-ag"])
-@pytest.mark.parametrize("egno,nx,ny,T,nr,k", CASES, ids=[f"e{c[0]}_{c[1]}x{c[2]}_T{c[3]}_P{c[4]}_k{c[5]}"
-                                                         for c in CASES])
+MODES = [(True, "neighbour", "overlap-nb"), (False, "neighbour", "serial-nb"), (True, "allgather", "overlap-ag")]
+# every case in the bench's schedule (overlapped halos, neighbour carries); the serial and allgather schedules on
+# the first case only by default, on every case in the extended tier (PDHG_TESTS=full)
+PARAMS, PARAM_IDS = [], []
+for ci, c in enumerate(CASES):
+    for ov, ex, mid in MODES:
+        marks = () if (mid == "overlap-nb" or ci == 0) else (pytest.mark.extended,)
+        PARAMS.append(pytest.param(*c, ov, ex, marks=marks))
+        PARAM_IDS.append(f"e{c[0]}_{c[1]}x{c[2]}_T{c[3]}_P{c[4]}_k{c[5]}-{mid}")
+
+
+@pytest.mark.parametrize("egno,nx,ny,T,nr,k,overlap,exchange", PARAMS, ids=PARAM_IDS)
 def test_slabs_match_single_context(native, egno, nx, ny, T, nr, k, overlap, exchange):
     import torch
     from pdhg_amd.context import PDHGContext
@@ -85,6 +93,7 @@ def test_slabs_match_single_context(native, egno, nx, ny, T, nr, k, overlap, exc
     ref.close()
 
 
+@pytest.mark.extended
 @pytest.mark.parametrize("env,path", [({"PDHG_XT_BATCH": "0"}, 2), ({"PDHG_XT_BATCH": "1", "PDHG_XT_DMA": "0"}, 3)],
                          ids=["ws", "batched"])
 def test_ws_slabs(native, monkeypatch, env, path):

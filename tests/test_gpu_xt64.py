@@ -40,7 +40,7 @@ def test_fp64_x_kernel(native, monkeypatch, parity_log, egno, nx, ny, T):
     assert all(m[k] <= b[k] for k in m), m
 
 
-@pytest.mark.parametrize("fuse", ["1", "0"], ids=["fused", "unfused"])
+@pytest.mark.parametrize("fuse", ["1", pytest.param("0", marks=pytest.mark.extended)], ids=["fused", "unfused"])
 def test_fp64_task_order_spectrum(native, monkeypatch, parity_log, fuse):
     """fp64 at C3's extents (4096^2): the residual spectrum handed to the x transform in task order (PDHG_TC_SPEC,
     one contiguous run per 4-row task; the x kernel's forward sweep reads 64-B groups) against the blocked layout --
@@ -66,3 +66,29 @@ def test_fp64_task_order_spectrum(native, monkeypatch, parity_log, fuse):
          "bitwise": float(np.array_equal(s1[0], s0[0]) and np.array_equal(s1[1], s0[1]))}
     parity_log("test_fp64_task_order_spectrum", "c3_4096x4096_T6_fuse" + fuse, m, {k: 1e-13 for k in m if k != "bitwise"})
     assert all(m[k] <= 1e-13 for k in m if k != "bitwise"), m
+
+
+def test_fp64_task_order_spectrum_primal_twice(native, monkeypatch, parity_log):
+    """Drop-in pairing the loop never makes: two update_primal calls in a row after a fused dual sweep.  With the
+    task-order spectrum stored over the R plane (tc_spec + fused residual) the first primal consumes R, so the
+    second must re-form the residual from (rho, alp) instead of reading the spectrum as R; against the
+    blocked layout, whose R survives the first call, on the same sequence (1e-12: fused vs unfused residual)."""
+    monkeypatch.setenv("PDHG_FUSE_RES", "1")
+    P = make_problem(2, 2, 4096, 4096, 4, 0.0, seeded=True)
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("PDHG_TC_SPEC", flag)
+        ctx = device_ctx(P, "fp64")
+        try:
+            assert ctx.path_info("tc_spec") == int(flag) and ctx.path_info("fused_residual") == 1
+            ctx.set_state(P["phi"], P["rho"], P["alp"])
+            ctx.iterate(1, TAU, SIGMA, -1.0, 1)          # the dual sweep leaves R formed
+            ctx.update_primal(TAU)
+            p1 = ctx.get_state(rho=False, alp=False)[0]
+            ctx.update_primal(TAU)
+            out[flag] = (p1, ctx.get_state(rho=False, alp=False)[0])
+        finally:
+            ctx.close()
+    m = {"first": rel(out["1"][0], out["0"][0]), "second": rel(out["1"][1], out["0"][1])}
+    parity_log("test_fp64_task_order_spectrum_primal_twice", "c3_4096x4096_T4", m, {k: 1e-12 for k in m})
+    assert all(v <= 1e-12 for v in m.values()), m
