@@ -5,7 +5,7 @@
 #   smoke                 __graft_entry__.smoke()
 #   tests[:<pytest -k>]   pytest -m gpu (optionally filtered)
 #   bench[:<args>]        python bench.py <args, commas for spaces>  -> bench_<n>.json
-#                         (leading NAME=value arguments of bench / py steps go to that step's environment)
+#                         (leading NAME=value arguments of bench / py / prof / sh steps go to that step's environment)
 #   prof:<config>[,args]  scripts/profile.sh <config> <tag> [bench args]
 #   sh:<script>,<args>    bash <script> <args> ('+' inside an argument stands for a space: counter groups)
 # Every GPU step runs under its own time limit; the first failure ends the script.
@@ -22,7 +22,7 @@ for step in "$@"; do
   arg=${arg//,/ }
   # leading NAME=value tokens of a bench / py step are set in that step's environment only
   ENVV=()
-  if [ "$kind" = bench ] || [ "$kind" = py ]; then
+  if [ "$kind" = bench ] || [ "$kind" = py ] || [ "$kind" = prof ] || [ "$kind" = sh ]; then
     read -ra TOK <<< "$arg"
     while [ ${#TOK[@]} -gt 0 ] && [[ ${TOK[0]} =~ ^[A-Z_][A-Z0-9_]*= ]]; do ENVV+=("${TOK[0]}"); TOK=("${TOK[@]:1}"); done
     arg="${TOK[*]}"
@@ -38,13 +38,13 @@ for step in "$@"; do
     bench) env "${ENVV[@]}" timeout -k 10 900 python -u bench.py $arg > "$OUT/bench_$n.json" 2> "$OUT/bench_$n.err" || { echo "bench failed rc=$?"; tail -20 "$OUT/bench_$n.err"; exit 1; }
            cat "$OUT/bench_$n.json" ;;
     prof)  read -ra TOK <<< "$arg"; PT="${TAG}_$(echo "${TOK[*]}" | tr -c 'A-Za-z0-9_\n' '_')"
-           timeout -k 10 1000 bash scripts/profile.sh "${TOK[0]}" "$PT" "${TOK[@]:1}" > "$OUT/prof_$n.log" 2>&1 || { echo "prof failed rc=$?"; tail -20 "$OUT/prof_$n.log"; exit 1; }
+           env "${ENVV[@]}" timeout -k 10 1000 bash scripts/profile.sh "${TOK[0]}" "$PT" "${TOK[@]:1}" > "$OUT/prof_$n.log" 2>&1 || { echo "prof failed rc=$?"; tail -20 "$OUT/prof_$n.log"; exit 1; }
            echo "profile: gpurun_out/prof_$PT"
            cd "$REPO" ;;
     py)    env "${ENVV[@]}" timeout -k 10 900 python -u $arg > "$OUT/py_$n.log" 2>&1 || { echo "py failed rc=$?"; tail -30 "$OUT/py_$n.log"; exit 1; }
            tail -40 "$OUT/py_$n.log" ;;
     sh)    read -ra TOK <<< "$arg"; TOK=("${TOK[@]//+/ }")
-           timeout -k 10 1100 bash "${TOK[@]}" > "$OUT/sh_$n.log" 2>&1 || { echo "sh failed rc=$?"; tail -20 "$OUT/sh_$n.log"; exit 1; }
+           env "${ENVV[@]}" timeout -k 10 1100 bash "${TOK[@]}" > "$OUT/sh_$n.log" 2>&1 || { echo "sh failed rc=$?"; tail -20 "$OUT/sh_$n.log"; exit 1; }
            tail -5 "$OUT/sh_$n.log"; cd "$REPO" ;;
     *) echo "unknown step $kind"; exit 2 ;;
   esac
