@@ -99,7 +99,9 @@ int pdhg_destroy(pdhg_ctx* ctx);
  *        contiguous [n_alp][T][nx][ny][n_ctrl] block.
  * Only the live control components are stored on the device:
  * set_state fails with PDHG_ERR_UNSUPPORTED if a dead component is non-zero;
- * get_state writes zeros there. */
+ * get_state writes zeros there.  A null array is not transferred: set_state overwrites the given parts of the
+ * current state and keeps the device's values of the others (window marching re-seeds phi alone when rho / alp
+ * are the ones the device holds); it resets the iteration / stop bookkeeping either way. */
 int pdhg_set_state(pdhg_ctx* ctx, const double* phi, const double* rho, const double* alp);
 int pdhg_get_state(pdhg_ctx* ctx, double* phi, double* rho, double* alp);
 int pdhg_get_phi_bar(pdhg_ctx* ctx, double* phi_bar);   /* [T+1][nx][ny] */

@@ -41,8 +41,9 @@ template <typename R> __device__ __forceinline__ R nclamp(R x, R lo, R hi) {
 }
 
 // Device control block: loop control that never round-trips through the host.
+constexpr int kHaltTail = 3;   // Ctrl::done: a speculative one-sub-iteration iteration stopped for the host (iterate())
 struct Ctrl {
-  int done;          // 0 running, 1 converged, 2 NaN
+  int done;          // 0 running, 1 converged, 2 NaN, kHaltTail: halted before the rest of the dual loop
   int iters;         // outer iterations executed since the last reset
   int inner_done;    // dual loop of the current outer iteration has exited early
   int inner_count;   // dual sub-iterations executed in the current outer iteration

@@ -77,8 +77,10 @@ __global__ void __launch_bounds__(1024) k_finalize_primal(const double* partials
 // After dual sub-iteration `sub`: err = sum (drho)^2/sum rho'^2 + sum_a sum (dalp)^2/sum alp'^2
 // (update_fns_in_pdhg.py:162-164); early exit flag when err < eps (:176).  n_dead reference
 // arrays that are not stored (egno 3's y controls, identically zero) contribute 0/0 = NaN.
+// spec (the speculative one-sub-iteration schedule of iterate(), pdhg_api.hip): a loop that does not exit here halts
+// the iteration instead (done = kHaltTail: every later kernel returns at entry) and the host runs the rest of the loop
 __device__ __forceinline__ void finalize_dual_sums(const double* out, int na, int n_dead, double eps, int sub,
-                                                   Ctrl* ctrl) {
+                                                   Ctrl* ctrl, int spec = 0) {
   const int ns = 3 + 3 * na;
   if (threadIdx.x == 0) {
     double err = out[0] / out[1];
@@ -94,14 +96,15 @@ __device__ __forceinline__ void finalize_dual_sums(const double* out, int na, in
     ctrl->err_inner = err;
     ctrl->inner_count = sub + 1;
     if (err < eps) ctrl->inner_done = 1;
+    else if (spec) ctrl->done = kHaltTail;
   }
 }
 __global__ void __launch_bounds__(1024) k_finalize_dual(const double* partials, int nrows, int na, int n_dead,
-                                                       double eps, int sub, Ctrl* ctrl) {
+                                                       double eps, int sub, Ctrl* ctrl, int spec = 0) {
   if (ctrl->done || ctrl->inner_done) return;
   __shared__ double out[kNumSums];
   reduce_partials(partials, nrows, 3 + 3 * na, out);
-  finalize_dual_sums(out, na, n_dead, eps, sub, ctrl);
+  finalize_dual_sums(out, na, n_dead, eps, sub, ctrl, spec);
 }
 
 // The fold and the finalize of a dual sub-iteration in one launch: workgroup b folds its chunk of the table into

@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -141,6 +142,9 @@ struct Impl : ImplBase {
   // PDHG_FOLD_FIN=0: two launches)
   bool fold_fin = false;
   bool dual_head = false;    // ... below 2^25 points: sub-iteration 0 alone, the rest in chunks (kernels_dual_multi.hpp)
+  bool spec_ok = false;      // iterate() may use the speculative one-sub-iteration schedule (head form, PDHG_SPEC)
+  bool spec = false;         // ... and uses it now (launch_dual / launch_outer / the captured graph)
+  long long spec_iters = 0, spec_halts = 0;   // iterations enqueued speculatively / halts (path_info, tests)
   bool dual_multi = false;   // rho_alp_iters > 1: the dual loop in chunks of sub-iterations (kernels_dual_multi.hpp)
   static constexpr int kMultiSub = 5;     // sub-iterations one chunk pass runs
   int NTd = 256, gxd = 0, gyd = 0, gzd = 0, jchunk_d = 1;
@@ -564,6 +568,10 @@ struct Impl : ImplBase {
     // after sub-iteration 0 in nearly every outer iteration, where 18 returning launches cost ~0.2 ms
     dual_head = multi_ok && !dual_multi;
     if (const char* e = getenv("PDHG_DUAL_HEAD")) dual_head = multi_ok && !dual_multi && atoi(e) != 0;   // A/B, tests
+    // the speculative schedule of iterate() needs the head form's one-sub-iteration shortcuts (k1_outer) and the
+    // two-launch fold / finalize (the halt flag is set by k_finalize_dual)
+    spec_ok = dual_head && k1_outer && !fold_fin;
+    if (const char* e = getenv("PDHG_SPEC")) spec_ok = spec_ok && atoi(e) != 0;   // A/B, tests
     partial_rows = std::max<size_t>({(size_t)gx4 * g4, (size_t)gx5 * g5, (size_t)g_outer, (size_t)g_fast_upd,
                                      (size_t)gxd * gyd * (gzd + 1), fourstep ? (size_t)9 * ((T + 1) / 2) : 1, 1,
                                      (dual_multi || dual_head) ? (size_t)kMultiSub * gxd * gyd * gzd : (size_t)1});
@@ -1601,9 +1609,19 @@ struct Impl : ImplBase {
         rows = fold_out;
         nrows = kFoldRows;
       }
-      hipLaunchKernelGGL(k_finalize_dual, dim3(1), dim3(1024), 0, stream, rows, nrows, na, n_dead, eps, s, p.ctrl);
+      hipLaunchKernelGGL(k_finalize_dual, dim3(1), dim3(1024), 0, stream, rows, nrows, na, n_dead, eps, s, p.ctrl,
+                         (head && spec) ? 1 : 0);
     }
-    if (head) {
+    if (head && !spec) return launch_dual_tail(sigma, eps, k);   // spec: only when sub-iteration 0 did not exit
+    HIP_TRY(hipGetLastError());
+    return PDHG_OK;
+  }
+  // the head form's rest of the dual loop: chunk passes from sub-iteration 1 (+ their finalizes, the final pass)
+  int launch_dual_tail(R sigma, double eps, int k) {
+    KP<R> p = kp;
+    p.sigma = sigma;
+    p.inplace = 0;
+    {
       ProfScope ps(this, "dual");
       if (pb.egno == 1) launch_dual_multi_e<1>(p, k, eps, 1);
       else if (pb.egno == 2) launch_dual_multi_e<2>(p, k, eps, 1);
@@ -1620,7 +1638,9 @@ struct Impl : ImplBase {
     // per-sub-iteration kernels skip the outer pass after a one-sub-iteration loop
     const int k1_skip = (k1_outer && !dual_multi) ? 1 : 0;
     if (k > 1) {
-      hipLaunchKernelGGL((k_outer_sums<R>), dim3(g_outer), dim3(256), 0, stream, p, (size_t)pb.T * plane(), k1_skip);
+      // spec: the iteration reaches here only after a one-sub-iteration loop, whose outer-sum pass returns at once
+      if (!spec)
+        hipLaunchKernelGGL((k_outer_sums<R>), dim3(g_outer), dim3(256), 0, stream, p, (size_t)pb.T * plane(), k1_skip);
       rows = g_outer;
     }
     hipLaunchKernelGGL(k_finalize_outer, dim3(1), dim3(1024), 0, stream, p.partials, rows, na, eps, k > 1 ? 1 : 0,
@@ -1659,7 +1679,7 @@ struct Impl : ImplBase {
   // events) and with PDHG_GRAPH=0.
   hipGraphExec_t gexec = nullptr;
   double g_tau = 0, g_sigma = 0, g_eps = 0;
-  int g_k = 0, g_window = 0, g_stop = -1;
+  int g_k = 0, g_window = 0, g_stop = -1, g_spec = -1;
   bool use_graph = true;
   bool warm = false;   // one eager iteration ran (kernel attributes set outside any capture)
   void drop_graph() {
@@ -1674,7 +1694,8 @@ struct Impl : ImplBase {
   }
   int ensure_graph(double tau, double sigma, double eps, int k, int window) {
     const int stop = stop_conv * 2 + stop_nan;   // kernel arguments of k_finalize_outer
-    if (gexec && g_tau == tau && g_sigma == sigma && g_eps == eps && g_k == k && g_window == window && g_stop == stop)
+    if (gexec && g_tau == tau && g_sigma == sigma && g_eps == eps && g_k == k && g_window == window && g_stop == stop &&
+        g_spec == (int)spec)
       return PDHG_OK;
     drop_graph();
     hipGraph_t g = nullptr;
@@ -1699,7 +1720,22 @@ struct Impl : ImplBase {
     g_k = k;
     g_window = window;
     g_stop = stop;
+    g_spec = (int)spec;
     return PDHG_OK;
+  }
+
+  // A speculative iteration halted after sub-iteration 0 (done = kHaltTail): wait for the no-op launches behind it,
+  // re-arm, and run the rest of its dual loop and its outer tests (launch_dual's tail + launch_outer of the full
+  // schedule).  h: the control block after it (iters counts the completed iterations, the halted one included).
+  int finish_halted(double sigma, double eps, int k, Ctrl& h) {
+    int rc;
+    HIP_TRY(hipStreamSynchronize(stream));
+    int zero = 0;
+    HIP_TRY(hipMemcpyAsync(&kp.ctrl->done, &zero, sizeof(int), hipMemcpyHostToDevice, stream));
+    spec = false;
+    if ((rc = launch_dual_tail((R)sigma, eps, k))) return rc;
+    if ((rc = launch_outer(eps, k))) return rc;
+    return read_ctrl(h);   // synchronizes (zero stays valid until the copy ran)
   }
 
   int iterate(int n, double tau, double sigma, double eps, int k, pdhg_stats* st) {
@@ -1707,8 +1743,30 @@ struct Impl : ImplBase {
     if ((rc = reset_ctrl())) return rc;
     const int window = 8;   // host runs at most 2*window iterations ahead of the device
     std::vector<hipEvent_t> evs;
-    int ran = 0;
     if (const char* e = getenv("PDHG_GRAPH")) use_graph = atoi(e) != 0;
+    // Speculative one-sub-iteration schedule (the head form, rho_alp_iters > 1): C2's T = 1 marching windows exit the
+    // dual loop after sub-iteration 0 in nearly every iteration, and the rest of the loop (chunk passes, finalizes,
+    // final pass, outer-sum pass: 6 launches) then only returns at once.  After a window of iterations that all ran
+    // one sub-iteration, the host enqueues iterations without those launches; an iteration whose loop does not exit
+    // after sub-iteration 0 halts (done = kHaltTail, every later kernel returns), and the host runs the rest of its
+    // loop and its outer tests -- the launches the full schedule would have made, in the same order -- then goes on
+    // with the full schedule for a few windows.  Same kernels on the same data: the states are the full schedule's
+    // bit for bit.  PDHG_SPEC=0 keeps the full schedule.
+    const bool spec_able = spec_ok && dual_head && k > 1 && k <= kDualMultiMax;
+    // PDHG_SPEC_FORCE=1 (tests): speculate from the first iteration and again right after every halt, so the halt /
+    // finish path runs as often as the loop needs more than one sub-iteration
+    const bool spec_force = spec_able && [] { const char* e = getenv("PDHG_SPEC_FORCE"); return e && atoi(e) != 0; }();
+    spec = spec_force;
+    struct SpecOff {   // every return path leaves the full schedule for the drop-in update_* calls
+      bool& s;
+      ~SpecOff() { s = false; }
+    } spec_off{spec};
+    int cool = 0;
+    long long last_iters = 0, last_inner = 0;
+    auto drain_events = [&]() {
+      for (auto e : evs) hipEventDestroy(e);
+      evs.clear();
+    };
     for (int i = 0; i < n;) {
       // a whole window from the graph when one fits and the state allows it; otherwise one eager iteration
       const bool steady = !fuse_res || res_valid;
@@ -1716,30 +1774,58 @@ struct Impl : ImplBase {
         if ((rc = ensure_graph(tau, sigma, eps, k, window))) return rc;
         HIP_TRY(hipGraphLaunch(gexec, stream));
         i += window;
-        ran += window;
+        if (spec) spec_iters += window;
       } else {
         if ((rc = launch_iteration(tau, sigma, eps, k))) return rc;
         warm = true;
         ++i;
-        ++ran;
+        if (spec) ++spec_iters;
       }
-      if (i % window == 0 && i < n) {
-        hipEvent_t e;
-        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(e, stream));
-        evs.push_back(e);
-        if (evs.size() >= 2) {
-          hipEvent_t old = evs[evs.size() - 2];
-          HIP_TRY(hipEventSynchronize(old));
-          HIP_TRY(hipMemcpy(h_done, &kp.ctrl->done, sizeof(int), hipMemcpyDeviceToHost));
-          if (*h_done) break;
-        }
+      const bool check = i % window == 0 && i < n;
+      if (!check) continue;
+      hipEvent_t e;
+      HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      HIP_TRY(hipEventRecord(e, stream));
+      evs.push_back(e);
+      if (evs.size() < 2) continue;
+      HIP_TRY(hipEventSynchronize(evs[evs.size() - 2]));
+      Ctrl h;
+      HIP_TRY(hipMemcpy(&h, kp.ctrl, sizeof(Ctrl), hipMemcpyDeviceToHost));
+      if (h.done == kHaltTail) {
+        ++spec_halts;
+        if ((rc = finish_halted(sigma, eps, k, h))) return rc;
+        drain_events();
+        i = h.iters;              // the halted iteration is complete; the ones enqueued after it were no-ops
+        spec = spec_force;
+        cool = spec_force ? 0 : 4;   // windows on the full schedule before speculating again
+        last_iters = h.iters;
+        last_inner = h.inner_total;
+        if (h.done) break;
+        continue;
+      }
+      if (h.done) break;
+      if (spec_able) {   // the checked window's iterations all ran one sub-iteration: speculate from here on
+        const long long d_it = h.iters - last_iters, d_in = h.inner_total - last_inner;
+        if (cool > 0) --cool;
+        else if (!spec && d_it > 0 && d_in == d_it) spec = true;
+        last_iters = h.iters;
+        last_inner = h.inner_total;
       }
     }
-    for (auto e : evs) hipEventDestroy(e);
+    drain_events();
     Ctrl h;
     if ((rc = read_ctrl(h))) return rc;
-    (void)ran;
+    while (h.done == kHaltTail) {   // a halt in the last windows: finish it and run what is left
+      ++spec_halts;
+      if ((rc = finish_halted(sigma, eps, k, h))) return rc;
+      spec = false;
+      for (int i = h.iters; i < n && !h.done; ++i) {
+        if ((rc = launch_iteration(tau, sigma, eps, k))) return rc;
+        if ((i + 1) % window == 0 && (rc = read_ctrl(h))) return rc;
+      }
+      if ((rc = read_ctrl(h))) return rc;
+    }
+    spec = false;
     if (st) {
       st->iters_run = h.iters;
       st->status = h.done;
@@ -2078,7 +2164,11 @@ struct Impl : ImplBase {
     res_valid = false;
     const size_t npl = plane();
     const int T = pb.T;
-    const int cur = 0;
+    // the parts given overwrite the CURRENT buffer set (two sets when rho_alp_iters > 1), so a part passed as null
+    // keeps the device's values -- window marching re-seeds phi alone when rho / alp are already resident
+    int cur = 0;
+    HIP_TRY(hipMemcpyAsync(&cur, &kp.ctrl->cur, sizeof(int), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
     const size_t nphi = (size_t)(T + 1) * npl;
     std::unique_ptr<R[]> buf(new R[nphi]);   // not value-initialised: filled before every copy out of it
     // fp64 planes straight from the caller's arrays (same layout); fp32 through a narrowing copy
@@ -2524,6 +2614,9 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
     else if (k == "res64") *value = im.res64 ? 1 : 0;
     else if (k == "dual_multi") *value = im.dual_multi ? 1 : 0;   // rho_alp_iters > 1: chunked dual passes
     else if (k == "dual_head") *value = im.dual_head ? 1 : 0;   // ... sub-iteration 0 alone, then the chunks
+    else if (k == "spec") *value = im.spec_ok ? 1 : 0;   // iterate(): speculative one-sub-iteration schedule allowed
+    else if (k == "spec_iters") *value = (int)std::min<long long>(im.spec_iters, INT_MAX);   // ... iterations run so
+    else if (k == "spec_halts") *value = (int)std::min<long long>(im.spec_halts, INT_MAX);   // ... and halts (cumulative)
     else if (k == "dual64") *value = (sizeof(typename std::remove_reference<decltype(im)>::type::Real) == 8 && im.fast_dual) ? 1 : 0;
     else if (k == "fast_dual") *value = im.fast_dual ? im.dual_rx : -1;
     else if (k == "dual_ypl") *value = im.fast_dual && im.dual_rx ? im.dual_ypl : 0;

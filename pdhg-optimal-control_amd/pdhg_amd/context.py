@@ -42,6 +42,8 @@ class PDHGContext:
         self.rho_alp_iters = int(rho_alp_iters)
         self._prob = prob
         self._h = self._create(prob, int(device))
+        self._version = 0         # bumped by every call that changes the device state
+        self._resident = None     # (version, rho, alp): host arrays known to equal the device's rho / alp
 
     def _create(self, prob, device):
         h = ctypes.c_void_p()
@@ -65,13 +67,41 @@ class PDHGContext:
             pass
 
     # ---- state ----
+    def alp_block(self, alp):
+        """The contiguous [n_alp, T, ...space, n_ctrl] block a tuple of control arrays views (get_state returns such
+        views), or None: lets set_state / the marching driver skip a stacking copy."""
+        b = getattr(alp[0], "base", None) if len(alp) else None
+        shape = (self.n_alp, self.T) + self._space + (self.n_ctrl,)
+        if not (isinstance(b, np.ndarray) and b.dtype == np.float64 and b.flags.c_contiguous and b.shape == shape
+                and len(alp) == self.n_alp):
+            return None
+        p0 = b.__array_interface__["data"][0]
+        for i, a in enumerate(alp):
+            if a.base is not b or a.shape != shape[1:] or a.__array_interface__["data"][0] != p0 + i * b.strides[0]:
+                return None
+        return b
+
     def set_state(self, phi=None, rho=None, alp=None):
+        """Upload the given parts of the state (reference layouts); a part passed as None keeps the device's values."""
         phi = None if phi is None else np.ascontiguousarray(phi, dtype=np.float64).reshape((self.T + 1,) + self._space)
         rho = None if rho is None else np.ascontiguousarray(rho, dtype=np.float64).reshape((self.T,) + self._space)
         if alp is not None:
-            alp = np.ascontiguousarray(np.stack([np.asarray(a, dtype=np.float64) for a in alp], axis=0))
-            alp = alp.reshape((self.n_alp, self.T) + self._space + (self.n_ctrl,))
+            blk = self.alp_block(alp)
+            if blk is None:
+                blk = np.ascontiguousarray(np.stack([np.asarray(a, dtype=np.float64) for a in alp], axis=0))
+            alp = blk.reshape((self.n_alp, self.T) + self._space + (self.n_ctrl,))
+        self._version += 1
         N.check(self._lib.pdhg_set_state(self._h, N.dptr(phi), N.dptr(rho), N.dptr(alp)))
+
+    def mark_resident(self, rho, alp):
+        """rho / alp (host arrays the caller will not modify) equal the device's state now."""
+        self._resident = (self._version, rho, tuple(alp))
+
+    def is_resident(self, rho, alp):
+        """True if rho / alp are the very arrays mark_resident recorded and the device state has not changed since."""
+        r = self._resident
+        return (r is not None and r[0] == self._version and rho is r[1] and alp is not None and
+                len(alp) == len(r[2]) and all(a is b for a, b in zip(alp, r[2])))
 
     def get_state(self, phi=True, rho=True, alp=True):
         """(phi, rho, alp) from the device; a part passed as False is not copied and comes back as None."""
@@ -98,19 +128,23 @@ class PDHGContext:
         return pb
 
     def set_phi_bar(self, phi_bar):
+        self._version += 1
         pb = np.ascontiguousarray(phi_bar, dtype=np.float64).reshape((self.T + 1,) + self._space)
         N.check(self._lib.pdhg_set_phi_bar(self._h, N.dptr(pb)))
 
     def init_state(self, g):
         g = np.ascontiguousarray(g, dtype=np.float64).reshape(self._space)
+        self._version += 1
         N.check(self._lib.pdhg_init_state(self._h, N.dptr(g)))
 
     # ---- updates ----
     def update_primal(self, tau):
+        self._version += 1
         N.check(self._lib.pdhg_update_primal(self._h, float(tau)))
 
     def update_dual(self, sigma, eps, rho_alp_iters):
         used = ctypes.c_int(0)
+        self._version += 1
         N.check(self._lib.pdhg_update_dual(self._h, float(sigma), float(eps), int(rho_alp_iters), ctypes.byref(used)))
         return used.value
 
@@ -126,6 +160,7 @@ class PDHGContext:
 
     def iterate(self, n_iters, tau, sigma, eps, rho_alp_iters):
         st = N.pdhg_stats()
+        self._version += 1
         N.check(self._lib.pdhg_iterate(self._h, int(n_iters), float(tau), float(sigma), float(eps),
                                        int(rho_alp_iters), ctypes.byref(st)))
         return {"iters_run": st.iters_run, "status": st.status, "inner_last": st.inner_last,

@@ -40,13 +40,18 @@ def _native_tag(fp, fd):
 
 
 def _device_oneiter(tag, fns_dict, phi0, rho0, alp0, x_arr, ndim, dt, dspatial, c_on_rho, epsl, stepsz_param,
-                    N_maxiter, print_freq, eps, verbose, stats):
+                    N_maxiter, print_freq, eps, verbose, stats, last_only=False):
+    """last_only (PDHG_multi_step, which reads results_all[-1] only, utils_pdhg_solver.py:187): the print-point
+    records keep no state copies (they would be discarded)."""
     spec = U._spec(fns_dict)
     phi0 = np.asarray(phi0, dtype=np.float64)
     T = phi0.shape[0] - 1
     ctx = U.get_context(spec, T, phi0.shape[1:], dt, dspatial, epsl, x_arr, tag["bc"], tag["C"], tag["pow"],
                         tag["Ct"], c_on_rho, tag["rho_alp_iters"], tag["precision"])
-    ctx.set_state(phi0, rho0, alp0)
+    if ctx.is_resident(rho0, alp0):   # the previous window's result, still on the device: re-seed phi alone
+        ctx.set_state(phi0, None, None)
+    else:
+        ctx.set_state(phi0, rho0, alp0)
     scale = 1.5                                           # utils_pdhg_solver.py:44-46
     tau, sigma = stepsz_param / scale, stepsz_param * scale
     k = tag["rho_alp_iters"]
@@ -55,7 +60,9 @@ def _device_oneiter(tag, fns_dict, phi0, rho0, alp0, x_arr, ndim, dt, dspatial, 
     last = None
     while i < N_maxiter:
         if print_freq > 0 and i % print_freq == 0:
-            if i == 0:   # the state just set: the caller's arrays (as the reference records them), no device copy
+            if last_only:
+                pass
+            elif i == 0:   # the state just set: the caller's arrays (as the reference records them), no device copy
                 phi_prev = phi0.copy()
                 rho_prev = np.array(rho0, dtype=np.float64).reshape((T,) + phi0.shape[1:])
             else:
@@ -64,9 +71,10 @@ def _device_oneiter(tag, fns_dict, phi0, rho0, alp0, x_arr, ndim, dt, dspatial, 
             last = st
             if st["status"] != 0:
                 break
-            _, _, alp_next = ctx.get_state(phi=False, rho=False)
             error = np.array([st["err1"], st["err2"]])
-            results_all.append((i, phi_prev, rho_prev, alp_next))
+            if not last_only:
+                _, _, alp_next = ctx.get_state(phi=False, rho=False)
+                results_all.append((i, phi_prev, rho_prev, alp_next))
             error_all.append(error)
             if verbose:
                 print("iteration {}, primal error {:.2E}, dual error {:.2E}".format(i, error[0], error[1]), flush=True)
@@ -92,6 +100,11 @@ def _device_oneiter(tag, fns_dict, phi0, rho0, alp0, x_arr, ndim, dt, dspatial, 
     if stats is not None:
         stats.append(dict(last, window_iters=i + 1))   # + the iterations this window ran
     phi, rho, alp = ctx.get_state()
+    # rho / alp as the device holds them: read-only (the reference returns immutable jax arrays), so the next window's
+    # set_state can keep them on the device when they come back unchanged (PDHG_multi_step: rho0, alp0 = rho_c, alp_c)
+    for a in (rho,) + tuple(alp):
+        a.flags.writeable = False
+    ctx.mark_resident(rho, alp)
     error = np.array([last["err1"], last["err2"]])
     results_all.append((i + 1, phi, rho, alp))
     error_all.append(error)
@@ -100,13 +113,14 @@ def _device_oneiter(tag, fns_dict, phi0, rho0, alp0, x_arr, ndim, dt, dspatial, 
 
 def PDHG_solver_oneiter(fn_update_primal, fn_update_dual, fns_dict, phi0, rho0, alp0, x_arr, t_arr, ndim, dt, dspatial,
                         c_on_rho, epsl=0.0, stepsz_param=0.9, fv=None, N_maxiter=1000000, print_freq=1000, eps=1e-6,
-                        tfboard=False, tfrecord_ind=0, verbose=True, stats=None):
-    """Outer PDHG loop (utils_pdhg_solver.py:9-94).  Returns (results_all, error_all)."""
+                        tfboard=False, tfrecord_ind=0, verbose=True, stats=None, _last_only=False):
+    """Outer PDHG loop (utils_pdhg_solver.py:9-94).  Returns (results_all, error_all).  _last_only (internal, used by
+    PDHG_multi_step): the print-point entries of results_all carry no state (only results_all[-1] is read there)."""
     tag = _native_tag(fn_update_primal, fn_update_dual)
     if tag is not None:
         U.check_fv(fv, ndim, np.shape(phi0)[1:], dspatial, tag["bc"])
         return _device_oneiter(tag, fns_dict, phi0, rho0, alp0, x_arr, ndim, dt, dspatial, c_on_rho, epsl,
-                               stepsz_param, N_maxiter, print_freq, eps, verbose, stats)
+                               stepsz_param, N_maxiter, print_freq, eps, verbose, stats, last_only=_last_only)
     # generic callables: the reference's host loop, one device call per update
     phi_prev, rho_prev, alp_prev = phi0, rho0, alp0
     tau, sigma = stepsz_param / 1.5, stepsz_param * 1.5
@@ -138,6 +152,16 @@ def PDHG_solver_oneiter(fn_update_primal, fn_update_dual, fns_dict, phi0, rho0, 
     results_all.append((i + 1, phi_next, rho_next, alp_next))
     error_all.append(error)
     return results_all, np.array(error_all)
+
+
+def _stacked(alp):
+    """np.stack(alp, axis=0) without the copy when the arrays are views of one such block (get_state's result)."""
+    b = getattr(alp[0], "base", None) if len(alp) else None
+    if isinstance(b, np.ndarray) and b.shape == (len(alp),) + alp[0].shape and b.flags.c_contiguous and \
+            all(a.base is b and np.shares_memory(a, b[i]) and a.__array_interface__["data"][0] ==
+                b[i].__array_interface__["data"][0] for i, a in enumerate(alp)):
+        return b
+    return np.stack(alp, axis=0)
 
 
 def PDHG_multi_step(fn_update_primal, fn_update_dual, fns_dict, g, x_arr, ndim, nt, nspatial, dt, dspatial, c_on_rho,
@@ -209,7 +233,8 @@ def PDHG_multi_step(fn_update_primal, fn_update_dual, fns_dict, g, x_arr, ndim, 
             results_all, errs = PDHG_solver_oneiter(fn_update_primal, fn_update_dual, fns_dict, phi0, rho0, alp0,
                                                     x_arr, t_arr, ndim, dt, dspatial, c_on_rho, epsl=epsl,
                                                     stepsz_param=stepsz_param, fv=fv, N_maxiter=N_maxiter,
-                                                    print_freq=print_freq, eps=eps, verbose=verbose, stats=stats)
+                                                    print_freq=print_freq, eps=eps, verbose=verbose, stats=stats,
+                                                    _last_only=True)
             if np.any(np.isnan(errs)):
                 if stepsz_param > s_min + s_delta:            # back-off, utils_pdhg_solver.py:180-183
                     stepsz_param -= s_delta
@@ -224,7 +249,7 @@ def PDHG_multi_step(fn_update_primal, fn_update_dual, fns_dict, g, x_arr, ndim, 
                 max_iters = max(max_iters, iters)
                 phi_all.append(phi_c[:-1] if i < nt_PDHG - 1 else phi_c)
                 rho_all.append(rho_c)
-                alp_all.append(np.stack(alp_c, axis=0))
+                alp_all.append(_stacked(alp_c))
                 errs_all.append(errs)
                 phi0 = phi0 + (phi_c[-1:] - phi0[0:1])        # warm start, :201-203
                 rho0, alp0 = rho_c, alp_c

@@ -555,6 +555,57 @@ def test_fp64_nx4096_x_transform(native, case):
     assert abs(st["err1"] - e1_o) <= 1e-8 * e1_o and abs(st["err2"] - e2_o) <= 1e-8 * e2_o
 
 
+def _march(monkeypatch, env, n=None, windows=None):
+    """The marching fixture's run (tests/golden/marching_c2dt_64.json: C2's dt, T = 1 windows, k = 10, eps 1e-6) through
+    the drop-in driver with `env`, on an n x n grid (default the fixture's 64^2) and the first `windows` windows;
+    returns (per-window stop counts, final state, {spec, spec_iters, spec_halts} summed over the driver's contexts)."""
+    import json
+    from pdhg_amd import set_fns, utils_pdhg_solver as S
+    from pdhg_amd import update_fns_in_pdhg as U
+    for key, v in env.items():
+        monkeypatch.setenv(key, v)
+    U.clear_cache()
+    F = json.load(open(os.path.join(HERE, "golden", "marching_c2dt_64.json")))
+    nx = ny = n or F["nx"]
+    ndim, egno = F["ndim"], F["egno"]
+    fns = set_fns.set_up_example_fns(egno, ndim, 0)
+    x_arr = O.make_grid(ndim, nx, ny, egno)
+    g = set_fns.set_up_J(egno, ndim, (2.0, 2.0))(x_arr)
+    dsp = (2.0 / nx, 2.0 / ny)
+    fv = O.compute_Dxx_fft_fv(ndim, (nx, ny), dsp, (0, 0))
+    fp, fd = S.make_update_fns(ndim, (0, 0), rho_alp_iters=F["rho_alp_iters"], precision="fp64")
+    stats = []
+    res, _ = S.PDHG_multi_step(fp, fd, fns, g, x_arr, ndim, (windows or F["windows"]) + 1, (nx, ny), F["dt"], dsp,
+                               70.0, time_step_per_PDHG=2, epsl=F["epsl"], stepsz_param=F["stepsz"], fv=fv,
+                               n_ctrl=ndim, N_maxiter=1000000, print_freq=1000000, eps=F["eps"], verbose=False,
+                               stats=stats)
+    spec = {key: sum(c.path_info(key) for c in U._CACHE.values()) for key in ("spec", "spec_iters", "spec_halts")}
+    U.clear_cache()
+    return [int(st["window_iters"]) for st in stats], res[0], spec
+
+
+def test_speculative_schedule_bitwise(native, monkeypatch, parity_log):
+    """iterate()'s speculative one-sub-iteration schedule (the marching default's T = 1 windows; pdhg_api.hip
+    iterate / finish_halted) against the full schedule (PDHG_SPEC=0) on the marching fixture: the same per-window stop
+    counts, NaN back-offs and final state bit for bit -- it leaves out only launches that return at once, and an
+    iteration whose loop does not exit after sub-iteration 0 halts and is finished by the host with the full
+    schedule's launches.  The default policy must have speculated; PDHG_SPEC_FORCE=1 speculates from every window's
+    first iteration and right after every halt, so the halt / finish path runs many times (asserted).  256^2 (the
+    head form needs ny % 256 == 0), the fixture's dt / k / eps / step size, its first 3 windows."""
+    it1, r1, sp1 = _march(monkeypatch, {"PDHG_SPEC": "1", "PDHG_SPEC_FORCE": "0"}, 256, 3)
+    itf, rf, spf = _march(monkeypatch, {"PDHG_SPEC": "1", "PDHG_SPEC_FORCE": "1"}, 256, 3)
+    it0, r0, sp0 = _march(monkeypatch, {"PDHG_SPEC": "0", "PDHG_SPEC_FORCE": "0"}, 256, 3)
+    parity_log("test_speculative_schedule_bitwise", "marching_c2dt_256_w3",
+               {"halts": sp1["spec_halts"], "spec_iters": sp1["spec_iters"], "forced_halts": spf["spec_halts"],
+                "forced_spec_iters": spf["spec_iters"]}, {}, iters=it1)
+    assert sp1["spec"] > 0 and sp1["spec_iters"] > 0 and sp0["spec_iters"] == 0, (sp1, sp0)
+    assert spf["spec_halts"] > 0, spf
+    assert it1 == it0 == itf
+    assert r1[0] == r0[0] == rf[0]
+    for a, b, c in zip(r1[1:], r0[1:], rf[1:]):
+        assert np.array_equal(a, b) and np.array_equal(c, b)
+
+
 @pytest.mark.parametrize("head,k1", [("1", "1"), ("0", "1"), ("1", "0"), ("0", "0")],
                          ids=["default", "head0", "k1outer0", "head0_k1outer0"])
 def test_marching_window_counts_fp64(native, monkeypatch, parity_log, head, k1):
