@@ -310,3 +310,167 @@ __global__ void __launch_bounds__(256) k_f16a_inv_1d(KP<R> p, const cplx<R>* __r
 }
 
 }  // namespace pdhg
+
+namespace pdhg {
+
+// ---- fused 1-D residual (C1, rho_alp_iters = 1, periodic x) ----
+// The dual step of row j (update_fns_in_pdhg.py:99-113, 150-165; k_dual_1d's arithmetic) also forms the NEXT primal's
+// continuity residual (update_fns_in_pdhg.py:72-81) from the rho', alp' it has just computed, so stage A of the
+// 16 x 4096 transform reads one residual row per row instead of rho rows j .. j+2 and both alp rows (round 5: stage A
+// fetched 1.5x its inputs; fp64 C1 0.97 GB per iteration).  A thread owns one x and marches over a chunk of time
+// rows (phi_bar row j+1 kept as the next step's row j); the x +- 1 values of the new rho' and fluxes
+// m1 = (rho'+1e-4) f+(alp1'), m2 = (rho'+1e-4) f-(alp2') come from the adjacent lanes (DPP), R_{j-1} is completed one
+// step later with rho'_j.  What a wave cannot form -- its edge x's neighbour terms -- the neighbouring waves write
+// to p.ex ([2][T][nx/64]: the left term eps rho'(x0-1)/dx^2 + m1(x0-1)/dx, the right term eps rho'(x1+1)/dx^2 -
+// m2(x1+1)/dx), and a chunk's last row leaves its time difference to stage A (rho rows j, j+1 of the state), which
+// adds both.  grid (nx/256, nchunk); block 256; partial rows blockIdx.y * gridDim.x + blockIdx.x.
+template <typename R, int EGNO>
+__global__ void __launch_bounds__(256) k_dual_1d_fr(KP<R> p, int jchunk) {
+  if (p.ctrl->done || p.ctrl->inner_done) return;
+  const int cur = p.ctrl->cur;   // in place (rho_alp_iters = 1)
+  const int nx = p.nx, T = p.T;
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int w = x >> 6, nw = nx >> 6;
+  const int j0 = blockIdx.y * jchunk, j1 = min(T, j0 + jchunk);
+  constexpr int NS = 9;
+  double s[NS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) s[i] = 0.0;
+  if (j0 < j1) {
+    const int xw = x - lane;   // the wave's first x; its neighbours outside the wave (periodic)
+    const int el = (xw - 1 + nx) % nx, er = (xw + kWave) % nx;
+    const R a = p.ax[x];
+    R* rho = p.rho[cur];
+    R* a1 = p.alp[cur][0];
+    R* a2 = p.alp[cur][1];
+    R* exl = p.ex;
+    R* exr = p.ex + (size_t)T * nw;
+    const int wl = (w - 1 + nw) % nw, wr = (w + 1) % nw;
+    struct In {
+      R pc, pl, pr, rho, b1, b2;
+    };
+    auto load = [&](int j) {
+      In in;
+      const R* f1 = p.phibar + (size_t)(j + 1) * nx;
+      in.pc = f1[x];
+      in.pl = f1[el];
+      in.pr = f1[er];
+      const size_t o = (size_t)j * nx + x;
+      in.rho = rho[o];
+      in.b1 = a1[o];
+      in.b2 = a2[o];
+      return in;
+    };
+    R f0 = p.phibar[(size_t)j0 * nx + x];   // phi_bar row j
+    In nxt = load(j0);
+    R rprev = (R)0, epsp = (R)0, divp = (R)0;   // rho'_{j-1} and row j-1's spatial terms
+    const bool use_eps = p.epsl != (R)0;
+#pragma unroll 1
+    for (int j = j0; j < j1; ++j) {
+      const In in = nxt;
+      nxt = load(min(j + 1, j1 - 1));
+      const R pc = in.pc;
+      const R pxm = lane_from_prev(pc, in.pl), pxp = lane_from_next(pc, in.pr);
+      const R DxR = (pxp - pc) * p.inv_dx;
+      const R DxL = (pc - pxm) * p.inv_dx;
+      const R r0 = in.rho;
+      const R pinv = (r0 + (R)1e-4) / p.sigma;
+      const R q = prox_recip<R, EGNO>(r0, p.sigma, pinv);
+      const R an0 = alp_prox<R, EGNO>(in.b1, DxR, a, pinv, q, true);
+      const R an1 = alp_prox<R, EGNO>(in.b2, DxL, a, pinv, q, false);
+      const R f1v = fpos<R>(fval<R, EGNO>(an0, a));
+      const R f2v = fneg<R>(fval<R, EGNO>(an1, a));
+      const R L = lag<R, EGNO>(an0 * an0) + lag<R, EGNO>(an1 * an1);
+      R vec = (pc - f0) * p.inv_dt;
+      if (use_eps) vec = vec - p.epsl * ((pxp + pxm - (R)2 * pc) * p.inv_dx2);
+      vec = vec - (DxR * f1v + DxL * f2v);
+      vec = vec - L;
+      const R rn = nmax<R>(r0 + p.sigma * vec, (R)0);
+      const size_t o = (size_t)j * nx + x;
+      rho[o] = rn;
+      a1[o] = an0;
+      a2[o] = an1;
+      const double dr = (double)rn - (double)r0;
+      s[0] += dr * dr;
+      s[1] += (double)rn * (double)rn;
+      s[2] += (double)r0 * (double)r0;
+      const double d0 = (double)an0 - (double)in.b1, d1 = (double)an1 - (double)in.b2;
+      s[3] += d0 * d0;
+      s[4] += (double)an0 * (double)an0;
+      s[5] += (double)in.b1 * (double)in.b1;
+      s[6] += d1 * d1;
+      s[7] += (double)an1 * (double)an1;
+      s[8] += (double)in.b2 * (double)in.b2;
+      // row j's residual terms (cont_residual_1d order: (time difference + eps Dxx rho') - div m)
+      const R m1 = (rn + (R)1e-4) * fpos<R>(fval<R, EGNO>(an0, a));
+      const R m2 = (rn + (R)1e-4) * fneg<R>(fval<R, EGNO>(an1, a));
+      const R rm = lane_from_prev(rn, (R)0), rp = lane_from_next(rn, (R)0);
+      const R m1m = lane_from_prev(m1, (R)0), m2p = lane_from_next(m2, (R)0);
+      const R epsj = use_eps ? p.epsl * ((rp + rm - (R)2 * rn) * p.inv_dx2) : (R)0;
+      const R divj = (m1 - m1m) * p.inv_dx + (m2p - m2) * p.inv_dx;
+      if (lane == 0) exr[(size_t)j * nw + wl] = (use_eps ? p.epsl * (rn * p.inv_dx2) : (R)0) - m2 * p.inv_dx;
+      if (lane == kWave - 1) exl[(size_t)j * nw + wr] = (use_eps ? p.epsl * (rn * p.inv_dx2) : (R)0) + m1 * p.inv_dx;
+      if (j > j0) p.res[(size_t)(j - 1) * nx + x] = ((rn - rprev) * p.inv_dt + epsp) - divp;
+      rprev = rn;
+      epsp = epsj;
+      divp = divj;
+      f0 = pc;
+    }
+    // the chunk's last row: at the window's end rho_T = 0 and + c/dt (update_fns_in_pdhg.py:78-80); inside the window
+    // rho'_{j1} belongs to the next chunk -- stage A adds the time difference
+    const R last = (j1 == T) ? (((R)0 - rprev) * p.inv_dt + epsp) - divp + p.c_over_dt : epsp - divp;
+    p.res[(size_t)(j1 - 1) * nx + x] = last;
+  }
+  block_reduce_store<NS>(s, p.partials, blockIdx.y * gridDim.x + blockIdx.x);
+}
+
+// Stage A (forward) of the fused 1-D residual: the residual rows j, j+1 as k_dual_1d_fr left them plus its wave-edge
+// terms (p.ex) and, on a chunk's last row, the time difference (rho_{j+1} - rho_j)/dt from the state; then the same
+// 16-point DFT over n1, twiddles and Y layout as k_f16a_fwd_1d.  grid (4096/256, pairs); block 256.
+template <typename R = float>
+__global__ void __launch_bounds__(256) k_f16a_fwd_fr_1d(KP<R> p, const cplx<R>* __restrict__ twN, cplx<R>* __restrict__ Y,
+                                                        int jchunk) {
+  using C = cplx<R>;
+  if (p.ctrl->done) return;
+  const int nx = p.nx, T = p.T;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int lane = c & (kWave - 1);
+  const int pair = blockIdx.y, j = 2 * pair;
+  const bool has2 = (j + 1) < T;
+  const int jb = has2 ? j + 1 : j;
+  const int nw = nx >> 6;
+  const R* R0 = p.res + (size_t)j * nx;
+  const R* R1 = p.res + (size_t)jb * nx;
+  const R* rho = p.rho[p.ctrl->cur];
+  const R* exl = p.ex;
+  const R* exr = p.ex + (size_t)T * nw;
+  const bool fx0 = (j + 1) % jchunk == 0 && j + 1 < T;          // chunk boundaries (uniform)
+  const bool fx1 = has2 && (j + 2) % jchunk == 0 && j + 2 < T;
+  C v[16];
+#pragma unroll
+  for (int n1 = 0; n1 < 16; ++n1) {
+    const int x = kF16N2 * n1 + c;
+    R r0 = R0[x];
+    R r1 = has2 ? R1[x] : (R)0;
+    if (lane == 0) {
+      r0 += exl[(size_t)j * nw + (x >> 6)];
+      if (has2) r1 += exl[(size_t)jb * nw + (x >> 6)];
+    } else if (lane == kWave - 1) {
+      r0 += exr[(size_t)j * nw + (x >> 6)];
+      if (has2) r1 += exr[(size_t)jb * nw + (x >> 6)];
+    }
+    if (fx0) r0 += (rho[(size_t)(j + 1) * nx + x] - rho[(size_t)j * nx + x]) * p.inv_dt;
+    if (fx1) r1 += (rho[(size_t)(j + 2) * nx + x] - rho[(size_t)(j + 1) * nx + x]) * p.inv_dt;
+    v[n1] = cmk<C>(r0, r1);
+  }
+  dft_any<C, 16>(v);
+  C wv[16];
+  twiddles_from3<C, 16>(wv, twN, c);   // W_65536^{c k1}
+  C* Yp = Y + (size_t)pair * nx + c;
+  Yp[0] = v[0];
+#pragma unroll
+  for (int k1 = 1; k1 < 16; ++k1) Yp[(size_t)k1 * kF16N2] = cmul(v[k1], wv[k1]);
+}
+
+}  // namespace pdhg

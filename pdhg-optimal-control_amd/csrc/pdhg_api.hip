@@ -153,6 +153,7 @@ struct Impl : ImplBase {
   // fused residual: the dual sweep also forms the next primal's residual rows (k_dual_lds_2d FR), the
   // residual kernel only completes the tile-edge terms and transforms (k_res_fwdy_fused_2d)
   bool fuse_res = false;
+  int gz_1d = 1, jchunk_1d = 1;   // 1-D fused residual (k_dual_1d_fr): time chunks of the dual sweep
   bool res_valid = false;   // p.res / p.ey hold the residual of the current (rho, alp)
   int n_cu = 256;           // compute units (persistent grids)
   size_t lds_res = 0, lds_xt = 0;
@@ -549,6 +550,13 @@ struct Impl : ImplBase {
       g5 = std::max(1, std::min(T, 8192 / std::max(1, gx5)));
       // chunked t-solve: one wave per 32-row chunk of 64 modes (T <= 512, Ct != 0)
       thomas_chunk = pb.Ct != 0.0 && T <= 16 * 32;
+      // fused 1-D residual (C1's 16 x 4096 path, rho_alp_iters = 1, periodic x): the dual sweep forms the residual
+      // rows (k_dual_1d_fr), stage A reads them (k_f16a_fwd_fr_1d); 8 time chunks of the sweep
+      fuse_res = fs16 && pb.bc_x == 0 && !two_sets && pb.egno != 3 && nx % 256 == 0;
+      if (const char* e = getenv("PDHG_FUSE_RES1D")) fuse_res = fuse_res && atoi(e) != 0;   // A/B: 0 = unfused
+      gz_1d = std::min(8, T);
+      jchunk_1d = (T + gz_1d - 1) / gz_1d;
+      gz_1d = (T + jchunk_1d - 1) / jchunk_1d;
       if (const char* e = getenv("PDHG_THOMAS_CHUNK")) thomas_chunk = thomas_chunk && atoi(e) != 0;   // override
     }
     g_outer = 2048;
@@ -628,10 +636,13 @@ struct Impl : ImplBase {
     }
     p.res = p.ex = p.ey = nullptr;
     p.rspec = nullptr;
-    if (fuse_res) {
+    if (fuse_res && is2d) {
       if ((rc = alloc(&p.res, (size_t)T * npl))) return rc;
       if ((rc = alloc(&p.ex, (size_t)T * (nx / 8) * 2 * ny))) return rc;
       if ((rc = alloc(&p.ey, (size_t)T * nx * (ny / (64 * dual_ypl)) * 2))) return rc;
+    } else if (fuse_res) {   // 1-D: residual rows + the wave-edge terms [2][T][nx/64]
+      if ((rc = alloc(&p.res, (size_t)T * npl))) return rc;
+      if ((rc = alloc(&p.ex, (size_t)2 * T * (nx / 64)))) return rc;
     }
     // the task-order spectrum reuses the fused residual's R plane: a task's spectrum run [x0 rows, all ky] is exactly
     // the region its R rows occupy, and the residual kernel holds those rows in registers before it stores the run
@@ -1469,7 +1480,9 @@ struct Impl : ImplBase {
           else if (f16_group == 8) hipLaunchKernelGGL((k_f16a_fwd_1d<E, 8, R>), ga, dim3(256), 0, stream, p, twx, Y);
           else hipLaunchKernelGGL((k_f16a_fwd_1d<E, 16, R>), ga, dim3(256), 0, stream, p, twx, Y);
         };
-        if (pb.egno == 1) fwd(std::integral_constant<int, 1>{});
+        if (fuse_res && res_valid)   // the residual rows the last dual sweep formed (k_dual_1d_fr)
+          hipLaunchKernelGGL((k_f16a_fwd_fr_1d<R>), ga, dim3(256), 0, stream, p, twx, Y, jchunk_1d);
+        else if (pb.egno == 1) fwd(std::integral_constant<int, 1>{});
         else fwd(std::integral_constant<int, 2>{});
         if ((rc = ensure_lds(k_f16b_fwd_1d<R>, ldsb))) return rc;
         hipLaunchKernelGGL(k_f16b_fwd_1d<R>, dim3(8, npairs), dim3(512), ldsb, stream, p, twx, Y);
@@ -1587,14 +1600,24 @@ struct Impl : ImplBase {
             case 2: hipLaunchKernelGGL((k_dual_2d<R, 2>), g, dim3(256), 0, stream, p); break;
             default: hipLaunchKernelGGL((k_dual_2d<R, 3>), g, dim3(256), 0, stream, p); break;
           }
+        } else if (fuse_res && p.inplace) {   // the sweep also forms the next residual (k_dual_1d_fr)
+          const dim3 gf(pb.nx / 256, gz_1d);
+          if (pb.egno == 1)
+            hipLaunchKernelGGL((k_dual_1d_fr<R, 1>), gf, dim3(256), 0, stream, p, jchunk_1d);
+          else
+            hipLaunchKernelGGL((k_dual_1d_fr<R, 2>), gf, dim3(256), 0, stream, p, jchunk_1d);
+          res_valid = true;
         } else {
+          res_valid = false;
           if (pb.egno == 1)
             hipLaunchKernelGGL((k_dual_1d<R, 1>), g, dim3(256), 0, stream, p);
           else
             hipLaunchKernelGGL((k_dual_1d<R, 2>), g, dim3(256), 0, stream, p);
         }
       }
-      const int nrows_d = (pb.ndim == 2 && fast_dual) ? gxd * gyd * gzd : gx5 * g5;
+      const int nrows_d = (pb.ndim == 2 && fast_dual) ? gxd * gyd * gzd
+                                                      : (pb.ndim == 1 && fuse_res && p.inplace) ? (pb.nx / 256) * gz_1d
+                                                                                                : gx5 * g5;
       const double* rows = p.partials;
       int nrows = nrows_d;
       if (nrows_d > 2 * kFoldRows * 16) {   // one workgroup reading ~1 MiB of rows took 45-65 us at C1 / C3
@@ -2383,7 +2406,7 @@ struct Impl : ImplBase {
     }
     // fused residual: the dual also writes the residual rows (+1), the tile-edge row terms (2 rows per 8)
     // and the strip-edge column terms (2 per 256); the residual kernel reads them and writes the spectrum
-    const double edge = fuse_res ? 2.0 / 8.0 + 2.0 / (64.0 * dual_ypl) : 0.0;
+    const double edge = !fuse_res ? 0.0 : d2 ? 2.0 / 8.0 + 2.0 / (64.0 * dual_ypl) : 2.0 / 64.0;   // 1-D: per wave
     if (cls == "dual") return S * N * (1.0 + 2.0 * nr + (fuse_res ? 1.0 + edge : 0.0));
     if (cls == "residual") return S * N * (fuse_res ? 2.0 + edge : nr + 1.0);
     if (cls == "precond") return S * N * (d2 ? 4.0 : 2.0);   // 2-D: x-DHT+Thomas fwd (2N) + bwd+x-DHT (2N)

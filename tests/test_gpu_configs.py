@@ -78,7 +78,7 @@ CASES = {
     # the fused residual at ny = 8192: 4-row half-tile tasks of the 8-row sweep (k_res_fwdy_fused_2d<.., 8192, 4, 512>)
     "c4_rows_ny8192@fr": ({"PDHG_FUSE_RES": "1", "PDHG_SHORT_T": "0"}, {"rows_rw": 4, "fused_residual": 1,
                                                                         "res_threads": 512, "fast_dual": 8}),
-    "c1_exact": ({}, {"fourstep": 1, "glb_line": 1, "thomas_chunk": 1, "fs16": 1, "fs_wide": 0}),
+    "c1_exact": ({}, {"fourstep": 1, "glb_line": 1, "thomas_chunk": 1, "fs16": 1, "fs_wide": 0, "fused_residual": 1}),
     "c1_exact@wide": ({"PDHG_FS16": "0"}, {"fourstep": 1, "fs16": 0, "fs_wide": 1}),
     "c1_exact@tile16": ({"PDHG_FS16": "0", "PDHG_FS_WIDE": "0"}, {"fourstep": 1, "fs16": 0, "fs_wide": 0}),
     "c1_exact@thomas1": ({"PDHG_THOMAS_CHUNK": "0"}, {"fourstep": 1, "fs16": 1, "thomas_chunk": 0}),
