@@ -429,7 +429,7 @@ __global__ void __launch_bounds__(256) k_dual_1d_fr(KP<R> p, int jchunk) {
 // terms (p.ex) and, on a chunk's last row, the time difference (rho_{j+1} - rho_j)/dt from the state; then the same
 // 16-point DFT over n1, twiddles and Y layout as k_f16a_fwd_1d.  grid (4096/256, pairs); block 256.
 template <typename R = float>
-__global__ void __launch_bounds__(256) k_f16a_fwd_fr_1d(KP<R> p, const cplx<R>* __restrict__ twN, cplx<R>* __restrict__ Y,
+__global__ void __launch_bounds__(256) k_f16a_fwd_fused_1d(KP<R> p, const cplx<R>* __restrict__ twN, cplx<R>* __restrict__ Y,
                                                         int jchunk) {
   using C = cplx<R>;
   if (p.ctrl->done) return;

@@ -551,10 +551,12 @@ struct Impl : ImplBase {
       // chunked t-solve: one wave per 32-row chunk of 64 modes (T <= 512, Ct != 0)
       thomas_chunk = pb.Ct != 0.0 && T <= 16 * 32;
       // fused 1-D residual (C1's 16 x 4096 path, rho_alp_iters = 1, periodic x): the dual sweep forms the residual
-      // rows (k_dual_1d_fr), stage A reads them (k_f16a_fwd_fr_1d); 8 time chunks of the sweep
+      // rows (k_dual_1d_fr), stage A reads them (k_f16a_fwd_fused_1d); 8 time chunks of the sweep
       fuse_res = fs16 && pb.bc_x == 0 && !two_sets && pb.egno != 3 && nx % 256 == 0;
       if (const char* e = getenv("PDHG_FUSE_RES1D")) fuse_res = fuse_res && atoi(e) != 0;   // A/B: 0 = unfused
-      gz_1d = std::min(8, T);
+      gz_1d = 8;
+      if (const char* e = getenv("PDHG_FR1D_CHUNKS")) gz_1d = std::max(1, std::min(32, atoi(e)));   // tuning
+      gz_1d = std::min(gz_1d, T);
       jchunk_1d = (T + gz_1d - 1) / gz_1d;
       gz_1d = (T + jchunk_1d - 1) / jchunk_1d;
       if (const char* e = getenv("PDHG_THOMAS_CHUNK")) thomas_chunk = thomas_chunk && atoi(e) != 0;   // override
@@ -1481,7 +1483,7 @@ struct Impl : ImplBase {
           else hipLaunchKernelGGL((k_f16a_fwd_1d<E, 16, R>), ga, dim3(256), 0, stream, p, twx, Y);
         };
         if (fuse_res && res_valid)   // the residual rows the last dual sweep formed (k_dual_1d_fr)
-          hipLaunchKernelGGL((k_f16a_fwd_fr_1d<R>), ga, dim3(256), 0, stream, p, twx, Y, jchunk_1d);
+          hipLaunchKernelGGL((k_f16a_fwd_fused_1d<R>), ga, dim3(256), 0, stream, p, twx, Y, jchunk_1d);
         else if (pb.egno == 1) fwd(std::integral_constant<int, 1>{});
         else fwd(std::integral_constant<int, 2>{});
         if ((rc = ensure_lds(k_f16b_fwd_1d<R>, ldsb))) return rc;
