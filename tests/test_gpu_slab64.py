@@ -205,3 +205,49 @@ def test_fp64_slabs_task_order_spectrum(native, parity_log, monkeypatch):
     m = _metrics(st, st_ref, got, want)
     parity_log("test_fp64_slabs_task_order_spectrum", "e2_4096x4096_T8_P2", m, {key: TOL for key in m})
     assert all(v <= TOL for v in m.values()), m
+
+
+def test_fp64_slabs_c4_task_order(native, parity_log, monkeypatch):
+    """C4's task-order residual spectrum + transpose (to_c4) inside fp64 t-slabs: the fused residual's row-range
+    launches (interior rows, then the halo row) transpose their own rows.  C4's 8192^2 plane, 4 rows in 2 slabs,
+    epsl = 0.1, from the reference initial state with a seeded rough rho (no window-sized control arrays on the
+    host); against the single fp64 context with the same layout, 1e-11 (phi, rho, err1, err2)."""
+    import torch
+    from pdhg_amd.context import PDHGContext
+    from pdhg_amd.slab import LocalComm, SlabContext, SlabRunner, slab_bounds
+    monkeypatch.setenv("PDHG_FUSE_RES", "1")
+    monkeypatch.setenv("PDHG_SHORT_T", "0")
+    G = make_problem(2, 2, 8192, 8192, 1, 0.1, seeded=False)
+    T, nr, n = 4, 2, 4
+    dt = 1.0 / 40
+    g = G["g"][0]
+    rho = 70.0 * np.random.default_rng(13).uniform(0.5, 1.5, (T, 8192, 8192))
+    ref = PDHGContext(2, 2, 8192, 8192, T, G["dx"], G["dy"], dt, G["xs"], G["ys"], epsl=0.1, precision="fp64")
+    try:
+        assert ref.path_info("to_c4") == 1
+        ref.init_state(g)
+        ref.set_state(rho=rho)
+        st_ref = ref.iterate(n, TAU, SIGMA, -1.0, 1)
+        want = ref.get_state(alp=False)
+    finally:
+        ref.close()
+    slabs = [SlabContext(r, nr, T, 2, 8192, 8192, G["dx"], G["dy"], dt, G["xs"], G["ys"], epsl=0.1, precision="fp64")
+             for r in range(nr)]
+    try:
+        assert all(s.path_info("to_c4") == 1 for s in slabs)
+        for s, (j0, j1) in zip(slabs, slab_bounds(T, nr)):
+            s.init_state(g)
+            s.set_state(rho=rho[j0:j1])
+        st = SlabRunner(slabs, LocalComm(nr)).iterate(n, TAU, SIGMA, -1.0, 1)
+        torch.cuda.synchronize()
+        parts = [s.get_state(alp=False) for s in slabs]
+    finally:
+        for s in slabs:
+            s.close()
+    phi = np.concatenate([parts[0][0]] + [p[0][1:] for p in parts[1:]], axis=0)
+    rho_s = np.concatenate([p[1] for p in parts], axis=0)
+    m = {"phi": rel(phi, want[0]), "rho": rel(rho_s, want[1]),
+         "err1": abs(st["err1"] - st_ref["err1"]) / st_ref["err1"],
+         "err2": abs(st["err2"] - st_ref["err2"]) / st_ref["err2"]}
+    parity_log("test_fp64_slabs_c4_task_order", "e2_8192x8192_T4_P2_eps0.1", m, {k: TOL for k in m})
+    assert all(v <= TOL for v in m.values()), m
