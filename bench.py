@@ -42,6 +42,7 @@ CONFIGS = {
     "c1": (1, 1, 0.0, 65536, 1, 401),
     "c0": (1, 1, 0.0, 160, 1, 41),
     "c3w1": (2, 2, 0.1, 4096, 4096, 2),   # one T = 1 window of C3's grid (time_step_per_PDHG = 2 default)
+    "c2w1": (1, 2, 0.0, 2048, 2048, 2),   # one T = 1 window of C2's grid (the marching default's window)
     "c3w4": (2, 2, 0.1, 4096, 4096, 5),   # short windows of C3's grid (kernel-policy crossover)
     "c3w8": (2, 2, 0.1, 4096, 4096, 9),
     # one GPU's share of the 8-GPU t-slab runs as a window of its own (C3: 200 / 8 rows, C4: 400 / 8 rows; the

@@ -1260,8 +1260,11 @@ __global__ void __launch_bounds__(512) k_precond_xt_ws_2d(KP<float> p, const flo
 // computed; every load reads a valid address (rows outside a Dirichlet edge are clamped, then
 // zeroed by a select), so nothing drains the load queue.  y neighbours come from the adjacent
 // lanes (DPP), the wave-edge ones from uniform loads.  Sums as in k_dual_2d (double per point).
-template <int EGNO, typename R = float>
-__global__ void __launch_bounds__(256) k_dual_fast_2d(KP<R> p, int jchunk, int jbase, int jend, int zbase) {
+// ONE: every workgroup has exactly one time row (jchunk == 1, e.g. the T = 1 marching windows): the row is loaded
+// once, with no prefetch registers (the marching form re-loads its last row to stay branch-free), the same arithmetic.
+// ONE = 2: the same with 4 waves per SIMD asked of the compiler (fp64: 128 VGPRs + 28 B of spill, A/B only).
+template <int EGNO, typename R = float, int ONE = 0>
+__global__ void __launch_bounds__(256, ONE == 2 ? 4 : 1) k_dual_fast_2d(KP<R> p, int jchunk, int jbase, int jend, int zbase) {
   using V = V4<R>;
   if (p.ctrl->done || p.ctrl->inner_done) return;
   constexpr int NA = (EGNO == 3) ? 2 : 4;
@@ -1318,11 +1321,7 @@ __global__ void __launch_bounds__(256) k_dual_fast_2d(KP<R> p, int jchunk, int j
       return in;
     };
     V f0 = ld4(p.phibar + (size_t)j0 * plane + rxc + y);   // phi_bar row j
-    In nxt = load(j0);
-#pragma unroll 1
-    for (int j = j0; j < j1; ++j) {
-      const In in = nxt;
-      nxt = load(min(j + 1, j1 - 1));   // (the last step reloads its own row: keeps the loop branch-free)
+    auto step = [&](int j, const In& in) {
       const V pm = zxm ? z4r<R>() : in.pm, pp = zxp ? z4r<R>() : in.pp, pc = in.pc;
       const R pyl = lane_from_prev(pc.w, zym ? (R)0 : in.el);
       const R pyr = lane_from_next(pc.x, zyp ? (R)0 : in.er);
@@ -1361,6 +1360,17 @@ __global__ void __launch_bounds__(256) k_dual_fast_2d(KP<R> p, int jchunk, int j
         for (int a = 0; a < NA; ++a) st4(ad[a] + o, an4[a]);
       }
       f0 = pc;
+    };
+    if constexpr (ONE) {   // one row per workgroup: no next-row prefetch (half the input registers)
+      step(j0, load(j0));
+    } else {
+      In nxt = load(j0);
+#pragma unroll 1
+      for (int j = j0; j < j1; ++j) {
+        const In in = nxt;
+        nxt = load(min(j + 1, j1 - 1));   // (the last step reloads its own row: keeps the loop branch-free)
+        step(j, in);
+      }
     }
   }
   block_reduce_store<NS>(s, p.partials, ((zbase + (int)blockIdx.z) * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x);

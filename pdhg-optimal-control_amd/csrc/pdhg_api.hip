@@ -149,6 +149,7 @@ struct Impl : ImplBase {
   static constexpr int kMultiSub = 5;     // sub-iterations one chunk pass runs
   int NTd = 256, gxd = 0, gyd = 0, gzd = 0, jchunk_d = 1;
   int dual_rx = 0;   // > 0: k_dual_lds_2d with dual_rx x rows per workgroup (x neighbours through LDS)
+  int dual_one = 1;   // row-per-thread dual with one time row per workgroup: k_dual_fast_2d<.., ONE> (no prefetch)
   int dual_ypl = 4;  // y per lane of k_dual_lds_2d (fp64: 4 or 2)
   // fused residual: the dual sweep also forms the next primal's residual rows (k_dual_lds_2d FR), the
   // residual kernel only completes the tile-edge terms and transforms (k_res_fwdy_fused_2d)
@@ -434,6 +435,7 @@ struct Impl : ImplBase {
         }
         if (const char* e = getenv("PDHG_DUAL_YPL"))   // tuning: fp64 LDS dual with 2 y per lane
           if (sizeof(R) == 8 && dual_rx == 8 && atoi(e) == 2) dual_ypl = 2;
+        if (const char* e = getenv("PDHG_DUAL_ONE")) dual_one = atoi(e);   // A/B: 0 marching form, 2 (fp64) 4 waves/SIMD
         NTd = dual_rx ? dual_rx * 64 : std::min(256, ny / 4);
         gxd = dual_rx ? nx / dual_rx : nx;
         gyd = dual_rx ? ny / (64 * dual_ypl) : (ny / 4 + NTd - 1) / NTd;
@@ -1522,7 +1524,11 @@ struct Impl : ImplBase {
         case 4: hipLaunchKernelGGL((k_dual_lds_2d<EGNO, 4>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase); break;
         case 8: hipLaunchKernelGGL((k_dual_lds_2d<EGNO, 8>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase); break;
         case 16: hipLaunchKernelGGL((k_dual_lds_2d<EGNO, 16>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase); break;
-        default: hipLaunchKernelGGL((k_dual_fast_2d<EGNO>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase);
+        default:
+          if (jchunk_d == 1 && dual_one)
+            hipLaunchKernelGGL((k_dual_fast_2d<EGNO, float, 1>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase);
+          else
+            hipLaunchKernelGGL((k_dual_fast_2d<EGNO>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase);
       }
     } else {
       const dim3 g(gxd, gyd, gz);
@@ -1539,6 +1545,10 @@ struct Impl : ImplBase {
         hipLaunchKernelGGL((k_dual_lds_2d<EGNO, 8, false, double, 2>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase);
       else if (dual_rx == 8)
         hipLaunchKernelGGL((k_dual_lds_2d<EGNO, 8, false, double>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase);
+      else if (jchunk_d == 1 && dual_one == 2)
+        hipLaunchKernelGGL((k_dual_fast_2d<EGNO, double, 2>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase);
+      else if (jchunk_d == 1 && dual_one)
+        hipLaunchKernelGGL((k_dual_fast_2d<EGNO, double, 1>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase);
       else
         hipLaunchKernelGGL((k_dual_fast_2d<EGNO, double>), g, dim3(NTd), 0, stream, p, jchunk_d, lo, hi, zbase);
     }
@@ -2645,6 +2655,7 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
     else if (k == "dual64") *value = (sizeof(typename std::remove_reference<decltype(im)>::type::Real) == 8 && im.fast_dual) ? 1 : 0;
     else if (k == "fast_dual") *value = im.fast_dual ? im.dual_rx : -1;
     else if (k == "dual_ypl") *value = im.fast_dual && im.dual_rx ? im.dual_ypl : 0;
+    else if (k == "dual_one") *value = (im.fast_dual && !im.dual_rx && im.jchunk_d == 1 && im.dual_one) ? 1 : 0;
     else if (k == "fast_xt")
       *value = im.fast_xt ? (im.half_real && im.xt_dma_hr ? 5 : im.batch_xt && !im.half_real
                                                                     ? (im.xt_dma && im.pb.nx == 4096 ? 4 : 3)

@@ -579,7 +579,8 @@ def _march(monkeypatch, env, n=None, windows=None):
                                70.0, time_step_per_PDHG=2, epsl=F["epsl"], stepsz_param=F["stepsz"], fv=fv,
                                n_ctrl=ndim, N_maxiter=1000000, print_freq=1000000, eps=F["eps"], verbose=False,
                                stats=stats)
-    spec = {key: sum(c.path_info(key) for c in U._CACHE.values()) for key in ("spec", "spec_iters", "spec_halts")}
+    spec = {key: sum(c.path_info(key) for c in U._CACHE.values())
+            for key in ("spec", "spec_iters", "spec_halts", "dual_one")}
     U.clear_cache()
     return [int(st["window_iters"]) for st in stats], res[0], spec
 
@@ -603,6 +604,22 @@ def test_speculative_schedule_bitwise(native, monkeypatch, parity_log):
     assert it1 == it0 == itf
     assert r1[0] == r0[0] == rf[0]
     for a, b, c in zip(r1[1:], r0[1:], rf[1:]):
+        assert np.array_equal(a, b) and np.array_equal(c, b)
+
+
+def test_dual_one_row_bitwise(native, monkeypatch, parity_log):
+    """The row-per-thread dual's one-row form (k_dual_fast_2d<.., ONE>: every workgroup one time row, as in the T = 1
+    marching windows; loaded once, no prefetch registers) against its marching form (PDHG_DUAL_ONE=0) and the
+    4-waves-per-SIMD build (=2) on the marching fixture at 256^2 (the row-per-thread dual needs ny % 256 == 0), its
+    first 3 windows: the same stop counts, back-offs and final state bit for bit (same arithmetic per point)."""
+    it1, r1, sp1 = _march(monkeypatch, {"PDHG_DUAL_ONE": "1"}, 256, 3)
+    it2, r2, sp2 = _march(monkeypatch, {"PDHG_DUAL_ONE": "2"}, 256, 3)
+    it0, r0, sp0 = _march(monkeypatch, {"PDHG_DUAL_ONE": "0"}, 256, 3)
+    parity_log("test_dual_one_row_bitwise", "marching_c2dt_256_w3", {"dual_one": sp1["dual_one"]}, {}, iters=it1)
+    assert sp1["dual_one"] > 0 and sp2["dual_one"] > 0 and sp0["dual_one"] == 0, (sp1, sp2, sp0)
+    assert it1 == it0 == it2
+    assert r1[0] == r0[0] == r2[0]
+    for a, b, c in zip(r1[1:], r0[1:], r2[1:]):
         assert np.array_equal(a, b) and np.array_equal(c, b)
 
 
