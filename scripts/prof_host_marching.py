@@ -18,3 +18,4 @@ finally:
     pr.disable()
     st = pstats.Stats(pr)
     st.sort_stats("tottime").print_stats(25)
+    st.sort_stats("cumulative").print_stats(30)
