@@ -318,7 +318,9 @@ __host__ __device__ constexpr int twlds_size(int n) {
   return 3 * ((n > 16 ? 16 : 0) + (n > 256 ? 256 : 0) + (n > 4096 ? 4096 : 0));
 }
 
-template <typename C, int N, int NL, int NT, int LS, int R, bool REG, int LINE = Pad<N>::LINE>
+// GLS: passes with LS >= GLS read their seeds from the global table tw (W_N) instead of twl -- the same values
+// fill_twlds copies, so the transform is bitwise the same; only the LS < GLS segments of TwLds need LDS.
+template <typename C, int N, int NL, int NT, int LS, int R, bool REG, int LINE = Pad<N>::LINE, int GLS = (1 << 30)>
 __device__ __forceinline__ void inplace_pass(C* __restrict__ a, const C* __restrict__ tw, const C* twl) {
   constexpr int nR = N / R;
   constexpr int tws = N / (LS * R);
@@ -343,13 +345,17 @@ __device__ __forceinline__ void inplace_pass(C* __restrict__ a, const C* __restr
           // fp64: W^r = (W^4k)^(r>>2 part) (W^k)^(r&3) applied row by row of the 4 x 4 split, so at most the three
           // low powers and one high factor are live (the full w[16] table is 60 VGPRs next to 64 of values)
           const C* t3 = twl + twlds_off(LS) + 3 * k;
-          const C w1 = t3[0], w2 = cmul(w1, w1), w3 = cmul(w2, w1);
+          auto sd = [&](int m) -> C {   // seed m of k: W^(k tws), W^(4 k tws), W^(8 k tws)
+            if constexpr (LS >= GLS) return tw[((m == 0 ? 1 : m == 1 ? 4 : 8) * k * tws) & (N - 1)];
+            else return t3[m];
+          };
+          const C w1 = sd(0), w2 = cmul(w1, w1), w3 = cmul(w2, w1);
 #pragma unroll
           for (int h = 0; h < 4; ++h) {
             C H;
-            if (h == 1) H = t3[1];
-            else if (h == 2) H = t3[2];
-            else if (h == 3) H = cmul(t3[1], t3[2]);
+            if (h == 1) H = sd(1);
+            else if (h == 2) H = sd(2);
+            else if (h == 3) H = cmul(sd(1), sd(2));
             if (h > 0) v[q][4 * h] = cmul(v[q][4 * h], H);
             v[q][4 * h + 1] = cmul(v[q][4 * h + 1], h > 0 ? cmul(H, w1) : w1);
             v[q][4 * h + 2] = cmul(v[q][4 * h + 2], h > 0 ? cmul(H, w2) : w2);
@@ -361,21 +367,28 @@ __device__ __forceinline__ void inplace_pass(C* __restrict__ a, const C* __restr
         C w[R];
         if constexpr (REG) {
           const C* t3 = twl + twlds_off(LS) + 3 * k;
-          w[1] = t3[0];
+          auto sd = [&](int m) -> C {
+            if constexpr (LS >= GLS) return tw[((m == 0 ? 1 : m == 1 ? 4 : 8) * k * tws) & (N - 1)];
+            else return t3[m];
+          };
+          const C s0 = sd(0);
+          w[1] = s0;
           if constexpr (R > 2) {
-            w[2] = cmul(t3[0], t3[0]);
-            w[3] = cmul(w[2], t3[0]);
+            w[2] = cmul(s0, s0);
+            w[3] = cmul(w[2], s0);
           }
           if constexpr (R > 4) {
-            w[4] = t3[1];
-            w[5] = cmul(t3[1], t3[0]);
-            w[6] = cmul(t3[1], w[2]);
-            w[7] = cmul(t3[1], w[3]);
+            const C s1 = sd(1);
+            w[4] = s1;
+            w[5] = cmul(s1, s0);
+            w[6] = cmul(s1, w[2]);
+            w[7] = cmul(s1, w[3]);
           }
           if constexpr (R > 8) {
-            w[8] = t3[2];
+            const C s2 = sd(2);
+            w[8] = s2;
 #pragma unroll
-            for (int r = 1; r < 8; ++r) w[8 + r] = cmul(t3[2], w[r]);
+            for (int r = 1; r < 8; ++r) w[8 + r] = cmul(s2, w[r]);
           }
         } else {
           twiddles_from3<C, R>(w, tw, k * tws);
@@ -399,13 +412,13 @@ __device__ __forceinline__ void inplace_pass(C* __restrict__ a, const C* __restr
   lds_sync();
 }
 
-template <typename C, int N, int NL, int NT, int LS, bool REG, int LINE = Pad<N>::LINE>
+template <typename C, int N, int NL, int NT, int LS, bool REG, int LINE = Pad<N>::LINE, int GLS = (1 << 30)>
 __device__ __forceinline__ void inplace_passes(C* a, const C* __restrict__ tw, const C* twl) {
   if constexpr (LS < N) {
     constexpr int rem = N / LS;
     constexpr int R = (rem >= 16) ? 16 : rem;
-    inplace_pass<C, N, NL, NT, LS, R, REG, LINE>(a, tw, twl);
-    inplace_passes<C, N, NL, NT, LS * R, REG, LINE>(a, tw, twl);
+    inplace_pass<C, N, NL, NT, LS, R, REG, LINE, GLS>(a, tw, twl);
+    inplace_passes<C, N, NL, NT, LS * R, REG, LINE, GLS>(a, tw, twl);
   }
 }
 
@@ -421,11 +434,19 @@ __device__ __forceinline__ void lds_fft_inplace_tl(C* a, const C* twl) {
   inplace_passes<C, N, NL, NT, 1, true, LINE>(a, nullptr, twl);
 }
 
+// The same with only the LS = 16 pass's 48 seeds in LDS (twl) and the later passes' seeds read from the global
+// table tw (W_N): bitwise the same transform in 768 B of seed LDS instead of TwLds<N>::SIZE * 16.
+template <typename C, int N, int NL, int NT, int LINE = Pad<N>::LINE>
+__device__ __forceinline__ void lds_fft_inplace_tl16(C* a, const C* twl, const C* __restrict__ tw) {
+  inplace_passes<C, N, NL, NT, 1, true, LINE, 256>(a, tw, twl);
+}
+
 
 // Fill the TwLds<N> table from the global twiddle table (W_N^m at tw[m]); caller syncs before use.
 template <typename C, int N>
-__device__ __forceinline__ void fill_twlds(C* twl, const C* __restrict__ tw, int tw_stride = 1) {
-  for (int i = threadIdx.x; i < TwLds<N>::SIZE; i += blockDim.x) {
+__device__ __forceinline__ void fill_twlds(C* twl, const C* __restrict__ tw, int tw_stride = 1,
+                                           int cnt = TwLds<N>::SIZE) {   // cnt = 48: the LS = 16 segment only
+  for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
     const int LS = i >= 816 ? 4096 : i >= 48 ? 256 : 16;
     const int e = i - twlds_off(LS);
     const int k = e / 3, m = e - 3 * k;

@@ -905,7 +905,10 @@ __global__ void __launch_bounds__(NT) k_precond_xt_fast_2d(KP<float> p, const fl
 // (fp32: 41 KiB at N = 4096, N * NL = 4096; fp64: N * NL = 2048, or N = 4096 with NL = 1, the column pair of
 // k_precond_xt_f64_2d).  HIP's second __launch_bounds__ argument is the minimum waves per SIMD: 4 keeps the
 // kernel at <= 128 VGPRs, so two 512-thread (four 256-thread) workgroups fit a CU.
-template <int N, int NL, int NT, typename R = float>
+// G16: only the LS = 16 pass's seeds in LDS, the later passes' from twx (bitwise the same transform): fp64 N = 2048
+// drops 46.75 -> 34.75 KiB of LDS, so four 256-thread workgroups fit a CU instead of three (1024 column pairs at C2:
+// one round of 4 per CU instead of 1.33 rounds of 3).
+template <int N, int NL, int NT, typename R = float, bool G16 = false>
 __global__ void __launch_bounds__(NT, 4) k_precond_x_t1_2d(KP<R> p, const cplx<R>* __restrict__ twx) {
   using C = cplx<R>;
   constexpr int IT = N * NL / NT;
@@ -917,7 +920,11 @@ __global__ void __launch_bounds__(NT, 4) k_precond_x_t1_2d(KP<R> p, const cplx<R
   extern __shared__ __align__(16) unsigned char smem_raw[];
   C* A = reinterpret_cast<C*>(smem_raw);
   C* twl = A + NL * LINE;
-  fill_twlds<C, N>(twl, twx);
+  fill_twlds<C, N>(twl, twx, 1, G16 ? 48 : TwLds<N>::SIZE);
+  auto fft = [&]() {
+    if constexpr (G16) lds_fft_inplace_tl16<C, N, NL, NT>(A, twl, twx);
+    else lds_fft_inplace_tl<C, N, NL, NT>(A, twl);
+  };
   const int tid = threadIdx.x;
   const int b = blockIdx.x + p.b0;
   constexpr int M = N * B;
@@ -931,7 +938,7 @@ __global__ void __launch_bounds__(NT, 4) k_precond_x_t1_2d(KP<R> p, const cplx<R
     A[(item & (NL - 1)) * LINE + pix(item >> lnl)] = v[i];
   }
   lds_sync();
-  lds_fft_inplace_tl<C, N, NL, NT>(A, twl);
+  fft();
   const R inv_ae = (R)1 / p.ae;
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
@@ -950,7 +957,7 @@ __global__ void __launch_bounds__(NT, 4) k_precond_x_t1_2d(KP<R> p, const cplx<R
     A[(item & (NL - 1)) * LINE + pix(item >> lnl)] = v[i];
   }
   lds_sync();
-  lds_fft_inplace_tl<C, N, NL, NT>(A, twl);
+  fft();
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
     const int item = tid + i * NT;

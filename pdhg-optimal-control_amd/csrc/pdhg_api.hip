@@ -176,6 +176,10 @@ struct Impl : ImplBase {
   bool xt_dma = false;            // x transform with the rows staged HBM -> LDS by DMA (k_precond_xt_dma_2d)
   bool xt_dma_hr = false;         // ... its half-real form at nx = 8192 (C4)
   bool t1_xt64 = false;           // fp64 T = 1 windows: k_precond_x_t1_2d<..., double> (shares PDHG_T1_XT)
+  // fp64 unfused residual's threads at ny = 2048: 256 on one-row windows (two 4-wave workgroups per CU, 225 VGPRs;
+  // C2's T = 1 residual 54 -> 47 us), 512 otherwise (C2's T = 100 unfused residual 4.66 vs 4.94 ms at 256)
+  int res64_nt2048 = 512;
+  bool t1_g16 = true;             // ... with the later passes' twiddle seeds from global memory (PDHG_T1_G16=0: all in LDS)
   bool f64_xt = false;            // fp64 nx = 4096: in-place line + register carries (k_precond_xt_f64_2d)
   int xt64_var = 0;               // nx = 2048 shape of it (threads, b' in registers or LDS)
   bool thomas_chunk = false;      // 1-D: t-solve in chunks of 32 rows (k_thomas_chunk_1d)
@@ -337,6 +341,9 @@ struct Impl : ImplBase {
       // fp64 one-row windows at a power-of-two nx: the carry-free transform needs only the padded lines
       t1_xt64 = sizeof(R) == 8 && T == 1 && pb.bc_x == 0 && !half_real && !slab && plx.pow2 &&
                 nxg >= 512 && nxg <= 4096 && nxg * (B / 2) == (nxg == 4096 ? 4096 : 2048);
+      if (const char* e = getenv("PDHG_T1_G16")) t1_g16 = atoi(e) != 0;   // A/B: the T = 1 x kernel's seed table
+      res64_nt2048 = T == 1 ? 256 : 512;
+      if (const char* e = getenv("PDHG_RES64_NT2048")) res64_nt2048 = atoi(e) == 256 ? 256 : 512;   // A/B
       if (!half_real && !f64_xt && (size_t)nxg * B > cap)
         return fail(PDHG_ERR_UNSUPPORTED, "nx=%d too large for the x-transform slab (max %zu in this precision)", nxg,
                     cap / 2);
@@ -977,8 +984,9 @@ struct Impl : ImplBase {
         ProfScope ps(this, "residual");
         p.row_base = lo;
         p.row_cnt = hi - lo;
-        auto go = [&](auto Nc) {
-          constexpr int N_ = decltype(Nc)::value, NT_ = 512;   // 1024 threads cap the fp64 rows at 128 VGPRs (spills)
+        auto go = [&](auto Nc, auto NTc) {
+          // 1024 threads cap the fp64 rows at 128 VGPRs (spills); ny = 2048 A/B: 256 threads (2 workgroups per CU)
+          constexpr int N_ = decltype(Nc)::value, NT_ = decltype(NTc)::value;
           const dim3 g((pb.nx / 4) * (hi - lo));
           int r2;
           switch (pb.egno) {
@@ -997,7 +1005,10 @@ struct Impl : ImplBase {
           }
           return (int)PDHG_OK;
         };
-        rc = pb.ny == 4096 ? go(std::integral_constant<int, 4096>{}) : go(std::integral_constant<int, 2048>{});
+        using I = std::integral_constant<int, 512>;
+        rc = pb.ny == 4096 ? go(std::integral_constant<int, 4096>{}, I{})
+             : res64_nt2048 == 256 ? go(std::integral_constant<int, 2048>{}, std::integral_constant<int, 256>{})
+                                   : go(std::integral_constant<int, 2048>{}, I{});
         if (rc) return rc;
         HIP_TRY(hipGetLastError());
         return PDHG_OK;
@@ -1107,12 +1118,15 @@ struct Impl : ImplBase {
       }
     }
     if constexpr (sizeof(R) == 8) {
-      // fp64 one-row window (the reference's marching default in its own precision): the carry-free x transform,
-      // four 256-thread workgroups per CU.  Measured (C2 marching, nx = 2048, B = 2): the generic kernel took
+      // fp64 one-row window (the reference's marching default in its own precision): the carry-free x transform.
+      // Measured (C2 marching, nx = 2048, B = 2): the generic kernel took
       // 156 us per launch, this one 28 us (67 MB read + 67 MB written: 4.8 TB/s)
       if (t1_xt64 && p.T == 1 && !p.slab && p.xt_phase == 0 && t1_xt) {
         ProfScope ps(this, "precond");
-        const size_t lds = (size_t)((p.B / 2) * (p.nx + p.nx / 16) + twlds_size(p.nx)) * sizeof(C);
+        // G16 (nx = 2048 / 4096, t1_g16): only the first twiddled pass's 48 seeds in LDS, so 4 (nx = 2048, 256
+        // threads) or 2 (nx = 4096, 512 threads) workgroups fit a CU instead of 3 / 1
+        const bool g16 = t1_g16 && (p.nx == 2048 || p.nx == 4096);
+        const size_t lds = (size_t)((p.B / 2) * (p.nx + p.nx / 16) + (g16 ? 48 : twlds_size(p.nx))) * sizeof(C);
         auto go = [&](auto kern, int nt) -> int {
           int r2;
           if ((r2 = ensure_lds(kern, lds))) return r2;
@@ -1120,8 +1134,14 @@ struct Impl : ImplBase {
           return (int)PDHG_OK;
         };
         switch (p.nx) {
-          case 4096: rc = go(k_precond_x_t1_2d<4096, 1, 512, double>, 512); break;
-          case 2048: rc = go(k_precond_x_t1_2d<2048, 1, 256, double>, 256); break;   // 512 threads: 28.06 vs 27.64 us
+          case 4096:
+            rc = g16 ? go(k_precond_x_t1_2d<4096, 1, 512, double, true>, 512)
+                     : go(k_precond_x_t1_2d<4096, 1, 512, double>, 512);
+            break;
+          case 2048:   // 512 threads: 28.06 vs 27.64 us (3 workgroups per CU by LDS)
+            rc = g16 ? go(k_precond_x_t1_2d<2048, 1, 256, double, true>, 256)
+                     : go(k_precond_x_t1_2d<2048, 1, 256, double>, 256);
+            break;
           case 1024: rc = go(k_precond_x_t1_2d<1024, 2, 512, double>, 512); break;
           case 512: rc = go(k_precond_x_t1_2d<512, 4, 512, double>, 512); break;
           default: rc = fail(PDHG_ERR_UNSUPPORTED, "no fp64 one-row x kernel for nx=%d", p.nx);
@@ -2655,6 +2675,8 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
     else if (k == "dual64") *value = (sizeof(typename std::remove_reference<decltype(im)>::type::Real) == 8 && im.fast_dual) ? 1 : 0;
     else if (k == "fast_dual") *value = im.fast_dual ? im.dual_rx : -1;
     else if (k == "dual_ypl") *value = im.fast_dual && im.dual_rx ? im.dual_ypl : 0;
+    else if (k == "res64_nt") *value = im.res64 ? (im.pb.ny == 2048 ? im.res64_nt2048 : 512) : 0;
+    else if (k == "t1_g16") *value = (im.t1_xt64 && im.t1_xt && im.t1_g16 && (im.pb.nx == 2048 || im.pb.nx == 4096)) ? 1 : 0;
     else if (k == "dual_one") *value = (im.fast_dual && !im.dual_rx && im.jchunk_d == 1 && im.dual_one) ? 1 : 0;
     else if (k == "fast_xt")
       *value = im.fast_xt ? (im.half_real && im.xt_dma_hr ? 5 : im.batch_xt && !im.half_real

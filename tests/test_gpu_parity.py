@@ -390,21 +390,28 @@ def test_t1_x_transform_fp32(native, case):
 @pytest.mark.parametrize("case", T1_FAST, ids=["e{}d{}_{}x{}_T{}_eps{}".format(*c) for c in T1_FAST])
 def test_t1_x_transform_fp64(native, monkeypatch, case):
     """The same one-row windows in the reference's precision: k_precond_x_t1_2d<..., double> vs the oracle (primal
-    U <= 1e-12, 10 iterations <= 1e-10) and vs the generic runtime-radix x kernel (PDHG_T1_XT=0) to rounding."""
+    U <= 1e-12, 10 iterations <= 1e-10) and vs the generic runtime-radix x kernel (PDHG_T1_XT=0) to rounding; at nx =
+    2048 / 4096 the default G16 form (later passes' twiddle seeds from global memory) bitwise against the all-LDS
+    seed table (PDHG_T1_G16=0)."""
     P = make_problem(*case, seeded=False)
     phi_o = _oracle_primal(P, P["phi"], P["rho"], P["alp"])
     out = []
-    for t1 in ("1", "0"):
+    g16 = case[2] in (2048, 4096)
+    for t1, g in (("1", "1"), ("0", "1"), ("1", "0")):
         monkeypatch.setenv("PDHG_T1_XT", t1)
+        monkeypatch.setenv("PDHG_T1_G16", g)
         ctx = device_ctx(P, "fp64")
         try:
             assert ctx.path_info("t1_xt64") == int(t1)
+            assert ctx.path_info("t1_g16") == int(t1 == "1" and g == "1" and g16)
             ctx.set_state(P["phi"], P["rho"], P["alp"])
             ctx.update_primal(TAU)
             out.append(ctx.get_state()[0])
         finally:
             ctx.close()
+    monkeypatch.setenv("PDHG_T1_G16", "1")
     assert rel(out[0], phi_o) < 1e-12 and rel(out[0], out[1]) < 1e-13
+    assert np.array_equal(out[0], out[2])
     phi_o, rho_o, _, e1_o, _ = _oracle_iterate(P, 10)
     monkeypatch.setenv("PDHG_T1_XT", "1")
     ctx = device_ctx(P, "fp64")

@@ -130,3 +130,25 @@ def test_dual64_matches_oracle(native, case, k, monkeypatch):
         if np.linalg.norm(a_o) > 0:
             assert rel(a_d, a_o) < 1e-10
     assert rel(rho_d, out["0"][0]) < 1e-12
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c[3] == 2048], ids=[i for c, i in zip(CASES, IDS) if c[3] == 2048])
+def test_res64_threads(native, case, monkeypatch, parity_log):
+    """ny = 2048: the residual's 256-thread workgroups (two per CU, each thread two y groups; the default on one-row
+    windows) against the 512-thread form (PDHG_RES64_NT2048): the same per-point expressions and transform, compiled
+    for a different thread mapping; phi' agrees to rounding (measured: not bit for bit; the difference is logged)."""
+    P = make_problem(*case)
+    out = []
+    for nt in ("256", "512"):
+        monkeypatch.setenv("PDHG_RES64_NT2048", nt)
+        ctx = device_ctx(P, "fp64")
+        try:
+            assert ctx.path_info("res64_nt") == int(nt)
+            ctx.set_state(P["phi"], P["rho"], P["alp"])
+            ctx.update_primal(TAU)
+            out.append(ctx.get_state()[0])
+        finally:
+            ctx.close()
+    parity_log("test_res64_threads", "_".join(map(str, case)), {"phi_256_vs_512": rel(out[0], out[1])},
+               {"phi_256_vs_512": 1e-13})
+    assert rel(out[0], out[1]) < 1e-13
