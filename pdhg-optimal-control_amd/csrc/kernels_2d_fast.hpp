@@ -559,7 +559,9 @@ __global__ void __launch_bounds__(256) k_res_fwdy_fused_transpose_2d(KP<R> p, in
 // G workgroups striding over the T * nx/RW row-group tasks; block NT; LDS RW/2 * (N + N/16) * 8 B.
 // sums: [0] sum (phi'-phi)^2, [1] sum phi^2 (old), [2] sum phi'^2
 // RW = 2 with B = 1 (fp64 at C4's ny = 8192 with the half-real x blocks): one line, 16-B chunks.
-template <int N, int RW, int NT, int PF = 1, typename R = float>
+// G16: only the first twiddled pass's seeds in LDS, the later passes' from twy (bitwise the same transform; fp64 ny = 2048
+// with 256 threads: 70.4 KiB of LDS, two workgroups per CU -- the one-row windows' update)
+template <int N, int RW, int NT, int PF = 1, typename R = float, bool G16 = false>
 __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<R> p, const cplx<R>* __restrict__ twy) {
   using C = cplx<R>;
   using V = V4<R>;
@@ -571,7 +573,7 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<R> p, const cplx<
   R* Af = reinterpret_cast<R*>(A);
   constexpr bool TWL = N <= 4096;   // twiddle seeds in LDS (see k_res_fwdy_fused_2d)
   C* twl = A + NL * Pad<N>::LINE;
-  if constexpr (TWL) fill_twlds<C, N>(twl, twy);
+  if constexpr (TWL) fill_twlds<C, N>(twl, twy, 1, G16 ? 48 : TwLds<N>::SIZE);
   const int nx = p.nx, B = p.B, nb = p.nb;
   const int ngx = nx / RW;
   const int ntask = ngx * p.T;
@@ -648,7 +650,8 @@ __global__ void __launch_bounds__(NT) k_invy_update_fast_2d(KP<R> p, const cplx<
     ldstep(0);
     lds_sync();
     if (!(p.dbg & 64)) {   // timing experiments only (PDHG_DBG): 64 skips the transform
-      if constexpr (TWL) lds_fft_inplace_tl<C, N, NL, NT, Pad<N>::LINE>(A, twl);
+      if constexpr (TWL && G16) lds_fft_inplace_tl16<C, N, NL, NT, Pad<N>::LINE>(A, twl, twy);
+      else if constexpr (TWL) lds_fft_inplace_tl<C, N, NL, NT, Pad<N>::LINE>(A, twl);
       else lds_fft_inplace<C, N, NL, NT>(A, twy);
     }
 #pragma unroll

@@ -179,6 +179,7 @@ struct Impl : ImplBase {
   // fp64 unfused residual's threads at ny = 2048: 256 on one-row windows (two 4-wave workgroups per CU, 225 VGPRs;
   // C2's T = 1 residual 54 -> 47 us), 512 otherwise (C2's T = 100 unfused residual 4.66 vs 4.94 ms at 256)
   int res64_nt2048 = 512;
+  int upd_t1 = 0;                 // fp64 ny = 2048 update on one-row windows: 256 threads + G16 seeds (2: PF 2, 1: PF 4)
   bool t1_g16 = true;             // ... with the later passes' twiddle seeds from global memory (PDHG_T1_G16=0: all in LDS)
   bool f64_xt = false;            // fp64 nx = 4096: in-place line + register carries (k_precond_xt_f64_2d)
   int xt64_var = 0;               // nx = 2048 shape of it (threads, b' in registers or LDS)
@@ -343,6 +344,8 @@ struct Impl : ImplBase {
                 nxg >= 512 && nxg <= 4096 && nxg * (B / 2) == (nxg == 4096 ? 4096 : 2048);
       if (const char* e = getenv("PDHG_T1_G16")) t1_g16 = atoi(e) != 0;   // A/B: the T = 1 x kernel's seed table
       res64_nt2048 = T == 1 ? 256 : 512;
+      upd_t1 = T == 1 ? 2 : 0;   // steady marching iteration 0.2196 (512 threads) / 0.2150 (PF 4) / 0.2131 ms (PF 2)
+      if (const char* e = getenv("PDHG_UPD_T1")) upd_t1 = T == 1 ? atoi(e) : 0;   // A/B: 0 = 512-thread update
       if (const char* e = getenv("PDHG_RES64_NT2048")) res64_nt2048 = atoi(e) == 256 ? 256 : 512;   // A/B
       if (!half_real && !f64_xt && (size_t)nxg * B > cap)
         return fail(PDHG_ERR_UNSUPPORTED, "nx=%d too large for the x-transform slab (max %zu in this precision)", nxg,
@@ -1306,8 +1309,20 @@ struct Impl : ImplBase {
             hipLaunchKernelGGL(kern, dim3(g_fast_upd), dim3(512), lds_upd64, stream, p, twy);
             return (int)PDHG_OK;
           };
-          rc = pb.ny == 4096 ? go(k_invy_update_fast_2d<4096, 4, 512, 4, double>)
-                             : go(k_invy_update_fast_2d<2048, 4, 512, 4, double>);
+          if (pb.ny == 2048 && upd_t1 > 0) {   // one-row windows: 256 threads, two workgroups per CU (G16 seeds)
+            const size_t lds = lds_res64 + (size_t)48 * sizeof(C);
+            auto go2 = [&](auto kern) {
+              int r3;
+              if ((r3 = ensure_lds(kern, lds))) return r3;
+              hipLaunchKernelGGL(kern, dim3(g_fast_upd), dim3(256), lds, stream, p, twy);
+              return (int)PDHG_OK;
+            };
+            rc = upd_t1 == 2 ? go2(k_invy_update_fast_2d<2048, 4, 256, 2, double, true>)
+                             : go2(k_invy_update_fast_2d<2048, 4, 256, 4, double, true>);
+          } else {
+            rc = pb.ny == 4096 ? go(k_invy_update_fast_2d<4096, 4, 512, 4, double>)
+                               : go(k_invy_update_fast_2d<2048, 4, 512, 4, double>);
+          }
           if (rc) return rc;
           upd_done = true;
         } else if (upd8192) {   // fp64 ny = 8192, half-real x blocks: 2-row tasks on one padded line
@@ -2676,6 +2691,7 @@ int pdhg_path_info(pdhg_ctx* ctx, const char* key, int* value) {
     else if (k == "fast_dual") *value = im.fast_dual ? im.dual_rx : -1;
     else if (k == "dual_ypl") *value = im.fast_dual && im.dual_rx ? im.dual_ypl : 0;
     else if (k == "res64_nt") *value = im.res64 ? (im.pb.ny == 2048 ? im.res64_nt2048 : 512) : 0;
+    else if (k == "upd_t1") *value = (im.res64 && im.pb.ny == 2048) ? im.upd_t1 : 0;
     else if (k == "t1_g16") *value = (im.t1_xt64 && im.t1_xt && im.t1_g16 && (im.pb.nx == 2048 || im.pb.nx == 4096)) ? 1 : 0;
     else if (k == "dual_one") *value = (im.fast_dual && !im.dual_rx && im.jchunk_d == 1 && im.dual_one) ? 1 : 0;
     else if (k == "fast_xt")

@@ -152,3 +152,32 @@ def test_res64_threads(native, case, monkeypatch, parity_log):
     parity_log("test_res64_threads", "_".join(map(str, case)), {"phi_256_vs_512": rel(out[0], out[1])},
                {"phi_256_vs_512": 1e-13})
     assert rel(out[0], out[1]) < 1e-13
+
+
+T1_CASES = [(1, 2, 8, 2048, 1, 0.0), (2, 2, 2048, 2048, 1, 0.1)]
+
+
+@pytest.mark.parametrize("case", T1_CASES, ids=["e{}_{}x{}_T1_eps{}".format(c[0], c[2], c[3], c[5]) for c in T1_CASES])
+def test_update_t1_shapes(native, case, monkeypatch, parity_log):
+    """One-row windows at ny = 2048: the update's 256-thread workgroups with the G16 seed table (two per CU; prefetch
+    depth 2 = default, 4) against the 512-thread form (PDHG_UPD_T1=0) -- phi' and phi_bar to rounding (the difference
+    is logged) -- and the primal against the fp64 oracle."""
+    P = make_problem(*case)
+    out = []
+    for v in ("1", "2", "0"):
+        monkeypatch.setenv("PDHG_UPD_T1", v)
+        ctx = device_ctx(P, "fp64")
+        try:
+            assert ctx.path_info("upd_t1") == int(v)
+            ctx.set_state(P["phi"], P["rho"], P["alp"])
+            ctx.update_primal(TAU)
+            out.append((ctx.get_state()[0], ctx.get_phi_bar()))
+        finally:
+            ctx.close()
+    phi_o = _primal(P)
+    d = {"v1_vs_512": rel(out[0][0], out[2][0]), "v2_vs_512": rel(out[1][0], out[2][0]),
+         "U_vs_oracle": rel((out[0][0] - P["phi"]) / TAU, (phi_o - P["phi"]) / TAU)}
+    parity_log("test_update_t1_shapes", "_".join(map(str, case)), d,
+               {"v1_vs_512": 1e-13, "v2_vs_512": 1e-13, "U_vs_oracle": 1e-10})
+    assert d["v1_vs_512"] < 1e-13 and d["v2_vs_512"] < 1e-13 and d["U_vs_oracle"] < 1e-10
+    assert rel(out[0][1], out[2][1]) < 1e-13
