@@ -206,15 +206,10 @@ __global__ void __launch_bounds__(256) k_outer_sums(KP<R> p, size_t n, int k1_sk
 // End of an outer iteration: err1, err2 (utils_pdhg_solver.py:58-68), stop tests (:74-80).
 // outer_rows > 0: reduce k_outer_sums partials first (k > 1); else use the sub-iteration-0 sums (also with k1_skip
 // when the dual loop ran one sub-iteration: k_outer_sums skipped).
-__global__ void __launch_bounds__(1024) k_finalize_outer(const double* partials, int outer_rows, int na, double eps,
-                                                        int flip, int stop_conv, int stop_nan, Ctrl* ctrl,
-                                                        int k1_skip = 0) {
-  if (ctrl->done) return;
-  __shared__ double out[kNumSums];
-  if (k1_skip && ctrl->inner_count == 1) outer_rows = 0;   // uniform: inner_count is not written below
-  if (outer_rows > 0) reduce_partials(partials, outer_rows, kNumSums, out);
-  if (threadIdx.x == 0) {
-    const double* os = (outer_rows > 0) ? out : ctrl->outer_sums;
+// thread 0's part (os: the outer sums)
+__device__ __forceinline__ void finalize_outer_sums(const double* os, int na, double eps, int flip, int stop_conv,
+                                                    int stop_nan, Ctrl* ctrl) {
+  {
     const double err1 = sqrt(ctrl->s_dphi) / sqrt(ctrl->s_phi_old);
     double err2 = sqrt(os[0]) / sqrt(os[2]);
     for (int a = 0; a < na; ++a) {
@@ -240,6 +235,44 @@ __global__ void __launch_bounds__(1024) k_finalize_outer(const double* partials,
     ctrl->kstar_found = 0;
     ctrl->primal_valid = 0;
   }
+}
+__global__ void __launch_bounds__(1024) k_finalize_outer(const double* partials, int outer_rows, int na, double eps,
+                                                        int flip, int stop_conv, int stop_nan, Ctrl* ctrl,
+                                                        int k1_skip = 0) {
+  if (ctrl->done) return;
+  __shared__ double out[kNumSums];
+  if (k1_skip && ctrl->inner_count == 1) outer_rows = 0;   // uniform: inner_count is not written below
+  if (outer_rows > 0) reduce_partials(partials, outer_rows, kNumSums, out);
+  if (threadIdx.x == 0) finalize_outer_sums((outer_rows > 0) ? out : ctrl->outer_sums, na, eps, flip, stop_conv,
+                                           stop_nan, ctrl);
+}
+
+// A speculative iteration's sub-iteration-0 finalize and its outer finalize in one launch (iterate()'s speculative
+// schedule, pdhg_api.hip): the two were adjacent launches there -- k_finalize_dual(spec) then k_finalize_outer with
+// the one-sub-iteration skip (inner_count == 1, sums from ctrl->outer_sums) -- and thread 0 runs both bodies in that
+// order, so the control block ends the same.  A loop that does not exit halts (done = kHaltTail) and the outer part
+// is not run, as k_finalize_outer returned at entry then.
+// prim_rows > 0: the iteration's primal finalize too (k_finalize_primal's reduction of the update's rows, first: a
+// halted iteration's outer tests, run later by the host, read its sums)
+__global__ void __launch_bounds__(1024) k_finalize_dual_outer(const double* prim_partials, int prim_rows,
+                                                             const double* partials, int nrows, int na, int n_dead,
+                                                             double eps, int flip, int stop_conv, int stop_nan,
+                                                             Ctrl* ctrl) {
+  if (ctrl->done || ctrl->inner_done) return;
+  __shared__ double out[kNumSums];
+  if (prim_rows > 0) {
+    reduce_partials(prim_partials, prim_rows, 3, out);
+    if (threadIdx.x == 0) {
+      const double row0_sq = ctrl->row0_sq;
+      ctrl->s_dphi = out[0];
+      ctrl->s_phi_old = out[1] + row0_sq;
+      ctrl->s_phi_new = out[2] + row0_sq;
+      ctrl->primal_valid = 1;
+    }
+  }
+  reduce_partials(partials, nrows, 3 + 3 * na, out);
+  finalize_dual_sums(out, na, n_dead, eps, 0, ctrl, 1);
+  if (threadIdx.x == 0 && ctrl->done == 0) finalize_outer_sums(ctrl->outer_sums, na, eps, flip, stop_conv, stop_nan, ctrl);
 }
 
 // ---- state initialisation / conversion ----

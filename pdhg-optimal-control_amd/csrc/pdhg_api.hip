@@ -143,6 +143,8 @@ struct Impl : ImplBase {
   bool fold_fin = false;
   bool dual_head = false;    // ... below 2^25 points: sub-iteration 0 alone, the rest in chunks (kernels_dual_multi.hpp)
   bool spec_ok = false;      // iterate() may use the speculative one-sub-iteration schedule (head form, PDHG_SPEC)
+  bool fin_merge = true;     // ... with its dual and outer finalizes in one launch (PDHG_FIN_MERGE=0: two)
+  bool outer_merged = false; // launch_dual merged this iteration's outer finalize: launch_outer skips it
   bool spec = false;         // ... and uses it now (launch_dual / launch_outer / the captured graph)
   long long spec_iters = 0, spec_halts = 0;   // iterations enqueued speculatively / halts (path_info, tests)
   bool dual_multi = false;   // rho_alp_iters > 1: the dual loop in chunks of sub-iterations (kernels_dual_multi.hpp)
@@ -198,6 +200,8 @@ struct Impl : ImplBase {
   size_t partial_rows = 0;
   static constexpr int kFoldRows = 64;   // rows of the first fold level (k_fold_partials) after the table
   double* fold_out = nullptr;
+  double* prim_partials = nullptr;   // the update's partial rows when the speculative finalize merges the primal's
+  int prim_merged_rows = 0;          // > 0: launch_primal left its finalize to k_finalize_dual_outer (rows to reduce)
   bool primal_done = false;
   int stop_conv = 1, stop_nan = 1;   // reference stop rules (utils_pdhg_solver.py:74-80)
   // profiling
@@ -594,6 +598,7 @@ struct Impl : ImplBase {
     // two-launch fold / finalize (the halt flag is set by k_finalize_dual)
     spec_ok = dual_head && k1_outer && !fold_fin;
     if (const char* e = getenv("PDHG_SPEC")) spec_ok = spec_ok && atoi(e) != 0;   // A/B, tests
+    if (const char* e = getenv("PDHG_FIN_MERGE")) fin_merge = atoi(e) != 0;        // A/B, tests
     partial_rows = std::max<size_t>({(size_t)gx4 * g4, (size_t)gx5 * g5, (size_t)g_outer, (size_t)g_fast_upd,
                                      (size_t)gxd * gyd * (gzd + 1), fourstep ? (size_t)9 * ((T + 1) / 2) : 1, 1,
                                      (dual_multi || dual_head) ? (size_t)kMultiSub * gxd * gyd * gzd : (size_t)1});
@@ -640,8 +645,11 @@ struct Impl : ImplBase {
       for (int a = 0; a < 4; ++a) p.alp[1][a] = p.alp[0][a];
     }
     for (int a = na; a < 4; ++a) p.alp[0][a] = p.alp[1][a] = nullptr;
-    if ((rc = alloc(&p.partials, (partial_rows + kFoldRows) * kNumSums))) return rc;
+    // rows: the kernels' partials, the fold's rows, and the update's partials of a speculative iteration (kept for the
+    // merged finalize: the dual reuses the first region)
+    if ((rc = alloc(&p.partials, (2 * partial_rows + kFoldRows) * kNumSums))) return rc;
     fold_out = p.partials + partial_rows * kNumSums;
+    prim_partials = fold_out + kFoldRows * kNumSums;
     if ((rc = alloc(&p.ctrl, 1))) return rc;
     if (glb_line) {   // 2 lines of nx complex per concurrent workgroup (gx1 >= gx4)
       C* g = nullptr;
@@ -1299,6 +1307,10 @@ struct Impl : ImplBase {
       }
       int upd_rows = gx4 * g4;
       bool upd_done = false;
+      // speculative schedule: the update's sums go to their own rows and k_finalize_dual_outer reduces them (the
+      // same rows in the same order as k_finalize_primal), one launch fewer
+      const bool prim_merge = spec && fin_merge && !dual_multi && !sums_out;
+      if (prim_merge) p.partials = prim_partials;
       if constexpr (sizeof(R) == 8) {
         if (res64) {
           ProfScope ps(this, "update");
@@ -1385,6 +1397,8 @@ struct Impl : ImplBase {
       if (sums_out)
         hipLaunchKernelGGL(k_reduce_vec, dim3(1), dim3(1024), 0, stream, p.partials, upd_rows, 3,
                            kp.j0 == 0 ? row0_sq : 0.0, sums_out);
+      else if (prim_merge)
+        prim_merged_rows = upd_rows;
       else
         hipLaunchKernelGGL(k_finalize_primal, dim3(1), dim3(1024), 0, stream, p.partials, upd_rows, 1, p.ctrl);
     } else {
@@ -1679,8 +1693,16 @@ struct Impl : ImplBase {
         rows = fold_out;
         nrows = kFoldRows;
       }
-      hipLaunchKernelGGL(k_finalize_dual, dim3(1), dim3(1024), 0, stream, rows, nrows, na, n_dead, eps, s, p.ctrl,
-                         (head && spec) ? 1 : 0);
+      if (head && spec && s == 0 && k > 1 && k1_outer && !dual_multi && fin_merge) {
+        // the speculative iteration's dual and outer finalizes in one launch; launch_outer then launches nothing
+        hipLaunchKernelGGL(k_finalize_dual_outer, dim3(1), dim3(1024), 0, stream, prim_partials, prim_merged_rows,
+                           rows, nrows, na, n_dead, eps, 1, stop_conv, stop_nan, p.ctrl);
+        prim_merged_rows = 0;
+        outer_merged = true;
+      } else {
+        hipLaunchKernelGGL(k_finalize_dual, dim3(1), dim3(1024), 0, stream, rows, nrows, na, n_dead, eps, s, p.ctrl,
+                           (head && spec) ? 1 : 0);
+      }
     }
     if (head && !spec) return launch_dual_tail(sigma, eps, k);   // spec: only when sub-iteration 0 did not exit
     HIP_TRY(hipGetLastError());
@@ -1702,6 +1724,10 @@ struct Impl : ImplBase {
   }
 
   int launch_outer(double eps, int k) {
+    if (outer_merged) {   // k_finalize_dual_outer ran it (speculative schedule)
+      outer_merged = false;
+      return PDHG_OK;
+    }
     KP<R> p = kp;
     int rows = 0;
     // the chunked dual loop keeps no sub-iteration-0 outer sums (its tables hold 2 + 2 na sums), so only the
