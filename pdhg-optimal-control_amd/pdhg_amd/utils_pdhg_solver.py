@@ -253,7 +253,7 @@ def PDHG_multi_step(fn_update_primal, fn_update_dual, fns_dict, g, x_arr, ndim, 
                 errs_all.append(errs)
                 phi0 = phi0 + (phi_c[-1:] - phi0[0:1])        # warm start, :201-203
                 rho0, alp0 = rho_c, alp_c
-                phi_end = phi0.copy()        # the next window's warm start, saved whole
+                phi_end = phi0               # the next window's warm start, saved whole (a new array, never written)
                 break
         if save_middle_dir is not None and save_middle_prefix is not None and phi_end is not None:
             save(save_middle_dir, save_middle_prefix,
